@@ -1,0 +1,170 @@
+"""Seeded synthetic SGUFP instances in the reference's text format.
+
+The reference reads instances with ``Network::Network(const std::string&)``
+(/root/reference/Network.cpp:10-129):
+
+    n m S
+    tail head  lb_0 ub_0 r_0  lb_1 ub_1 r_1 ...      (m lines, S triples each)
+    Vbar
+    id id id ...
+
+The generator follows SURVEY.md §8(d): a layered DAG with source 0, sink n-1
+and K middle layers of width W.  Every middle node gets ``d`` distinct random
+out-arcs into the next layer, uncovered next-layer nodes get one in-arc, layer 0
+is fed from the source and the last layer drains into the sink.  Random extra
+inter-layer arcs are added (or removable ones trimmed) until |E| matches.
+Each middle node is in V-bar with probability ``f``.  Per scenario
+ub ~ U{5..50}, lb = 0 except sink arcs (lb ~ U{1..3} w.p. 0.3); the reward
+r ~ U{-5..30} is the same for every scenario (the reference subproblem uses
+scenario-0 rewards, grb.cpp:53,71,89, while the extensive form uses per-scenario
+rewards, StochasticModel.h:57-58 -- scenario-invariant rewards make both agree).
+
+Parallel arcs are never generated: the dual LP indexes beta/gamma by node pair
+(grb.cpp:8-39), so parallel arcs would alias there.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import List, Tuple
+
+import numpy as np
+
+
+@dataclasses.dataclass(frozen=True)
+class InstanceConfig:
+    name: str
+    n_arcs: int
+    layers: int        # K middle layers
+    width: int         # W nodes per middle layer
+    out_degree: int    # d distinct out-arcs per middle node
+    vbar_prob: float   # f
+    scenarios: int     # S
+
+
+# SURVEY.md §8(d) configurations.
+CONFIGS = {
+    "C1": InstanceConfig("C1", 40, 3, 6, 2, 1.0, 1),
+    "C2": InstanceConfig("C2", 200, 6, 12, 3, 0.5, 1),
+    "C3": InstanceConfig("C3", 1000, 12, 30, 3, 0.3, 64),
+    "C4": InstanceConfig("C4", 1000, 12, 30, 3, 0.3, 256),
+    "C5": InstanceConfig("C5", 5000, 10, 165, 3, 0.08, 512),
+}
+
+
+@dataclasses.dataclass
+class Instance:
+    n: int
+    tails: np.ndarray      # int32 [m]
+    heads: np.ndarray      # int32 [m]
+    lb: np.ndarray         # int32 [m, S]
+    ub: np.ndarray         # int32 [m, S]
+    reward: np.ndarray     # int32 [m, S]
+    vbar: List[int]
+
+    @property
+    def m(self) -> int:
+        return int(self.tails.shape[0])
+
+    @property
+    def scenarios(self) -> int:
+        return int(self.lb.shape[1])
+
+    def to_text(self) -> str:
+        out = [f"{self.n} {self.m} {self.scenarios}"]
+        for a in range(self.m):
+            parts = [str(int(self.tails[a])), str(int(self.heads[a]))]
+            for s in range(self.scenarios):
+                parts += [str(int(self.lb[a, s])), str(int(self.ub[a, s])),
+                          str(int(self.reward[a, s]))]
+            out.append(" ".join(parts))
+        out.append("Vbar")
+        out.append(" ".join(str(v) for v in self.vbar))
+        return "\n".join(out) + "\n"
+
+    def write(self, path: str) -> None:
+        with open(path, "w") as fh:
+            fh.write(self.to_text())
+
+
+def generate(cfg: InstanceConfig, seed: int, scenarios: int | None = None) -> Instance:
+    """Deterministic (numpy PCG64) instance for ``cfg`` and ``seed``."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    S = cfg.scenarios if scenarios is None else scenarios
+    K, W, d = cfg.layers, cfg.width, cfg.out_degree
+    n = 2 + K * W
+    sink = n - 1
+
+    def node(layer: int, k: int) -> int:
+        return 1 + layer * W + k
+
+    arcs: List[Tuple[int, int]] = []
+    arcset = set()
+
+    def add(t: int, h: int) -> bool:
+        if (t, h) in arcset:
+            return False
+        arcset.add((t, h))
+        arcs.append((t, h))
+        return True
+
+    for k in range(W):
+        add(0, node(0, k))
+    for layer in range(K - 1):
+        covered = np.zeros(W, dtype=bool)
+        for k in range(W):
+            heads = rng.choice(W, size=min(d, W), replace=False)
+            for h in sorted(int(x) for x in heads):
+                add(node(layer, k), node(layer + 1, h))
+                covered[h] = True
+        for h in range(W):
+            if not covered[h]:
+                add(node(layer, int(rng.integers(0, W))), node(layer + 1, h))
+    for k in range(W):
+        add(node(K - 1, k), sink)
+
+    # top up / trim inter-layer arcs to hit |E| exactly
+    target = cfg.n_arcs
+    guard = 0
+    while len(arcs) < target and guard < 100000:
+        guard += 1
+        layer = int(rng.integers(0, K - 1))
+        add(node(layer, int(rng.integers(0, W))), node(layer + 1, int(rng.integers(0, W))))
+    guard = 0
+    while len(arcs) > target and guard < 100000:
+        guard += 1
+        idx = int(rng.integers(0, len(arcs)))
+        t, h = arcs[idx]
+        if t == 0 or h == sink:
+            continue
+        outdeg = sum(1 for (a, _) in arcs if a == t)
+        indeg = sum(1 for (_, b) in arcs if b == h)
+        if outdeg > 1 and indeg > 1:
+            arcs.pop(idx)
+            arcset.discard((t, h))
+    if len(arcs) != target:
+        raise ValueError(f"could not reach {target} arcs (got {len(arcs)})")
+
+    # file order: shuffle so that incoming-arc lists are not trivially sorted
+    order = rng.permutation(len(arcs))
+    arcs = [arcs[i] for i in order]
+    m = len(arcs)
+    tails = np.array([a[0] for a in arcs], dtype=np.int32)
+    heads = np.array([a[1] for a in arcs], dtype=np.int32)
+
+    ub = rng.integers(5, 51, size=(m, S)).astype(np.int32)
+    lb = np.zeros((m, S), dtype=np.int32)
+    sink_arcs = heads == sink
+    lbv = rng.integers(1, 4, size=(m, S)).astype(np.int32)
+    lbmask = rng.random(size=(m, S)) < 0.3
+    lb[sink_arcs] = np.where(lbmask[sink_arcs], lbv[sink_arcs], 0)
+    r = rng.integers(-5, 31, size=m).astype(np.int32)
+    reward = np.repeat(r[:, None], S, axis=1)
+
+    vbar = [v for v in range(1, n - 1) if rng.random() < cfg.vbar_prob]
+    if not vbar:
+        vbar = [node(K - 1, 0)]
+    return Instance(n=n, tails=tails, heads=heads, lb=lb, ub=ub, reward=reward, vbar=vbar)
+
+
+def generate_text(name: str, seed: int, scenarios: int | None = None) -> str:
+    return generate(CONFIGS[name], seed, scenarios).to_text()
