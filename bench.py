@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""B&B-node relaxations/s on the 1k-arc, 256-scenario synthetic instance (BASELINE.json).
+
+One step = NodeExplorer::process (NodeExplorer.cpp:915-986) for a whole batch of open
+nodes, on the device: build every relaxed DD, sweep the 16 feasibility + 64 optimality
+cuts of the pool over it (newest first), apply the reference's edits, and write the
+cutset children as frontier records (k_relax + k_scan2 + k_emit_children).  Inputs
+(network tables, cut rows, the open-node records) are resident in HBM before the
+timed region.  Exact DDs stop at the scenario-subproblem hand-off (status
+NEEDS_SUBPROBLEM, argmax path written) -- see DESIGN.md.
+
+Workload (config C4): seeded layered instance with 1000 arcs and 256
+scenarios, 16F + 64O synthetic cuts (tests2.cpp:259-286 recipe), a BFS frontier of
+open nodes from the root, incumbent = 40th percentile of the frontier's bounds.
+With N ranks every rank relaxes its own slice of a frontier N times as large
+(weak scaling, no collective on the data path; the per-step time is the max over
+ranks).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 the driver uses
+torch.distributed.run and this script reads RANK / LOCAL_RANK / WORLD_SIZE.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "B&B-node relaxations/sec + achieved HBM GB/s, 1k-arc 256-scenario synthetic"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--nodes", type=int, default=4096, help="open nodes per GPU per step")
+    ap.add_argument("--config", default="C4")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--n-feas", type=int, default=16)
+    ap.add_argument("--n-opt", type=int, default=64)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-sample", type=int, default=2048)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--profile-tag", default="r01")
+    return ap.parse_args()
+
+
+def pmc_traffic(tag: str, kernel: str = "k_relax"):
+    """HBM bytes per launch of `kernel` from committed rocprofv3 --pmc CSVs
+    (profiles/<tag>_pmc_fetch/*counter_collection.csv, profiles/<tag>_pmc_write/...).
+    gfx950: FETCH_SIZE (KB) reads half of a wide coalesced stream -> x2
+    (MI355X_MICROARCH.md §HBM); WRITE_SIZE (KB) is exact for 16-B stores."""
+    def load(pattern, counter):
+        vals = []
+        for path in glob.glob(os.path.join(ROOT, "profiles", pattern)):
+            import csv
+            with open(path) as fh:
+                for row in csv.DictReader(fh):
+                    if kernel in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                        vals.append(float(row["Counter_Value"]))
+        return vals
+    f = load(f"{tag}_pmc_fetch*/*counter_collection.csv", "FETCH_SIZE")
+    w = load(f"{tag}_pmc_write*/*counter_collection.csv", "WRITE_SIZE")
+    if not f or not w:
+        return None
+    return (2.0 * np.mean(f) + np.mean(w)) * 1024.0
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend)
+    import torch
+
+    from sgufp_solver_amd import engine as E
+    from sgufp_solver_amd import frontier, instance, pools
+
+    cfg = instance.CONFIGS[args.config]
+    inst = instance.generate(cfg, args.seed)
+    work = tempfile.mkdtemp(prefix=f"sgufp_bench_r{rank}_")
+    net = os.path.join(work, "net.txt")
+    inst.write(net)
+    pool = pools.synthetic_pool(inst, args.n_feas, args.n_opt, args.seed)
+
+    n = args.nodes
+    eng = E.Engine(net, local, max(n, 1024))
+    full = frontier.bfs_frontier(eng, n * world)          # identical on every rank
+    eng.add_cuts(pool)
+    # incumbent: 40th percentile of the (finite) bounds of the first 1024 records
+    probe = E.batch_slice(full, np.arange(min(1024, full.n)))
+    eng.upload(probe)
+    eng.relax_async(pools.DOUBLE_MIN)
+    eng.sync()
+    st, ex, lb, ub, nc = eng.results_arrays()
+    fin = ub[(st == 0) | (st == 3)]
+    incumbent = float(np.percentile(fin, 40)) if fin.size else 0.0
+    mine = E.batch_slice(full, np.arange(rank * n, min(full.n, (rank + 1) * n)))
+    eng.upload(mine)
+
+    eng.set_timing(True)
+    for _ in range(args.warmup):
+        eng.relax_async(incumbent)
+        eng.sync()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    relax_ms = []
+    emit_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.relax_async(incumbent)
+        eng.sync()
+        a, b = eng.last_timing()
+        relax_ms.append(a)
+        emit_ms.append(b)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-launch algorithmic bytes: 6A + sum_cuts(14A + 8N) + record in
+    st, ex, lb, ub, nc = eng.results_arrays()
+    dn, da, dl, sw = eng.stats()
+    g = mine.gl.astype(np.float64)
+    ns = np.diff(mine.states_off).astype(np.float64)
+    r_in = 2 * g + 2 * ns + 24
+    bytes_relax = float(np.sum(6.0 * da + sw * (14.0 * da + 8.0 * dn) + r_in))
+    ch = eng.children_batch()
+    r_out = float(np.sum(2 * ch.gl.astype(np.float64) + 2 * np.diff(ch.states_off) + 24)) if ch.n else 0.0
+    t_relax = float(np.mean(relax_ms)) / 1e3
+    achieved = bytes_relax / t_relax / 1e9
+    traffic = pmc_traffic(args.profile_tag)
+
+    total_nodes = mine.n * world
+    value = total_nodes * args.steps / elapsed
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "relaxations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"{args.config}: {cfg.n_arcs}-arc layered network, {inst.scenarios} scenarios, "
+                        f"{args.n_feas}F+{args.n_opt}O pool, BFS frontier of {n} open nodes per GPU",
+            "instance_seed": args.seed, "nodes_per_gpu": n, "incumbent": incumbent,
+            "total_layers": int(eng.info.total_layers),
+            "status_counts": {str(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
+            "avg_dd_nodes": float(np.mean(dn)), "avg_dd_arcs": float(np.mean(da)),
+            "avg_sweeps": float(np.mean(sw)), "children_per_step": int(ch.n),
+            "parallelism": f"frontier shards x{world}",
+        },
+        "hbm_gbps_algorithmic": round(achieved, 2),
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_relax",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": traffic,
+            "bytes_per_launch": bytes_relax,
+            "avg_launch_ms": round(t_relax * 1e3, 4),
+            "emit_ms": round(float(np.mean(emit_ms)), 4),
+            "children_record_bytes": r_out,
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(work, net, pool, mine, incumbent, args)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(work, net, pool, batch, incumbent, args):
+    """The reference's own RelaxedDDNew (oracle/_ref/ref_dd, built from its sources)
+    when present, else the clean-room port, on the host cores, bounded sample."""
+    from sgufp_solver_amd import engine as E
+    from sgufp_solver_amd import pools
+    sample = E.batch_slice(batch, np.arange(min(args.cpu_sample, batch.n)))
+    nodes = os.path.join(work, "nodes.txt")
+    cuts = os.path.join(work, "cuts.txt")
+    pools.write_nodes(nodes, E.batch_to_records(sample))
+    pools.write_pool(cuts, pool)
+    threads = max(1, min(16, os.cpu_count() or 1))
+    for kind, exe in (("reference", os.path.join(ROOT, "oracle", "_ref", "ref_dd")),
+                      ("port", os.path.join(ROOT, "oracle", "_build", "dd_oracle"))):
+        if not os.path.exists(exe):
+            continue
+        r = subprocess.run([exe, "time", net, cuts, nodes, incumbent.hex(), str(threads), str(args.cpu_seconds)],
+                           capture_output=True, text=True, timeout=args.cpu_seconds * 4 + 120)
+        if r.returncode != 0:
+            continue
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+        cpu_model = ""
+        try:
+            with open("/proc/cpuinfo") as fh:
+                cpu_model = next(l.split(":", 1)[1].strip() for l in fh if l.startswith("model name"))
+        except Exception:
+            pass
+        return {"value": round(out["relaxations"] / out["seconds"], 2), "unit": "relaxations/s", "cores": threads,
+                "kind": kind, "cpu": cpu_model,
+                "sample": f"{out['relaxations']} of the first {sample.n} open nodes of the same frontier, same pool and "
+                          f"incumbent, {out['seconds']:.1f} s on {threads} threads"}
+    return None
+
+
+if __name__ == "__main__":
+    main()

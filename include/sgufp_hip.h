@@ -1,0 +1,132 @@
+/*
+ * sgufp_hip.h -- C ABI of the MI355X relaxation engine (libsgufp_hip.so).
+ *
+ * Plain pointers and sizes only.  Every entry point replaces one piece of the
+ * reference's per-B&B-node relaxation path (var-nan/SGUFP_Solver @ 2025-07-18):
+ *
+ *   sgufp_create_from_file / sgufp_create
+ *       Network::Network(const std::string&)           Network.cpp:10-129, Network.h:113
+ *       (+ shuffleVBarNodes, Network.cpp:132-186)
+ *   sgufp_cuts_append
+ *       Inavap::Container::add(cut_node_t*)              Cut.h:461-465
+ *       (cut = Inavap::Cut{RHS, (key, coef)}            Cut.h:201-337; key = getKey(q,i,j) Cut.h:342-344)
+ *   sgufp_batch_upload + sgufp_batch_relax + sgufp_batch_results/_children/_paths
+ *       Inavap::NodeExplorer::process(Node, double optimalLB, Container&, Container&)
+ *                                                        NodeExplorer.cpp:915-986, NodeExplorer.h:130
+ *       i.e. RelaxedDDNew::buildTree / applyFeasibilityCut / applyOptimalityCut /
+ *       getCutset / getSolution                          DD.cpp:3528-4218, DD.h:797-808
+ *       for a whole batch of open nodes, up to the first scenario-subproblem call.
+ *   sgufp_batch_refine
+ *       the exact-DD refinement step of process: apply the cut the subproblem just
+ *       produced and return the next argmax path        NodeExplorer.cpp:946-969
+ *
+ * Conventions: functions return SGUFP_OK (0) or a negative SGUFP_ERR_* code; the
+ * caller owns every host buffer; a context is driven by one host thread at a time and
+ * owns one HIP stream.  Per-node outcomes use the reference's STATUS_OP values
+ * (NodeExplorer.h:81-85) plus SGUFP_NEEDS_SUBPROBLEM and error codes >= 16.
+ * Doubles are IEEE binary64 and bit-identical to the reference's results.
+ */
+#ifndef SGUFP_HIP_H
+#define SGUFP_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct sgufp_ctx sgufp_ctx;
+
+/* return codes */
+#define SGUFP_OK 0
+#define SGUFP_ERR_ARG (-1)
+#define SGUFP_ERR_NETWORK (-2)
+#define SGUFP_ERR_HIP (-3)
+#define SGUFP_ERR_CAPACITY (-4)
+#define SGUFP_ERR_STATE (-5)
+#define SGUFP_ERR_KEY (-6)
+
+/* per-node status (OutObject::STATUS_OP, NodeExplorer.h:81-85, + extensions) */
+#define SGUFP_SUCCESS 0
+#define SGUFP_PRUNED_BY_FEASIBILITY_CUT 1
+#define SGUFP_PRUNED_BY_OPTIMALITY_CUT 2
+#define SGUFP_NEEDS_SUBPROBLEM 3
+#define SGUFP_NODE_ERR_RECORD 16
+#define SGUFP_NODE_ERR_CAPACITY 17
+#define SGUFP_NODE_ERR_CUTSET 18
+
+typedef struct {
+    int32_t n, m, scenarios;     /* nodes, arcs, scenarios */
+    int32_t total_layers;        /* Network::totalLayers */
+    int32_t n_vbar;
+    int32_t max_states;          /* largest |out-arcs(q)| + 1 over V-bar nodes */
+    int32_t n_slots;             /* dense coefficients per cut row */
+    int32_t max_batch;
+    int64_t node_capacity;       /* DD nodes per slot */
+    int64_t arc_capacity;        /* merged-layer arcs per slot */
+    int64_t scratch_bytes;       /* device bytes held by the context */
+} sgufp_network_info;
+
+/* -- context ---------------------------------------------------------------- */
+sgufp_ctx *sgufp_create_from_file(const char *path, int device, int max_batch, int *err);
+sgufp_ctx *sgufp_create(int n, int m, int scenarios, const int32_t *tails, const int32_t *heads,
+                        const int32_t *lb, const int32_t *ub, const int32_t *reward, /* [m*scenarios] */
+                        int n_vbar, const int32_t *vbar, int device, int max_batch, int *err);
+void sgufp_destroy(sgufp_ctx *ctx);
+int sgufp_get_network_info(const sgufp_ctx *ctx, sgufp_network_info *out);
+/* processingOrder arc ids [total_layers] and V-bar order [n_vbar] */
+int sgufp_processing_order(const sgufp_ctx *ctx, int32_t *layer_arcs, int32_t *vbar_order);
+const char *sgufp_last_error(const sgufp_ctx *ctx);
+void *sgufp_stream(const sgufp_ctx *ctx); /* hipStream_t the kernels run on */
+
+/* Host-only parse of an instance file (no device is touched): totalLayers, then up to
+ * cap processingOrder arc ids and V-bar ids.  Returns SGUFP_OK or SGUFP_ERR_NETWORK. */
+int sgufp_probe_network(const char *path, int32_t *total_layers, int32_t *n_vbar, int32_t cap, int32_t *layer_arcs,
+                        int32_t *vbar_order);
+
+/* -- cut pool (global F and O Containers) ---------------------------------- */
+/* n_cuts cuts in insertion order; cut c has keys/vals [nnz_off[c], nnz_off[c+1]).
+ * keys are Inavap::getKey(q,i,j); lookup is first-match on the low 48 bits, zero
+ * coefficients may be present.  Keys that are not (i,q,j) of a V-bar arc pair are
+ * rejected with SGUFP_ERR_KEY.  Application order is newest first (LIFO list). */
+int sgufp_cuts_append(sgufp_ctx *ctx, int is_feasibility, int n_cuts, const double *rhs, const int64_t *nnz_off,
+                      const uint64_t *keys, const double *vals);
+int sgufp_cuts_clear(sgufp_ctx *ctx);
+int sgufp_cuts_count(const sgufp_ctx *ctx, int is_feasibility);
+
+/* -- batched relaxation ----------------------------------------------------- */
+/* Stage n open nodes (Inavap::Node, DD.h:456-478).  states of node k are
+ * states[states_off[k] .. states_off[k+1]), solution likewise. */
+int sgufp_batch_upload(sgufp_ctx *ctx, int n, const uint16_t *global_layer, const double *lb, const double *ub,
+                       const int64_t *states_off, const int16_t *states, const int64_t *sol_off,
+                       const int16_t *sol);
+/* Relax the staged batch against the current pools (asynchronous on the ctx stream). */
+int sgufp_batch_relax(sgufp_ctx *ctx, double optimal_lb);
+int sgufp_batch_sync(sgufp_ctx *ctx);
+/* Per node: status, exact flag, lb, ub, number of cutset children (any pointer may be NULL). */
+int sgufp_batch_results(sgufp_ctx *ctx, int32_t *status, uint8_t *exact, double *lb, double *ub,
+                        int32_t *n_children);
+/* Totals needed to size the children buffers. */
+int sgufp_batch_children_size(sgufp_ctx *ctx, int64_t *n_children, int64_t *n_states, int64_t *n_sol);
+/* Children of every node, concatenated in node order (child_off has n+1 entries). */
+int sgufp_batch_children(sgufp_ctx *ctx, int64_t *child_off, uint16_t *global_layer, double *lb, double *ub,
+                         int64_t *states_off, int16_t *states, int64_t *sol_off, int16_t *sol);
+/* Argmax paths of nodes with SGUFP_NEEDS_SUBPROBLEM (path_off has n+1 entries; others empty). */
+int sgufp_batch_paths(sgufp_ctx *ctx, int64_t *path_off, int16_t *paths);
+/* DD statistics: nodes / arcs right after the build, layers, cuts swept. */
+int sgufp_batch_stats(sgufp_ctx *ctx, int64_t *dd_nodes, int64_t *dd_arcs, int32_t *dd_layers, int32_t *sweeps);
+/* Apply, for each listed staged node (still SGUFP_NEEDS_SUBPROBLEM), the pool cut
+ * (is_feasibility[k], index in that pool) -- appended beforehand with
+ * sgufp_cuts_append -- and recompute status / ub / path. */
+int sgufp_batch_refine(sgufp_ctx *ctx, int n, const int32_t *node_idx, const uint8_t *is_feasibility,
+                       const int32_t *cut_index, double optimal_lb);
+
+/* -- timing (hipEvents on the ctx stream around each kernel of the last relax) -- */
+int sgufp_set_timing(sgufp_ctx *ctx, int enabled);
+int sgufp_last_timing(const sgufp_ctx *ctx, float *ms_relax, float *ms_emit);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SGUFP_HIP_H */

@@ -524,6 +524,38 @@ int main(int argc, char **argv) {
     using namespace oracle;
     if (argc < 2) return 2;
     std::string mode = argv[1];
+    if (mode == "refine" && argc == 8) {
+        // process() then the refinement loop (NodeExplorer.cpp:957-969) fed with <extra>
+        Net net;
+        if (!load_network(argv[2], net)) return 2;
+        auto cuts = read_cuts(argv[3]);
+        auto nodes = read_nodes(argv[4]);
+        double inc = std::strtod(argv[5], nullptr);
+        auto extra = read_cuts(argv[6]);
+        DD dd; dd.net = &net;
+        FILE *f = std::fopen(argv[7], "w");
+        std::fprintf(f, "%zu\n", nodes.size());
+        for (auto &nd : nodes) {
+            Result r = process(dd, nd, inc, cuts);
+            if (r.status == 3) {
+                double ub = r.ub;
+                for (auto &c : extra) {
+                    if (c.type == 1) {
+                        if (!dd.apply_feasibility(c)) { r.status = 1; break; }
+                    } else {
+                        ub = dd.apply_optimality(c, inc);
+                        if (ub <= inc) { r.status = 2; break; }
+                    }
+                }
+                r.path.clear();
+                if (r.status == 3) { r.ub = ub; r.path = dd.solution(); }
+                else { r.ub = DMIN; r.lb = DMIN; }
+            }
+            write_result(f, r);
+        }
+        std::fclose(f);
+        return 0;
+    }
     if ((mode == "relax" && argc == 7) || (mode == "time" && argc == 8)) {
         Net net;
         if (!load_network(argv[2], net)) { std::fprintf(stderr, "bad network\n"); return 2; }

@@ -231,6 +231,51 @@ int main(int argc, char **argv) {
         std::fclose(f);
         return 0;
     }
+    if (mode == "refine" && argc == 8) {
+        // process() up to the first subproblem, then the refinement loop of
+        // NodeExplorer.cpp:957-969 fed with the cuts of <extra> in order (instead of
+        // Gurobi's): each is applied to the exact DD, status/ub updated, path recomputed.
+        Network net{argv[2]};
+        auto cuts = read_cuts(argv[3]);
+        auto nodes = read_nodes(argv[4]);
+        double inc = parse_double(argv[5]);
+        auto extra = read_cuts(argv[6]);
+        Inavap::RelaxedDDNew dd{&net};
+        FILE *f = std::fopen(argv[7], "w");
+        std::fprintf(f, "%zu\n", nodes.size());
+        for (auto &nd : nodes) {
+            Result r = process(dd, nd, inc, cuts);
+            if (r.status == 3) {
+                double ub = r.ub;
+                for (auto &c : extra) {
+                    if (c.type == 1) {
+                        if (!dd.applyFeasibilityCut(c.cut)) { r.status = 1; break; }
+                    } else {
+                        ub = dd.applyOptimalityCut(c.cut, inc, ub);
+                        if (ub <= inc) { r.status = 2; break; }
+                    }
+                }
+                r.path.clear();
+                if (r.status == 3) { r.ub = ub; r.path = dd.getSolution(); }
+                else { r.ub = DOUBLE_MIN; r.lb = DOUBLE_MIN; }
+            }
+            write_result(f, r);
+        }
+        std::fclose(f);
+        return 0;
+    }
+    if (mode == "order" && argc == 4) {
+        // processingOrder / Vbar order / totalLayers of the reference loader
+        Network net{argv[2]};
+        FILE *f = std::fopen(argv[3], "w");
+        std::fprintf(f, "%u %zu %zu\n", net.totalLayers, net.processingOrder.size(), net.Vbar.size());
+        for (auto &p : net.processingOrder) std::fprintf(f, "%d ", p.second);
+        std::fprintf(f, "\n");
+        for (auto v : net.Vbar) std::fprintf(f, "%u ", v);
+        std::fprintf(f, "\n");
+        std::fclose(f);
+        return 0;
+    }
     if (mode == "time" && argc == 8) {
         // CPU baseline: static partition of the frontier over std::threads, each with
         // its own RelaxedDDNew (one NodeExplorer per thread, NodeExplorer.h:113-116).

@@ -1,0 +1,76 @@
+"""Native build: hipcc for gfx950, in-tree outputs (they travel to the GPU box).
+
+    libsgufp_hip.so   kernels + C ABI (include/sgufp_hip.h)
+    libsgufp_host.so  C++ mirror of the reference's host API (Network / NodeExplorer /
+                      DDSolver) on top of the C ABI
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
+          f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}"]
+
+HIP_SOURCES = ["dd_kernels.hip", "capi.cpp", "network.cpp"]
+HOST_SOURCES = ["host/inavap.cpp"]
+
+
+def _run(cmd, cwd=None):
+    r = subprocess.run(cmd, cwd=cwd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"build failed: {' '.join(cmd)}")
+    return r
+
+
+def _stale(target, sources):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def build_native(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(LIBDIR, exist_ok=True)
+    objdir = os.path.join(LIBDIR, "obj")
+    os.makedirs(objdir, exist_ok=True)
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
+    headers.append(os.path.join(ROOT, "include", "sgufp_hip.h"))
+    objs = []
+    for src in HIP_SOURCES:
+        path = os.path.join(CSRC, src)
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [path] + headers):
+            lang = ["-x", "hip"] if src.endswith(".hip") else []
+            cmd = [HIPCC, f"--offload-arch={ARCH}", *COMMON, *lang, "-c", path, "-o", obj]
+            if verbose:
+                print(" ".join(cmd))
+            _run(cmd)
+    lib = os.path.join(LIBDIR, "libsgufp_hip.so")
+    if force or _stale(lib, objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs])
+    host_srcs = [os.path.join(CSRC, s) for s in HOST_SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    if host_srcs:
+        hlib = os.path.join(LIBDIR, "libsgufp_host.so")
+        hheaders = [os.path.join(ROOT, "include", "sgufp", f) for f in os.listdir(os.path.join(ROOT, "include", "sgufp"))] \
+            if os.path.isdir(os.path.join(ROOT, "include", "sgufp")) else []
+        if force or _stale(hlib, host_srcs + hheaders + [lib]):
+            cxx = shutil.which("g++") or "g++"
+            _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", f"-I{os.path.join(ROOT, 'include')}",
+                  *host_srcs, "-o", hlib, f"-L{LIBDIR}", "-lsgufp_hip", f"-Wl,-rpath,$ORIGIN"])
+    return lib
+
+
+if __name__ == "__main__":
+    print(build_native(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,712 @@
+// C ABI of libsgufp_hip.so (declared in include/sgufp_hip.h): context, device
+// memory, cut-pool densification, batch staging and result retrieval.
+#include "sgufp_hip.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "dd_device.hpp"
+#include "network.hpp"
+
+namespace sgufp {
+// dd_kernels.hip
+size_t relax_lds_bytes(int Tcap, int Lcap);
+hipError_t launch_relax(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &, double,
+                        hipStream_t);
+hipError_t launch_scan(const uint32_t *, const uint32_t *, int, uint64_t *, uint64_t *, hipStream_t);
+hipError_t launch_emit(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &,
+                       const ChildOut &, hipStream_t);
+hipError_t launch_refine(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &,
+                         const int32_t *, const int32_t *, const uint8_t *, int, double, hipStream_t);
+}  // namespace sgufp
+
+using namespace sgufp;
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+struct sgufp_ctx {
+    Network net;
+    int device = 0;
+    int max_batch = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::vector<DevBuf> allocs;
+    size_t held = 0;
+
+    NetDev nd{};
+    Scratch sc{};
+    BatchOut out{};
+
+    // key (low 48 bits) -> slots carrying it
+    std::unordered_map<uint64_t, std::vector<int>> key_slots;
+
+    // cut pool
+    int row_cap = 0, n_rows = 0;
+    double *d_rows = nullptr, *d_rhs = nullptr;
+    std::vector<int32_t> f_rows, o_rows;      // insertion order, row ids
+    int32_t *d_forder = nullptr, *d_oorder = nullptr;
+    int order_cap = 0;
+    bool order_dirty = true;
+
+    // staged batch
+    int n = 0;
+    uint16_t *d_gl = nullptr, *d_sollen = nullptr;
+    double *d_lb = nullptr, *d_ub = nullptr;
+    uint32_t *d_mask = nullptr;
+    uint8_t *d_valid = nullptr;
+    int64_t *d_soloff = nullptr;
+    int16_t *d_sol = nullptr;
+    size_t sol_cap = 0;
+    std::vector<std::vector<int16_t>> host_sols;  // kept for path / child assembly on host
+
+    // outputs / children
+    uint64_t *d_coff = nullptr, *d_soff = nullptr;
+    size_t child_cap = 0, csol_cap = 0;
+    uint16_t *d_cgl = nullptr, *d_csollen = nullptr;
+    double *d_clb = nullptr, *d_cub = nullptr;
+    uint32_t *d_cmask = nullptr;
+    int64_t *d_csoloff = nullptr;
+    int16_t *d_csol = nullptr;
+    int64_t total_children = 0, total_csol = 0;
+    bool relaxed = false;
+
+    // refine staging
+    int32_t *d_rslots = nullptr, *d_rcuts = nullptr;
+    uint8_t *d_rfeas = nullptr;
+
+    bool timing = false;
+    hipEvent_t ev[4] = {};
+    float ms_relax = 0, ms_emit = 0;
+
+    ~sgufp_ctx() {
+        if (device >= 0) (void)hipSetDevice(device);
+        for (auto &b : allocs) (void)hipFree(b.p);
+        for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    bool hip_ok(hipError_t e, const char *what) {
+        if (e == hipSuccess) return true;
+        err = std::string(what) + ": " + hipGetErrorString(e);
+        return false;
+    }
+
+    template <typename T>
+    bool alloc(T *&ptr, size_t count, const char *what) {
+        void *p = nullptr;
+        size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+        if (!hip_ok(hipMalloc(&p, bytes), what)) return false;
+        allocs.push_back({p, bytes});
+        held += bytes;
+        ptr = (T *)p;
+        return true;
+    }
+    template <typename T>
+    void release(T *&ptr) {
+        for (size_t k = 0; k < allocs.size(); k++)
+            if (allocs[k].p == (void *)ptr) {
+                (void)hipFree(ptr);
+                held -= allocs[k].bytes;
+                allocs.erase(allocs.begin() + (long)k);
+                break;
+            }
+        ptr = nullptr;
+    }
+    template <typename T>
+    bool upload(T *dst, const T *src, size_t count) {
+        if (!count) return true;
+        return hip_ok(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyHostToDevice, stream), "H2D");
+    }
+    template <typename T>
+    bool download(T *dst, const T *src, size_t count) {
+        if (!count) return true;
+        return hip_ok(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyDeviceToHost, stream), "D2H");
+    }
+    bool sync() { return hip_ok(hipStreamSynchronize(stream), "stream sync"); }
+
+    bool init();
+    bool grow_rows(int need);
+    bool push_orders();
+    bool grow_children(size_t nchild, size_t nsol);
+    Pool pool() const {
+        Pool p;
+        p.rows = d_rows; p.rhs = d_rhs; p.stride = net.n_slots + 1;
+        p.f_order = d_forder; p.nf = (int)f_rows.size();
+        p.o_order = d_oorder; p.no = (int)o_rows.size();
+        return p;
+    }
+    BatchIn batch() const {
+        BatchIn b;
+        b.n = n; b.gl = d_gl; b.lb = d_lb; b.ub = d_ub; b.mask = d_mask; b.valid = d_valid;
+        b.sol_off = d_soloff; b.sol_len = d_sollen; b.sol = d_sol;
+        return b;
+    }
+};
+
+namespace {
+
+// Upper bound on DD nodes: every layer outside the last five has < 120 nodes or is a
+// single merged node (collapse rule, DD.cpp:3614); the last five expand exactly, and a
+// node with c states (-1 included) has one child with c states and c-1 with c-1.
+int64_t node_bound(const Network &net) {
+    const int L = net.L;
+    auto set_size = [&](int sid) { return sid >= 0 ? (int)net.sets[sid].size() : 1; };
+    int start = std::max(0, L - 5);
+    std::vector<int64_t> h(kMaxStates + 2, 0);
+    int c0 = set_size(net.layer_universe[start]);
+    h[c0] = (L > 5) ? kRelaxedMaxWidth - 1 : 1;
+    int64_t total = (int64_t)(kRelaxedMaxWidth - 1) * (start + 1);
+    for (int l = start; l < L; l++) {
+        if (net.layer_update[l] >= 0) {
+            int64_t w = 0;
+            for (auto x : h) w += x;
+            std::fill(h.begin(), h.end(), 0);
+            h[set_size(net.layer_update[l])] = w;
+        }
+        std::vector<int64_t> nh(h.size(), 0);
+        for (int c = 1; c < (int)h.size(); c++) {
+            if (!h[c]) continue;
+            nh[c] += h[c];
+            if (c > 1) nh[c - 1] += h[c] * (c - 1);
+        }
+        h.swap(nh);
+        int64_t w = 0;
+        for (auto x : h) w += x;
+        total += w;
+    }
+    return total + 8;
+}
+
+}  // namespace
+
+bool sgufp_ctx::init() {
+    if (!hip_ok(hipSetDevice(device), "hipSetDevice")) return false;
+    if (!hip_ok(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate")) return false;
+    for (auto &e : ev)
+        if (!hip_ok(hipEventCreate(&e), "hipEventCreate")) return false;
+    const int L = net.L;
+
+    // network tables
+    std::vector<int32_t> set_off, set_len;
+    std::vector<int16_t> set_val;
+    for (auto &s : net.sets) {
+        set_off.push_back((int32_t)set_val.size());
+        set_len.push_back((int32_t)s.size());
+        set_val.insert(set_val.end(), s.begin(), s.end());
+    }
+    int32_t *p_upd, *p_univ, *p_soff, *p_slen, *p_tab, *p_slotoff, *p_slothead, *p_head;
+    int16_t *p_sval;
+    uint8_t *p_changed;
+    if (!alloc(p_upd, L + 1, "net") || !alloc(p_univ, L + 1, "net") || !alloc(p_changed, L + 1, "net") ||
+        !alloc(p_soff, set_off.size(), "net") || !alloc(p_slen, set_len.size(), "net") ||
+        !alloc(p_sval, set_val.size(), "net") || !alloc(p_tab, net.slot_tab.size(), "net") ||
+        !alloc(p_slotoff, net.slot_off.size(), "net") || !alloc(p_slothead, net.slot_head.size(), "net") ||
+        !alloc(p_head, net.head.size(), "net"))
+        return false;
+    std::vector<uint8_t> changed(net.state_changed.begin(), net.state_changed.end());
+    changed.resize(L + 1, 0);
+    upload(p_upd, net.layer_update.data(), L + 1);
+    upload(p_univ, net.layer_universe.data(), L + 1);
+    upload(p_changed, changed.data(), L + 1);
+    upload(p_soff, set_off.data(), set_off.size());
+    upload(p_slen, set_len.data(), set_len.size());
+    upload(p_sval, set_val.data(), set_val.size());
+    upload(p_tab, net.slot_tab.data(), net.slot_tab.size());
+    upload(p_slotoff, net.slot_off.data(), net.slot_off.size());
+    upload(p_slothead, net.slot_head.data(), net.slot_head.size());
+    upload(p_head, net.head.data(), net.head.size());
+    nd.L = L;
+    nd.L5 = (unsigned)(L - 5);
+    nd.m = net.m;
+    nd.n_slots = net.n_slots;
+    nd.layer_update = p_upd; nd.layer_universe = p_univ; nd.changed = p_changed;
+    nd.set_off = p_soff; nd.set_len = p_slen; nd.set_val = p_sval;
+    nd.slot_tab = p_tab; nd.slot_off = p_slotoff; nd.slot_head = p_slothead; nd.arc_head = p_head;
+
+    for (int s = 0; s < net.n_slots; s++) key_slots[net.slot_key(s) & 0xFFFFFFFFFFFFull].push_back(s);
+
+    // per-slot scratch
+    const int maxU = std::max(1, net.max_states);
+    sc.Tcap = L + 2;
+    sc.Lcap = L + 1;
+    int64_t ncap = node_bound(net);
+    int64_t acap = std::max<int64_t>(1, (int64_t)std::max(0, L - 4) * (kRelaxedMaxWidth - 1) * maxU);
+    if (ncap > (int64_t)kParentMask || acap > (int64_t)0x7FFFFFFF) { err = "DD capacity beyond 22-bit indices"; return false; }
+    sc.Ncap = (int)ncap;
+    sc.Acap = (int)acap;
+    if (relax_lds_bytes(sc.Tcap, sc.Lcap) > 64 * 1024) { err = "too many layers for the LDS layer table"; return false; }
+    const size_t B = (size_t)max_batch;
+    if (!alloc(sc.ntopo, B * sc.Ncap, "scratch") || !alloc(sc.nflag, B * sc.Ncap, "scratch") ||
+        !alloc(sc.nmask, B * sc.Ncap, "scratch") || !alloc(sc.outcnt, B * sc.Ncap, "scratch") ||
+        !alloc(sc.s2, B * sc.Ncap, "scratch") || !alloc(sc.tw, B * sc.Ncap, "scratch") ||
+        !alloc(sc.atopo, B * sc.Acap, "scratch") || !alloc(sc.aflag, B * sc.Acap, "scratch") ||
+        !alloc(sc.lay, B * sc.Tcap * 5, "scratch") || !alloc(sc.rslot, B * sc.Lcap, "scratch") ||
+        !alloc(sc.meta, B * 8, "scratch") || !alloc(sc.ubv, B, "scratch"))
+        return false;
+    // outputs
+    if (!alloc(out.status, B, "out") || !alloc(out.exact, B, "out") || !alloc(out.lb, B, "out") ||
+        !alloc(out.ub, B, "out") || !alloc(out.nchild, B, "out") || !alloc(out.sol_need, B, "out") ||
+        !alloc(out.dd_nodes, B, "out") || !alloc(out.dd_arcs, B, "out") || !alloc(out.dd_layers, B, "out") ||
+        !alloc(out.sweeps, B, "out") || !alloc(out.path, B * sc.Lcap, "out") || !alloc(out.path_len, B, "out"))
+        return false;
+    // batch input
+    if (!alloc(d_gl, B, "batch") || !alloc(d_sollen, B, "batch") || !alloc(d_lb, B, "batch") ||
+        !alloc(d_ub, B, "batch") || !alloc(d_mask, B, "batch") || !alloc(d_valid, B, "batch") ||
+        !alloc(d_soloff, B, "batch") || !alloc(d_coff, B + 1, "batch") || !alloc(d_soff, B + 1, "batch") ||
+        !alloc(d_rslots, B, "batch") || !alloc(d_rcuts, B, "batch") || !alloc(d_rfeas, B, "batch"))
+        return false;
+    sol_cap = B * (size_t)std::max(1, L);
+    if (!alloc(d_sol, sol_cap, "batch")) return false;
+    if (!grow_rows(64)) return false;
+    return sync();
+}
+
+bool sgufp_ctx::grow_rows(int need) {
+    if (need <= row_cap) return true;
+    int cap = std::max(need, row_cap * 2);
+    const size_t stride = (size_t)net.n_slots + 1;
+    double *rows = nullptr, *rhs = nullptr;
+    if (!alloc(rows, (size_t)cap * stride, "cut rows") || !alloc(rhs, (size_t)cap, "cut rhs")) return false;
+    if (n_rows) {
+        if (!hip_ok(hipMemcpyAsync(rows, d_rows, (size_t)n_rows * stride * 8, hipMemcpyDeviceToDevice, stream), "D2D") ||
+            !hip_ok(hipMemcpyAsync(rhs, d_rhs, (size_t)n_rows * 8, hipMemcpyDeviceToDevice, stream), "D2D"))
+            return false;
+        if (!sync()) return false;
+    }
+    release(d_rows);
+    release(d_rhs);
+    d_rows = rows;
+    d_rhs = rhs;
+    row_cap = cap;
+    return true;
+}
+
+bool sgufp_ctx::push_orders() {
+    if (!order_dirty) return true;
+    int need = (int)std::max(f_rows.size(), o_rows.size());
+    if (need > order_cap) {
+        release(d_forder);
+        release(d_oorder);
+        order_cap = std::max(need, 2 * order_cap);
+        if (!alloc(d_forder, order_cap, "orders") || !alloc(d_oorder, order_cap, "orders")) return false;
+    }
+    // newest first: the Container is a LIFO list read from its head (Cut.h:456-465)
+    std::vector<int32_t> f(f_rows.rbegin(), f_rows.rend()), o(o_rows.rbegin(), o_rows.rend());
+    if (!upload(d_forder, f.data(), f.size()) || !upload(d_oorder, o.data(), o.size())) return false;
+    if (!sync()) return false;
+    order_dirty = false;
+    return true;
+}
+
+bool sgufp_ctx::grow_children(size_t nchild, size_t nsol) {
+    if (nchild > child_cap) {
+        release(d_cgl); release(d_csollen); release(d_clb); release(d_cub); release(d_cmask); release(d_csoloff);
+        child_cap = std::max(nchild, child_cap * 2);
+        if (!alloc(d_cgl, child_cap, "children") || !alloc(d_csollen, child_cap, "children") ||
+            !alloc(d_clb, child_cap, "children") || !alloc(d_cub, child_cap, "children") ||
+            !alloc(d_cmask, child_cap, "children") || !alloc(d_csoloff, child_cap, "children"))
+            return false;
+    }
+    if (nsol > csol_cap) {
+        release(d_csol);
+        csol_cap = std::max(nsol, csol_cap * 2);
+        if (!alloc(d_csol, csol_cap, "children")) return false;
+    }
+    return true;
+}
+
+static sgufp_ctx *finish_create(sgufp_ctx *ctx, int *err) {
+    if (!ctx->init()) {
+        if (err) *err = SGUFP_ERR_HIP;
+        delete ctx;
+        return nullptr;
+    }
+    if (err) *err = SGUFP_OK;
+    return ctx;
+}
+
+extern "C" {
+
+sgufp_ctx *sgufp_create_from_file(const char *path, int device, int max_batch, int *err) {
+    if (!path || max_batch <= 0) { if (err) *err = SGUFP_ERR_ARG; return nullptr; }
+    auto *ctx = new sgufp_ctx();
+    ctx->device = device;
+    ctx->max_batch = max_batch;
+    if (!ctx->net.load_file(path)) {
+        if (err) *err = SGUFP_ERR_NETWORK;
+        delete ctx;
+        return nullptr;
+    }
+    return finish_create(ctx, err);
+}
+
+sgufp_ctx *sgufp_create(int n, int m, int scenarios, const int32_t *tails, const int32_t *heads, const int32_t *lb,
+                        const int32_t *ub, const int32_t *reward, int n_vbar, const int32_t *vbar, int device,
+                        int max_batch, int *err) {
+    if (n <= 0 || m < 0 || scenarios <= 0 || max_batch <= 0 || (m && (!tails || !heads || !lb || !ub || !reward)) ||
+        (n_vbar && !vbar)) {
+        if (err) *err = SGUFP_ERR_ARG;
+        return nullptr;
+    }
+    auto *ctx = new sgufp_ctx();
+    ctx->device = device;
+    ctx->max_batch = max_batch;
+    if (!ctx->net.load_arrays(n, m, scenarios, tails, heads, lb, ub, reward, n_vbar, vbar)) {
+        if (err) *err = SGUFP_ERR_NETWORK;
+        delete ctx;
+        return nullptr;
+    }
+    return finish_create(ctx, err);
+}
+
+void sgufp_destroy(sgufp_ctx *ctx) { delete ctx; }
+
+const char *sgufp_last_error(const sgufp_ctx *ctx) {
+    if (!ctx) return "null context";
+    return ctx->err.empty() ? ctx->net.error.c_str() : ctx->err.c_str();
+}
+
+void *sgufp_stream(const sgufp_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int sgufp_get_network_info(const sgufp_ctx *ctx, sgufp_network_info *o) {
+    if (!ctx || !o) return SGUFP_ERR_ARG;
+    o->n = ctx->net.n; o->m = ctx->net.m; o->scenarios = ctx->net.S;
+    o->total_layers = ctx->net.L;
+    o->n_vbar = (int32_t)ctx->net.vbar.size();
+    o->max_states = ctx->net.max_states;
+    o->n_slots = ctx->net.n_slots;
+    o->max_batch = ctx->max_batch;
+    o->node_capacity = ctx->sc.Ncap;
+    o->arc_capacity = ctx->sc.Acap;
+    o->scratch_bytes = (int64_t)ctx->held;
+    return SGUFP_OK;
+}
+
+int sgufp_processing_order(const sgufp_ctx *ctx, int32_t *layer_arcs, int32_t *vbar_order) {
+    if (!ctx) return SGUFP_ERR_ARG;
+    if (layer_arcs) std::copy(ctx->net.layer_arc.begin(), ctx->net.layer_arc.end(), layer_arcs);
+    if (vbar_order) std::copy(ctx->net.vbar.begin(), ctx->net.vbar.end(), vbar_order);
+    return SGUFP_OK;
+}
+
+int sgufp_probe_network(const char *path, int32_t *total_layers, int32_t *n_vbar, int32_t cap, int32_t *layer_arcs,
+                        int32_t *vbar_order) {
+    if (!path) return SGUFP_ERR_ARG;
+    Network net;
+    if (!net.load_file(path)) return SGUFP_ERR_NETWORK;
+    if (total_layers) *total_layers = net.L;
+    if (n_vbar) *n_vbar = (int32_t)net.vbar.size();
+    for (int k = 0; layer_arcs && k < std::min<int>(cap, net.L); k++) layer_arcs[k] = net.layer_arc[k];
+    for (int k = 0; vbar_order && k < std::min<int>(cap, (int)net.vbar.size()); k++) vbar_order[k] = net.vbar[k];
+    return SGUFP_OK;
+}
+
+int sgufp_cuts_append(sgufp_ctx *ctx, int is_feasibility, int n_cuts, const double *rhs, const int64_t *nnz_off,
+                      const uint64_t *keys, const double *vals) {
+    if (!ctx || n_cuts < 0 || (n_cuts && (!rhs || !nnz_off))) return SGUFP_ERR_ARG;
+    if (n_cuts == 0) return SGUFP_OK;
+    const size_t stride = (size_t)ctx->net.n_slots + 1;
+    std::vector<double> rows((size_t)n_cuts * stride, 0.0);
+    std::vector<uint8_t> seen(stride);
+    for (int c = 0; c < n_cuts; c++) {
+        std::fill(seen.begin(), seen.end(), 0);
+        double *row = rows.data() + (size_t)c * stride;
+        for (int64_t k = nnz_off[c]; k < nnz_off[c + 1]; k++) {
+            uint64_t key = keys[k] & 0xFFFFFFFFFFFFull;
+            auto it = ctx->key_slots.find(key);
+            if (it == ctx->key_slots.end()) {
+                ctx->err = "cut key is not an (i,q,j) triple of a DD layer";
+                return SGUFP_ERR_KEY;
+            }
+            for (int s : it->second) {
+                if (seen[s]) continue;  // Cut::get returns the first match (Cut.h:278-281)
+                seen[s] = 1;
+                row[s] = vals[k];
+            }
+        }
+    }
+    int first = ctx->n_rows;
+    if (!ctx->grow_rows(first + n_cuts)) return SGUFP_ERR_HIP;
+    if (!ctx->upload(ctx->d_rows + (size_t)first * stride, rows.data(), rows.size()) ||
+        !ctx->upload(ctx->d_rhs + first, rhs, (size_t)n_cuts) || !ctx->sync())
+        return SGUFP_ERR_HIP;
+    for (int c = 0; c < n_cuts; c++) (is_feasibility ? ctx->f_rows : ctx->o_rows).push_back(first + c);
+    ctx->n_rows += n_cuts;
+    ctx->order_dirty = true;
+    return SGUFP_OK;
+}
+
+int sgufp_cuts_clear(sgufp_ctx *ctx) {
+    if (!ctx) return SGUFP_ERR_ARG;
+    ctx->f_rows.clear();
+    ctx->o_rows.clear();
+    ctx->n_rows = 0;
+    ctx->order_dirty = true;
+    return SGUFP_OK;
+}
+
+int sgufp_cuts_count(const sgufp_ctx *ctx, int is_feasibility) {
+    if (!ctx) return SGUFP_ERR_ARG;
+    return (int)(is_feasibility ? ctx->f_rows.size() : ctx->o_rows.size());
+}
+
+int sgufp_batch_upload(sgufp_ctx *ctx, int n, const uint16_t *gl, const double *lb, const double *ub,
+                       const int64_t *states_off, const int16_t *states, const int64_t *sol_off, const int16_t *sol) {
+    if (!ctx || n < 0 || n > ctx->max_batch || (n && (!gl || !lb || !ub || !states_off || !sol_off)))
+        return SGUFP_ERR_ARG;
+    const Network &net = ctx->net;
+    std::vector<uint32_t> mask(n, 0);
+    std::vector<uint8_t> valid(n, 1);
+    std::vector<int64_t> soff(n);
+    std::vector<uint16_t> slen(n);
+    size_t total = 0;
+    for (int k = 0; k < n; k++) {
+        int64_t l = sol_off[k + 1] - sol_off[k];
+        if (l < 0 || l > net.L) { valid[k] = 0; l = 0; }
+        soff[k] = (int64_t)total;
+        slen[k] = (uint16_t)l;
+        total += (size_t)l;
+    }
+    std::vector<int16_t> sols(total);
+    ctx->host_sols.assign(n, {});
+    for (int k = 0; k < n; k++) {
+        if (slen[k]) std::memcpy(sols.data() + soff[k], sol + sol_off[k], slen[k] * sizeof(int16_t));
+        ctx->host_sols[k].assign(sols.begin() + soff[k], sols.begin() + soff[k] + slen[k]);
+        for (int t = 0; t < slen[k]; t++) {
+            int d = sols[soff[k] + t];
+            if (d != -1 && (d < 0 || d >= net.m)) valid[k] = 0;
+        }
+        int g = gl[k];
+        if (g > net.L) { valid[k] = 0; continue; }
+        if (g < net.L && net.layer_update[g] >= 0) continue;  // states replaced at this layer (DD.cpp:3557-3571)
+        int u = net.layer_universe[g];
+        int prev = -1;
+        for (int64_t t = states_off[k]; t < states_off[k + 1]; t++) {
+            int r = -1;
+            if (u >= 0) {
+                const auto &U = net.sets[u];
+                auto it = std::lower_bound(U.begin(), U.end(), states[t]);
+                if (it != U.end() && *it == states[t]) r = (int)(it - U.begin());
+            }
+            if (r < 0 || r <= prev) { valid[k] = 0; break; }  // not a sorted subset of the universe
+            mask[k] |= 1u << r;
+            prev = r;
+        }
+    }
+    if (total > ctx->sol_cap) {
+        ctx->release(ctx->d_sol);
+        ctx->sol_cap = std::max(total, 2 * ctx->sol_cap);
+        if (!ctx->alloc(ctx->d_sol, ctx->sol_cap, "batch")) return SGUFP_ERR_HIP;
+    }
+    ctx->n = n;
+    if (!ctx->upload(ctx->d_gl, gl, n) || !ctx->upload(ctx->d_lb, lb, n) || !ctx->upload(ctx->d_ub, ub, n) ||
+        !ctx->upload(ctx->d_mask, mask.data(), n) || !ctx->upload(ctx->d_valid, valid.data(), n) ||
+        !ctx->upload(ctx->d_soloff, soff.data(), n) || !ctx->upload(ctx->d_sollen, slen.data(), n) ||
+        !ctx->upload(ctx->d_sol, sols.data(), total) || !ctx->sync())
+        return SGUFP_ERR_HIP;
+    ctx->relaxed = false;
+    return SGUFP_OK;
+}
+
+int sgufp_batch_relax(sgufp_ctx *ctx, double optimal_lb) {
+    if (!ctx) return SGUFP_ERR_ARG;
+    if (!ctx->push_orders()) return SGUFP_ERR_HIP;
+    const BatchIn in = ctx->batch();
+    const Pool pool = ctx->pool();
+    hipStream_t st = ctx->stream;
+    if (ctx->timing) hipEventRecord(ctx->ev[0], st);
+    if (!ctx->hip_ok(launch_relax(ctx->nd, ctx->sc, in, pool, ctx->out, optimal_lb, st), "k_relax")) return SGUFP_ERR_HIP;
+    if (ctx->timing) hipEventRecord(ctx->ev[1], st);
+    if (in.n > 0 &&
+        !ctx->hip_ok(launch_scan(ctx->out.nchild, ctx->out.sol_need, in.n, ctx->d_coff, ctx->d_soff, st), "k_scan2"))
+        return SGUFP_ERR_HIP;
+    uint64_t tot[2] = {0, 0};
+    if (in.n > 0) {
+        if (!ctx->download(&tot[0], ctx->d_coff + in.n, 1) || !ctx->download(&tot[1], ctx->d_soff + in.n, 1))
+            return SGUFP_ERR_HIP;
+    }
+    if (!ctx->sync()) return SGUFP_ERR_HIP;
+    ctx->total_children = (int64_t)tot[0];
+    ctx->total_csol = (int64_t)tot[1];
+    if (!ctx->grow_children((size_t)tot[0], (size_t)tot[1])) return SGUFP_ERR_HIP;
+    ChildOut co;
+    co.child_off = ctx->d_coff; co.sol_base = ctx->d_soff;
+    co.gl = ctx->d_cgl; co.lb = ctx->d_clb; co.ub = ctx->d_cub; co.mask = ctx->d_cmask;
+    co.sol_off = ctx->d_csoloff; co.sol_len = ctx->d_csollen; co.sol = ctx->d_csol;
+    if (ctx->timing) hipEventRecord(ctx->ev[2], st);
+    if (tot[0] > 0 && !ctx->hip_ok(launch_emit(ctx->nd, ctx->sc, in, pool, ctx->out, co, st), "k_emit_children"))
+        return SGUFP_ERR_HIP;
+    if (ctx->timing) hipEventRecord(ctx->ev[3], st);
+    ctx->relaxed = true;
+    return SGUFP_OK;
+}
+
+int sgufp_batch_sync(sgufp_ctx *ctx) {
+    if (!ctx) return SGUFP_ERR_ARG;
+    if (!ctx->sync()) return SGUFP_ERR_HIP;
+    if (ctx->timing && ctx->relaxed) {
+        hipEventElapsedTime(&ctx->ms_relax, ctx->ev[0], ctx->ev[1]);
+        hipEventElapsedTime(&ctx->ms_emit, ctx->ev[2], ctx->ev[3]);
+    }
+    return SGUFP_OK;
+}
+
+int sgufp_batch_results(sgufp_ctx *ctx, int32_t *status, uint8_t *exact, double *lb, double *ub, int32_t *n_children) {
+    if (!ctx || !ctx->relaxed) return ctx ? SGUFP_ERR_STATE : SGUFP_ERR_ARG;
+    const int n = ctx->n;
+    std::vector<uint32_t> nc(n);
+    if ((status && !ctx->download(status, ctx->out.status, n)) || (exact && !ctx->download(exact, ctx->out.exact, n)) ||
+        (lb && !ctx->download(lb, ctx->out.lb, n)) || (ub && !ctx->download(ub, ctx->out.ub, n)) ||
+        (n_children && !ctx->download(nc.data(), ctx->out.nchild, n)) || !ctx->sync())
+        return SGUFP_ERR_HIP;
+    if (n_children)
+        for (int k = 0; k < n; k++) n_children[k] = (int32_t)nc[k];
+    return SGUFP_OK;
+}
+
+int sgufp_batch_children_size(sgufp_ctx *ctx, int64_t *n_children, int64_t *n_states, int64_t *n_sol) {
+    if (!ctx || !ctx->relaxed) return ctx ? SGUFP_ERR_STATE : SGUFP_ERR_ARG;
+    const size_t nc = (size_t)ctx->total_children;
+    std::vector<uint16_t> gl(nc), sl(nc);
+    std::vector<uint32_t> mask(nc);
+    if (!ctx->download(gl.data(), ctx->d_cgl, nc) || !ctx->download(sl.data(), ctx->d_csollen, nc) ||
+        !ctx->download(mask.data(), ctx->d_cmask, nc) || !ctx->sync())
+        return SGUFP_ERR_HIP;
+    int64_t ns = 0, nsol = 0;
+    for (size_t c = 0; c < nc; c++) {
+        ns += __builtin_popcount(mask[c]);
+        nsol += sl[c];
+    }
+    if (n_children) *n_children = (int64_t)nc;
+    if (n_states) *n_states = ns;
+    if (n_sol) *n_sol = nsol;
+    return SGUFP_OK;
+}
+
+int sgufp_batch_children(sgufp_ctx *ctx, int64_t *child_off, uint16_t *gl, double *lb, double *ub,
+                         int64_t *states_off, int16_t *states, int64_t *sol_off, int16_t *sol) {
+    if (!ctx || !ctx->relaxed) return ctx ? SGUFP_ERR_STATE : SGUFP_ERR_ARG;
+    const int n = ctx->n;
+    const size_t nc = (size_t)ctx->total_children;
+    std::vector<uint64_t> coff(n + 1);
+    std::vector<uint16_t> cgl(nc), csl(nc);
+    std::vector<double> clb(nc), cub(nc);
+    std::vector<uint32_t> cmask(nc);
+    std::vector<int64_t> csoff(nc);
+    std::vector<int16_t> csol((size_t)ctx->total_csol);
+    if (!ctx->download(coff.data(), ctx->d_coff, n + 1) || !ctx->download(cgl.data(), ctx->d_cgl, nc) ||
+        !ctx->download(csl.data(), ctx->d_csollen, nc) || !ctx->download(clb.data(), ctx->d_clb, nc) ||
+        !ctx->download(cub.data(), ctx->d_cub, nc) || !ctx->download(cmask.data(), ctx->d_cmask, nc) ||
+        !ctx->download(csoff.data(), ctx->d_csoloff, nc) || !ctx->download(csol.data(), ctx->d_csol, csol.size()) ||
+        !ctx->sync())
+        return SGUFP_ERR_HIP;
+    const Network &net = ctx->net;
+    if (child_off)
+        for (int k = 0; k <= n; k++) child_off[k] = (int64_t)coff[k];
+    int64_t so = 0, ss = 0;
+    for (size_t c = 0; c < nc; c++) {
+        if (gl) gl[c] = cgl[c];
+        if (lb) lb[c] = clb[c];
+        if (ub) ub[c] = cub[c];
+        if (states_off) states_off[c] = ss;
+        int u = net.layer_universe[cgl[c]];
+        for (uint32_t m = cmask[c]; m; m &= m - 1) {
+            int r = __builtin_ctz(m);
+            if (states) states[ss] = net.sets[u][r];
+            ss++;
+        }
+        if (sol_off) sol_off[c] = so;
+        if (sol) std::memcpy(sol + so, csol.data() + csoff[c], csl[c] * sizeof(int16_t));
+        so += csl[c];
+    }
+    if (states_off) states_off[nc] = ss;
+    if (sol_off) sol_off[nc] = so;
+    return SGUFP_OK;
+}
+
+int sgufp_batch_paths(sgufp_ctx *ctx, int64_t *path_off, int16_t *paths) {
+    if (!ctx || !ctx->relaxed || !path_off) return ctx ? SGUFP_ERR_STATE : SGUFP_ERR_ARG;
+    const int n = ctx->n;
+    std::vector<int32_t> st(n);
+    std::vector<uint16_t> pl(n);
+    if (!ctx->download(st.data(), ctx->out.status, n) || !ctx->download(pl.data(), ctx->out.path_len, n) || !ctx->sync())
+        return SGUFP_ERR_HIP;
+    int64_t off = 0;
+    for (int k = 0; k < n; k++) {
+        path_off[k] = off;
+        if (st[k] == SGUFP_NEEDS_SUBPROBLEM) {
+            if (paths && !ctx->download(paths + off, ctx->out.path + (size_t)k * ctx->sc.Lcap, pl[k])) return SGUFP_ERR_HIP;
+            off += pl[k];
+        }
+    }
+    path_off[n] = off;
+    return ctx->sync() ? SGUFP_OK : SGUFP_ERR_HIP;
+}
+
+int sgufp_batch_stats(sgufp_ctx *ctx, int64_t *dd_nodes, int64_t *dd_arcs, int32_t *dd_layers, int32_t *sweeps) {
+    if (!ctx || !ctx->relaxed) return ctx ? SGUFP_ERR_STATE : SGUFP_ERR_ARG;
+    const int n = ctx->n;
+    std::vector<uint32_t> a(n), b(n), c(n), d(n);
+    if (!ctx->download(a.data(), ctx->out.dd_nodes, n) || !ctx->download(b.data(), ctx->out.dd_arcs, n) ||
+        !ctx->download(c.data(), ctx->out.dd_layers, n) || !ctx->download(d.data(), ctx->out.sweeps, n) ||
+        !ctx->sync())
+        return SGUFP_ERR_HIP;
+    for (int k = 0; k < n; k++) {
+        if (dd_nodes) dd_nodes[k] = a[k];
+        if (dd_arcs) dd_arcs[k] = b[k];
+        if (dd_layers) dd_layers[k] = (int32_t)c[k];
+        if (sweeps) sweeps[k] = (int32_t)d[k];
+    }
+    return SGUFP_OK;
+}
+
+int sgufp_batch_refine(sgufp_ctx *ctx, int n, const int32_t *node_idx, const uint8_t *is_feasibility,
+                       const int32_t *cut_index, double optimal_lb) {
+    if (!ctx || !ctx->relaxed || n < 0 || n > ctx->max_batch || (n && (!node_idx || !is_feasibility || !cut_index)))
+        return SGUFP_ERR_ARG;
+    if (n == 0) return SGUFP_OK;
+    std::vector<int32_t> rows(n);
+    for (int k = 0; k < n; k++) {
+        const auto &v = is_feasibility[k] ? ctx->f_rows : ctx->o_rows;
+        if (node_idx[k] < 0 || node_idx[k] >= ctx->n || cut_index[k] < 0 || cut_index[k] >= (int)v.size())
+            return SGUFP_ERR_ARG;
+        rows[k] = v[cut_index[k]];
+    }
+    if (!ctx->upload(ctx->d_rslots, node_idx, n) || !ctx->upload(ctx->d_rcuts, rows.data(), n) ||
+        !ctx->upload(ctx->d_rfeas, is_feasibility, n))
+        return SGUFP_ERR_HIP;
+    if (!ctx->hip_ok(launch_refine(ctx->nd, ctx->sc, ctx->batch(), ctx->pool(), ctx->out, ctx->d_rslots, ctx->d_rcuts,
+                                   ctx->d_rfeas, n, optimal_lb, ctx->stream),
+                     "k_refine"))
+        return SGUFP_ERR_HIP;
+    return ctx->sync() ? SGUFP_OK : SGUFP_ERR_HIP;
+}
+
+int sgufp_set_timing(sgufp_ctx *ctx, int enabled) {
+    if (!ctx) return SGUFP_ERR_ARG;
+    ctx->timing = enabled != 0;
+    return SGUFP_OK;
+}
+
+int sgufp_last_timing(const sgufp_ctx *ctx, float *ms_relax, float *ms_emit) {
+    if (!ctx) return SGUFP_ERR_ARG;
+    if (ms_relax) *ms_relax = ctx->ms_relax;
+    if (ms_emit) *ms_emit = ctx->ms_emit;
+    return SGUFP_OK;
+}
+
+}  // extern "C"

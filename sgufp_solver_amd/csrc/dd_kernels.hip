@@ -1,0 +1,1017 @@
+// MI355X (gfx950) kernels for the per-B&B-node relaxation of SGUFP_Solver.
+//
+// One open node = one relaxed decision diagram = one 64-lane wavefront (a single-wave
+// workgroup).  Per node the kernel
+//   1. builds the relaxed DD layer by layer (RelaxedDDNew::buildTree / buildNextLayer,
+//      /root/reference/DD.cpp:3528-3694): wave prefix scans give child offsets, state
+//      sets are u32 masks over the V-bar node's sorted state universe;
+//   2. sweeps every pool cut over it (applyFeasibilityCut DD.cpp:3842-3930,
+//      applyOptimalityCut DD.cpp:3932-4023): a layered (max,+) longest path whose
+//      previous-layer state2 lives in LDS; coefficients come from dense cut rows
+//      (one slot per (layer, head) key, Cut.h:275-282/342-344) gathered once per layer
+//      by 32 lanes and broadcast by rank;
+//   3. applies the reference's edits exactly: last-layer removal with the bottom-up
+//      deletion cascade (DD.cpp:4040-4119), width-1 arc pruning (DD.cpp:3895-3928,
+//      3987-4021), running-min terminal weights;
+//   4. finishes like NodeExplorer::process (NodeExplorer.cpp:915-986): the cutset
+//      layer and child count (getCutset, DD.cpp:4179-4218) or, for an exact DD, the
+//      argmax path (getSolution, DD.cpp:3825-3840) for the scenario subproblem.
+// A second kernel writes the cutset children as frontier records.
+//
+// Bit-exactness: only IEEE adds, compares and std::max/std::min-style selects are used,
+// in the reference's order (ties resolved exactly like the sequential folds); the file is
+// compiled with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "dd_device.hpp"
+
+namespace sgufp {
+
+#define DMIN (-__DBL_MAX__)
+#define DMAX (__DBL_MAX__)
+
+constexpr uint32_t kCollapseWidth = 120;  // RELAXED_MAX_WIDTH (DD.h:732)
+
+__device__ __forceinline__ int lane() { return (int)threadIdx.x; }
+__device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }  // std::max
+__device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b : a; }  // std::min
+
+// LDS is in order within a wavefront; this only stops the compiler from moving
+// LDS accesses across the point (the workgroup is a single wave).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// Global-memory hand-off between lanes of the wave (stores complete, then loads).
+__device__ __forceinline__ void wave_mem_sync() { __syncthreads(); }
+
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        uint32_t y = __shfl_up(x, d, kWave);
+        if (lane() >= d) x += y;
+    }
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+    for (int d = kWave / 2; d; d >>= 1) x += __shfl_xor(x, d, kWave);
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_or(uint32_t x) {
+#pragma unroll
+    for (int d = kWave / 2; d; d >>= 1) x |= __shfl_xor(x, d, kWave);
+    return x;
+}
+
+// (value, priority) arg-max.  A sequential std::max fold keeps either the newer or the
+// older of two equal values; equal doubles differ only in the sign of zero, and the
+// priority reproduces which one the fold would keep.
+struct VP {
+    double v;
+    int p;  // INT_MIN = empty
+};
+__device__ __forceinline__ VP vp_pick(VP a, VP b) {
+    if (b.p == INT_MIN) return a;
+    if (a.p == INT_MIN) return b;
+    if (a.v > b.v) return a;
+    if (b.v > a.v) return b;
+    return (a.p > b.p) ? a : b;
+}
+__device__ __forceinline__ VP wave_vp(VP x) {
+#pragma unroll
+    for (int d = kWave / 2; d; d >>= 1) {
+        VP y;
+        y.v = __shfl_xor(x.v, d, kWave);
+        y.p = __shfl_xor(x.p, d, kWave);
+        x = vp_pick(x, y);
+    }
+    return x;
+}
+// fold "acc = max(x_k, acc)" (new element wins ties) -> priority k;
+// fold "acc = max(acc, x_k)" (old element wins ties) -> priority -k-2.
+__device__ __forceinline__ int prio_new(int k) { return k; }
+__device__ __forceinline__ int prio_old(int k) { return -k - 2; }
+
+// ------------------------------------------------------------------------------------
+// Per-DD view: the layer table lives in LDS for the lifetime of the kernel, the
+// node/arc arrays in this slot's HBM scratch.
+struct DD {
+    // LDS
+    uint32_t *noff, *nn, *nalive, *aoff, *acnt;
+    int32_t *rslot;
+    double *buf0, *buf1;
+    double *coef;     // [kMaxU] per-rank coefficients of the layer being swept
+    int16_t *walk;    // [Tcap] decisions collected by a path walk
+    // HBM (slot base applied)
+    uint32_t *ntopo;
+    uint8_t *nflag;
+    uint32_t *nmask;
+    uint32_t *outcnt;
+    double *s2;
+    double *tw;
+    uint32_t *atopo;
+    uint8_t *aflag;
+    // scalars
+    int g, len, T, exact, aligned;
+};
+
+struct LdsCarve {
+    size_t bytes;
+    size_t o_lay, o_rslot, o_buf, o_coef, o_walk;
+};
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+__host__ __device__ inline LdsCarve lds_carve(int Tcap, int Lcap) {
+    LdsCarve c;
+    size_t o = 0;
+    c.o_lay = o; o = align16(o + (size_t)Tcap * 5 * 4);
+    c.o_rslot = o; o = align16(o + (size_t)Lcap * 4);
+    c.o_buf = o; o = align16(o + (size_t)2 * kLdsWidth * 8);
+    c.o_coef = o; o = align16(o + (size_t)kMaxU * 8);
+    c.o_walk = o; o = align16(o + (size_t)Tcap * 2);
+    c.bytes = o;
+    return c;
+}
+
+__device__ inline void dd_bind(DD &d, uint8_t *smem, const Scratch &sc, int slot) {
+    LdsCarve c = lds_carve(sc.Tcap, sc.Lcap);
+    uint32_t *lay = (uint32_t *)(smem + c.o_lay);
+    d.noff = lay;
+    d.nn = lay + sc.Tcap;
+    d.nalive = lay + 2 * sc.Tcap;
+    d.aoff = lay + 3 * sc.Tcap;
+    d.acnt = lay + 4 * sc.Tcap;
+    d.rslot = (int32_t *)(smem + c.o_rslot);
+    d.buf0 = (double *)(smem + c.o_buf);
+    d.buf1 = d.buf0 + kLdsWidth;
+    d.coef = (double *)(smem + c.o_coef);
+    d.walk = (int16_t *)(smem + c.o_walk);
+    size_t N = (size_t)slot * sc.Ncap, A = (size_t)slot * sc.Acap;
+    d.ntopo = sc.ntopo + N;
+    d.nflag = sc.nflag + N;
+    d.nmask = sc.nmask + N;
+    d.outcnt = sc.outcnt + N;
+    d.s2 = sc.s2 + N;
+    d.tw = sc.tw + N;
+    d.atopo = sc.atopo + A;
+    d.aflag = sc.aflag + A;
+}
+
+// Coefficient slot of state rank r at DD layer k (arc from tree layer k-1 into k).
+// Structural layer (decides which decision the rank is) = g+k-1; coefficient layer
+// (decides the key's (q, i)) = sol_len+k-1, exactly the reference's running index
+// `i` (DD.cpp:3940,3952) -- the two differ only for records whose solution vector
+// is shorter than their global layer.
+__device__ inline int rank_slot(const NetDev &net, const DD &d, int k, int r) {
+    int ls = d.g + k - 1;
+    if (d.aligned) return net.slot_tab[ls * kMaxU + r];
+    int u = net.layer_universe[ls];
+    if (u < 0 || r >= net.set_len[u]) return -1;
+    int dec = net.set_val[net.set_off[u] + r];
+    if (dec < 0) return -1;
+    int lc = d.len + k - 1;
+    int j = net.arc_head[dec];
+    for (int s = net.slot_off[lc]; s < net.slot_off[lc + 1]; s++)
+        if (net.slot_head[s] == j) return s;
+    return net.n_slots;
+}
+
+__device__ inline int16_t rank_value(const NetDev &net, int layer, int r) {
+    int u = net.layer_universe[layer];
+    return net.set_val[net.set_off[u] + r];
+}
+
+// Arc weight as the reference stores it: the coefficient of the last swept cut,
+// 0 before any cut and always 0 for a -1 decision (DD.cpp:3559-3560, 3866-3868).
+__device__ inline double arc_weight(const NetDev &net, const DD &d, int k, int r, const double *row) {
+    if (!row || r == 0) return 0.0;
+    int s = rank_slot(net, d, k, r);
+    return s >= 0 ? row[s] : 0.0;
+}
+
+// per-layer coefficient table in LDS: coef[r] for every rank
+__device__ inline void load_layer_coef(const NetDev &net, const DD &d, int k, const double *row) {
+    if (lane() < kMaxU) {
+        int s = (lane() == 0) ? -1 : rank_slot(net, d, k, lane());
+        d.coef[lane()] = s >= 0 ? row[s] : 0.0;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Build (buildTree + buildNextLayer).  Returns false on capacity overflow.
+__device__ bool dd_build(const NetDev &net, DD &d, const Scratch &sc, uint32_t root_mask, uint32_t &n_nodes,
+                         uint32_t &n_arcs) {
+    const int L = net.L;
+    if (lane() == 0) {
+        d.ntopo[0] = kNoRank << kRankShift;
+        d.nflag[0] = kAlive | kInAlive;
+        d.nmask[0] = root_mask;
+        d.s2[0] = DMIN;
+        d.noff[0] = 0; d.nn[0] = 1; d.nalive[0] = 1; d.aoff[0] = 0; d.acnt[0] = 0;
+    }
+    wave_mem_sync();
+    uint32_t total_nodes = 1, total_arcs = 0, merged_nodes = 0;
+    uint32_t next_size = 0;
+    int idx = 0;
+    int exact = 1;
+    bool ok = true;
+    for (int a = d.g; a < L; a++, idx++) {
+        if (idx + 2 > sc.Tcap) { ok = false; break; }
+        const uint32_t cnoff = d.noff[idx], cn = d.nn[idx];
+        const int upd = net.layer_update[a];
+        if (upd >= 0) {  // stateUpdateMap.contains(a): every current-layer node takes the full set
+            const int sl = net.set_len[upd];
+            const uint32_t full = (sl >= 32) ? 0xFFFFFFFFu : ((1u << sl) - 1u);
+            for (uint32_t i = lane(); i < cn; i += kWave) d.nmask[cnoff + i] = full;
+            next_size = cn * (uint32_t)sl;
+            wave_mem_sync();
+        }
+        if (next_size >= kCollapseWidth && (unsigned)(d.g + idx) < net.L5) {
+            // collapse into one node; one arc per (parent, state) in order
+            exact = 0;
+            const uint32_t mnode = total_nodes, base_arc = total_arcs;
+            uint32_t carry = 0, uni = 0;
+            for (uint32_t base = 0; base < cn; base += kWave) {
+                uint32_t i = base + lane();
+                bool valid = i < cn;
+                uint32_t m = valid ? d.nmask[cnoff + i] : 0u;
+                uint32_t c = __popc(m);
+                uint32_t incl = wave_scan_incl(c);
+                uint32_t off = base_arc + carry + incl - c;
+                if (valid && off + c <= (uint32_t)sc.Acap) {
+                    uint32_t t = 0, mm = m;
+                    while (mm) {
+                        uint32_t r = __ffs(mm) - 1;
+                        mm &= mm - 1;
+                        d.atopo[off + t] = i | (r << kRankShift);
+                        d.aflag[off + t] = kAlive;
+                        t++;
+                    }
+                    d.outcnt[cnoff + i] = c;
+                }
+                uni |= m;
+                carry += __shfl(incl, kWave - 1, kWave);
+            }
+            uni = wave_or(uni);
+            if (base_arc + carry > (uint32_t)sc.Acap || mnode + 1 > (uint32_t)sc.Ncap) { ok = false; break; }
+            if (lane() == 0) {
+                d.ntopo[mnode] = kNoRank << kRankShift;
+                d.nflag[mnode] = kAlive | kInAlive;
+                d.nmask[mnode] = uni;
+                d.s2[mnode] = DMIN;
+                d.noff[idx + 1] = mnode; d.nn[idx + 1] = 1; d.nalive[idx + 1] = 1;
+                d.aoff[idx + 1] = base_arc; d.acnt[idx + 1] = carry;
+            }
+            total_nodes += 1;
+            merged_nodes += 1;
+            total_arcs += carry;
+            next_size = __popc(uni);
+        } else {
+            // exact expansion: one child per (parent, state), child states = parent minus decision
+            const uint32_t first = total_nodes;
+            uint32_t carry = 0, ns = 0;
+            for (uint32_t base = 0; base < cn; base += kWave) {
+                uint32_t i = base + lane();
+                bool valid = i < cn;
+                uint32_t m = valid ? d.nmask[cnoff + i] : 0u;
+                uint32_t c = __popc(m);
+                uint32_t incl = wave_scan_incl(c);
+                uint32_t off = first + carry + incl - c;
+                uint32_t has0 = m & 1u;
+                uint32_t cs = has0 ? c + (c - 1) * (c - 1) : c * (c ? c - 1 : 0);
+                if (valid && off + c <= (uint32_t)sc.Ncap) {
+                    uint32_t t = 0, mm = m;
+                    while (mm) {
+                        uint32_t r = __ffs(mm) - 1;
+                        mm &= mm - 1;
+                        uint32_t ch = off + t;
+                        d.ntopo[ch] = i | (r << kRankShift);
+                        d.nflag[ch] = kAlive | kInAlive;
+                        d.nmask[ch] = (r == 0) ? m : (m & ~(1u << r));
+                        d.s2[ch] = DMIN;
+                        t++;
+                    }
+                    d.outcnt[cnoff + i] = c;
+                }
+                ns += wave_sum(valid ? cs : 0u);
+                carry += __shfl(incl, kWave - 1, kWave);
+            }
+            if (first + carry > (uint32_t)sc.Ncap) { ok = false; break; }
+            if (lane() == 0) {
+                d.noff[idx + 1] = first; d.nn[idx + 1] = carry; d.nalive[idx + 1] = carry;
+                d.aoff[idx + 1] = 0; d.acnt[idx + 1] = 0;
+            }
+            total_nodes += carry;
+            next_size = ns;
+        }
+        wave_mem_sync();
+    }
+    if (!ok) return false;
+    d.T = idx + 1;
+    d.exact = exact;
+    // terminal arcs: weight DOUBLE_MAX (DD.cpp:3587-3597); one out-arc per last-layer node
+    const uint32_t lo = d.noff[d.T - 1], ln = d.nn[d.T - 1];
+    for (uint32_t i = lane(); i < ln; i += kWave) {
+        d.tw[lo + i] = DMAX;
+        d.outcnt[lo + i] = 1;
+    }
+    n_nodes = total_nodes + 1;                                            // + terminal
+    n_arcs = (total_nodes - 1 - merged_nodes) + total_arcs + ln;          // exact in-arcs + merged + terminal
+    wave_mem_sync();
+    return true;
+}
+
+// ------------------------------------------------------------------------------------
+// One cut sweep over layers 1..T-1 (the shared body of both apply functions).
+__device__ void dd_sweep(const NetDev &net, DD &d, const double *row, double root_value) {
+    if (lane() == 0) {
+        d.s2[0] = root_value;
+        d.buf0[0] = root_value;
+    }
+    wave_lds_sync();
+    for (int k = 1; k < d.T; k++) {
+        const uint32_t noff = d.noff[k], n = d.nn[k];
+        const uint32_t pnoff = d.noff[k - 1], pn = d.nn[k - 1];
+        const bool prev_lds = pn <= (uint32_t)kLdsWidth;
+        const bool cur_lds = n <= (uint32_t)kLdsWidth;
+        double *pbuf = (k & 1) ? d.buf0 : d.buf1;
+        double *cbuf = (k & 1) ? d.buf1 : d.buf0;
+        load_layer_coef(net, d, k, row);
+        wave_lds_sync();
+        const uint32_t acnt = d.acnt[k];
+        if (acnt) {
+            // merged node: max over its alive incoming arcs, in creation order
+            const uint32_t aoff = d.aoff[k];
+            VP best{0.0, INT_MIN};
+            for (uint32_t base = 0; base < acnt; base += kWave) {
+                uint32_t a = base + lane();
+                if (a < acnt && (d.aflag[aoff + a] & kAlive)) {
+                    uint32_t t = d.atopo[aoff + a];
+                    uint32_t p = t & kParentMask, r = t >> kRankShift;
+                    double x = prev_lds ? pbuf[p] : d.s2[pnoff + p];
+                    VP c;
+                    if (r != 0) { c.v = x + d.coef[r]; c.p = prio_new((int)a); }
+                    else { c.v = x; c.p = prio_old((int)a); }
+                    best = vp_pick(best, c);
+                }
+            }
+            best = wave_vp(best);
+            double v = (best.p == INT_MIN) ? DMIN : smax(best.v, DMIN);
+            // an empty fold leaves DOUBLE_MIN; a -1 arc equal to DOUBLE_MIN keeps the initial value (same bits)
+            if (lane() == 0) {
+                d.s2[noff] = v;
+                cbuf[0] = v;
+            }
+        } else {
+            for (uint32_t base = 0; base < n; base += kWave) {
+                uint32_t i = base + lane();
+                if (i < n) {
+                    uint32_t node = noff + i;
+                    uint8_t f = d.nflag[node];
+                    if (f & kAlive) {
+                        uint32_t t = d.ntopo[node];
+                        uint32_t p = t & kParentMask, r = t >> kRankShift;
+                        double x;
+                        if (!(f & kInAlive)) x = DMIN;
+                        else {
+                            x = prev_lds ? pbuf[p] : d.s2[pnoff + p];
+                            if (r != 0) x = x + d.coef[r];
+                        }
+                        d.s2[node] = x;
+                        if (cur_lds) cbuf[i] = x;
+                    }
+                }
+            }
+        }
+        if (!cur_lds || !prev_lds) wave_mem_sync();
+        else wave_lds_sync();
+    }
+    wave_mem_sync();
+}
+
+// arg-max with first-wins ties over alive nodes of layer k; value getter by functor
+template <typename F>
+__device__ inline VP layer_max_first(const DD &d, int k, F val) {
+    const uint32_t noff = d.noff[k], n = d.nn[k];
+    VP best{0.0, INT_MIN};
+    for (uint32_t base = 0; base < n; base += kWave) {
+        uint32_t i = base + lane();
+        if (i < n && (d.nflag[noff + i] & kAlive)) best = vp_pick(best, VP{val(noff + i), prio_old((int)i)});
+    }
+    return wave_vp(best);
+}
+
+// the single alive node of a width-1 layer
+__device__ inline uint32_t layer_single(const DD &d, int k) {
+    const uint32_t noff = d.noff[k], n = d.nn[k];
+    uint32_t found = 0xFFFFFFFFu;
+    for (uint32_t base = 0; base < n; base += kWave) {
+        uint32_t i = base + lane();
+        uint64_t b = __ballot(i < n && (d.nflag[noff + i] & kAlive));
+        if (b) { found = noff + base + (uint32_t)(__ffsll((unsigned long long)b) - 1); break; }
+    }
+    return found;
+}
+
+// Width-1 arc pruning over layers [first, end) (DD.cpp:3895-3928, 3987-4021).
+// Returns false when a width-1 layer would lose all of its incoming arcs.
+__device__ bool dd_prune(const NetDev &net, DD &d, const double *row, int first, int end, double thresh) {
+    const int last = d.T - 1;
+    VP mx = layer_max_first(d, last, [&](uint32_t node) { return d.s2[node]; });
+    const double maxState = (mx.p == INT_MIN) ? DMIN : smax(DMIN, mx.v);
+    for (int k = first; k < end; k++) {
+        if (d.nalive[k] != 1) continue;
+        const uint32_t M = layer_single(d, k);
+        const double gain = maxState - d.s2[M];
+        const uint32_t pnoff = d.noff[k - 1];
+        load_layer_coef(net, d, k, row);
+        wave_lds_sync();
+        const uint32_t acnt = d.acnt[k];
+        uint32_t total = 0, pruned = 0;
+        if (acnt) {
+            const uint32_t aoff = d.aoff[k];
+            for (uint32_t base = 0; base < acnt; base += kWave) {
+                uint32_t a = base + lane();
+                bool alive = a < acnt && (d.aflag[aoff + a] & kAlive);
+                bool pr = false;
+                if (alive) {
+                    uint32_t t = d.atopo[aoff + a];
+                    uint32_t p = t & kParentMask, r = t >> kRankShift;
+                    double w = (r == 0) ? 0.0 : d.coef[r];
+                    pr = ((d.s2[pnoff + p] + w) + gain) <= thresh;
+                    if (pr) {
+                        d.aflag[aoff + a] = 0;
+                        atomicSub(&d.outcnt[pnoff + p], 1u);
+                    }
+                }
+                total += wave_sum(alive ? 1u : 0u);
+                pruned += wave_sum(pr ? 1u : 0u);
+            }
+        } else {
+            uint32_t t = d.ntopo[M];
+            uint8_t f = d.nflag[M];
+            uint32_t p = t & kParentMask, r = t >> kRankShift;
+            if (f & kInAlive) {
+                total = 1;
+                double w = (r == 0) ? 0.0 : d.coef[r];
+                if (((d.s2[pnoff + p] + w) + gain) <= thresh) {
+                    pruned = 1;
+                    if (lane() == 0) {
+                        d.nflag[M] = f & (uint8_t)~kInAlive;
+                        d.outcnt[pnoff + p] -= 1u;
+                    }
+                }
+            }
+        }
+        wave_mem_sync();
+        if (total == pruned) return false;
+    }
+    return true;
+}
+
+// applyFeasibilityCut after the sweep: last-layer removal + cascade, then pruning.
+__device__ bool dd_post_feasibility(const NetDev &net, DD &d, const double *row) {
+    const int last = d.T - 1;
+    const uint32_t lo = d.noff[last], ln = d.nn[last];
+    uint32_t rm = 0;
+    for (uint32_t base = 0; base < ln; base += kWave) {
+        uint32_t i = base + lane();
+        bool kill = false;
+        if (i < ln) {
+            uint8_t f = d.nflag[lo + i];
+            if ((f & kAlive) && d.s2[lo + i] < -0.01) {
+                kill = true;
+                d.nflag[lo + i] = f | kKill;
+            }
+        }
+        rm += wave_sum(kill ? 1u : 0u);
+    }
+    if (rm == d.nalive[last]) return false;
+    if (rm) {
+        wave_mem_sync();
+        // bottom-up deletion: a parent dies when its last alive out-arc dies in this batch
+        for (int k = last; k >= 1; k--) {
+            const uint32_t noff = d.noff[k], n = d.nn[k], pnoff = d.noff[k - 1];
+            const uint32_t acnt = d.acnt[k];
+            uint32_t killed = 0, parent_killed = 0;
+            if (acnt) {
+                const uint32_t M = noff;
+                if (d.nflag[M] & kKill) {
+                    killed = 1;
+                    const uint32_t aoff = d.aoff[k];
+                    for (uint32_t base = 0; base < acnt; base += kWave) {
+                        uint32_t a = base + lane();
+                        bool pk = false;
+                        if (a < acnt && (d.aflag[aoff + a] & kAlive)) {
+                            uint32_t p = d.atopo[aoff + a] & kParentMask;
+                            d.aflag[aoff + a] = 0;
+                            if (atomicSub(&d.outcnt[pnoff + p], 1u) == 1u) {
+                                d.nflag[pnoff + p] |= kKill;
+                                pk = true;
+                            }
+                        }
+                        parent_killed += wave_sum(pk ? 1u : 0u);
+                    }
+                    wave_mem_sync();
+                    if (lane() == 0) d.nflag[M] = 0;
+                }
+            } else {
+                for (uint32_t base = 0; base < n; base += kWave) {
+                    uint32_t i = base + lane();
+                    bool kk = false, pk = false;
+                    if (i < n) {
+                        uint8_t f = d.nflag[noff + i];
+                        if (f & kKill) {
+                            kk = true;
+                            if (f & kInAlive) {
+                                uint32_t p = d.ntopo[noff + i] & kParentMask;
+                                // exactly one decrement sees 1: that lane marks the parent
+                                if (atomicSub(&d.outcnt[pnoff + p], 1u) == 1u) {
+                                    d.nflag[pnoff + p] |= kKill;
+                                    pk = true;
+                                }
+                            }
+                            d.nflag[noff + i] = 0;
+                        }
+                    }
+                    killed += wave_sum(kk ? 1u : 0u);
+                    parent_killed += wave_sum(pk ? 1u : 0u);
+                }
+            }
+            if (lane() == 0) d.nalive[k] -= killed;
+            wave_mem_sync();
+            if (!parent_killed) break;
+        }
+    }
+    if (!d.exact) return dd_prune(net, d, row, 1, last, -0.01);
+    return true;
+}
+
+// applyOptimalityCut after the sweep.  Returns the terminal state (or DOUBLE_MIN).
+__device__ double dd_post_optimality(const NetDev &net, DD &d, const double *row, double optimal) {
+    const int last = d.T - 1;
+    const uint32_t lo = d.noff[last], ln = d.nn[last];
+    VP best{0.0, INT_MIN};
+    for (uint32_t base = 0; base < ln; base += kWave) {
+        uint32_t i = base + lane();
+        if (i < ln && (d.nflag[lo + i] & kAlive)) {
+            double w = smin(d.tw[lo + i], d.s2[lo + i]);
+            d.tw[lo + i] = w;
+            best = vp_pick(best, VP{w, prio_old((int)i)});
+        }
+    }
+    best = wave_vp(best);
+    const double term = (best.p == INT_MIN) ? DMIN : smax(DMIN, best.v);
+    wave_mem_sync();
+    if (term <= optimal) return term;
+    if (!d.exact) {
+        if (!dd_prune(net, d, row, 3, last - 1, optimal - 0.01)) return DMIN;
+    }
+    return term;
+}
+
+// getPathForNode (DD.cpp:3796-3820): walk up, first in-arc whose parent.state2 + weight
+// equals this node's state2; if none matches, continue through the first in-arc
+// without recording a decision.  Decisions land in d.walk (bottom-up); returns count.
+__device__ int dd_walk(const NetDev &net, DD &d, uint32_t node, int k, const double *row) {
+    int cnt = 0;
+    while (k > 0) {
+        const uint32_t pnoff = d.noff[k - 1];
+        const double cur = d.s2[node];
+        const uint32_t acnt = d.acnt[k];
+        uint32_t parent;
+        int found = 0;
+        int16_t dec = 0;
+        if (acnt) {
+            const uint32_t aoff = d.aoff[k];
+            uint32_t first_alive = 0xFFFFFFFFu, match = 0xFFFFFFFFu;
+            for (uint32_t base = 0; base < acnt && match == 0xFFFFFFFFu; base += kWave) {
+                uint32_t a = base + lane();
+                bool alive = a < acnt && (d.aflag[aoff + a] & kAlive);
+                bool hit = false;
+                if (alive) {
+                    uint32_t t = d.atopo[aoff + a];
+                    uint32_t p = t & kParentMask, r = t >> kRankShift;
+                    hit = (d.s2[pnoff + p] + arc_weight(net, d, k, (int)r, row)) == cur;
+                }
+                uint64_t ba = __ballot(alive), bh = __ballot(hit);
+                if (first_alive == 0xFFFFFFFFu && ba) first_alive = base + (uint32_t)(__ffsll((unsigned long long)ba) - 1);
+                if (bh) match = base + (uint32_t)(__ffsll((unsigned long long)bh) - 1);
+            }
+            uint32_t pick = (match != 0xFFFFFFFFu) ? match : first_alive;
+            if (pick == 0xFFFFFFFFu) break;  // no incoming arc left (reference: UB)
+            uint32_t t = d.atopo[d.aoff[k] + pick];
+            parent = pnoff + (t & kParentMask);
+            if (match != 0xFFFFFFFFu) {
+                found = 1;
+                dec = rank_value(net, d.g + k - 1, (int)(t >> kRankShift));
+            }
+        } else {
+            uint32_t t = d.ntopo[node];
+            uint32_t p = t & kParentMask, r = t >> kRankShift;
+            parent = pnoff + p;
+            if ((d.s2[parent] + arc_weight(net, d, k, (int)r, row)) == cur) {
+                found = 1;
+                dec = rank_value(net, d.g + k - 1, (int)r);
+            }
+        }
+        if (found) {
+            if (lane() == 0) d.walk[cnt] = dec;
+            cnt++;
+        }
+        node = parent;
+        k--;
+    }
+    wave_lds_sync();
+    return cnt;
+}
+
+__device__ inline void load_meta_layers(DD &d, const Scratch &sc, int slot) {
+    const int32_t *meta = sc.meta + (size_t)slot * 8;
+    d.g = meta[0]; d.len = meta[1]; d.T = meta[2]; d.exact = meta[3]; d.aligned = meta[4];
+    const uint32_t *lay = sc.lay + (size_t)slot * sc.Tcap * 5;
+    for (int k = lane(); k < d.T; k += kWave) {
+        d.noff[k] = lay[k]; d.nn[k] = lay[sc.Tcap + k]; d.nalive[k] = lay[2 * sc.Tcap + k];
+        d.aoff[k] = lay[3 * sc.Tcap + k]; d.acnt[k] = lay[4 * sc.Tcap + k];
+    }
+    wave_mem_sync();
+}
+
+__device__ inline void store_meta_layers(const DD &d, const Scratch &sc, int slot, int last_cut, int status,
+                                         int cut_layer, double ub) {
+    int32_t *meta = sc.meta + (size_t)slot * 8;
+    if (lane() == 0) {
+        meta[0] = d.g; meta[1] = d.len; meta[2] = d.T; meta[3] = d.exact; meta[4] = d.aligned;
+        meta[5] = last_cut; meta[6] = status; meta[7] = cut_layer;
+        sc.ubv[slot] = ub;
+    }
+    uint32_t *lay = sc.lay + (size_t)slot * sc.Tcap * 5;
+    for (int k = lane(); k < d.T; k += kWave) {
+        lay[k] = d.noff[k]; lay[sc.Tcap + k] = d.nn[k]; lay[2 * sc.Tcap + k] = d.nalive[k];
+        lay[3 * sc.Tcap + k] = d.aoff[k]; lay[4 * sc.Tcap + k] = d.acnt[k];
+    }
+}
+
+// root fold of 64 cuts at once: lane c folds cut order[c0 + c] over the root solution
+__device__ inline double root_fold(const Pool &pool, const int32_t *order, int cnt, int c0, const DD &d) {
+    int c = c0 + lane();
+    double v = 0.0;
+    if (c < cnt) {
+        int id = order[c];
+        const double *row = pool.rows + (size_t)id * pool.stride;
+        v = pool.rhs[id];
+        for (int t = 0; t < d.len; t++) {
+            int s = d.rslot[t];
+            if (s >= 0) v = v + row[s];
+        }
+    }
+    return v;
+}
+
+// exact DD: argmax terminal arc (strict >, first wins) then the path of its tail
+__device__ int dd_solution_path(const NetDev &net, DD &d, const double *row, int16_t *out_path,
+                                const int16_t *rsol) {
+    const int last = d.T - 1;
+    const uint32_t lo = d.noff[last], ln = d.nn[last];
+    VP best{0.0, INT_MIN};
+    for (uint32_t base = 0; base < ln; base += kWave) {
+        uint32_t i = base + lane();
+        if (i < ln && (d.nflag[lo + i] & kAlive)) best = vp_pick(best, VP{d.tw[lo + i], prio_old((int)i)});
+    }
+    best = wave_vp(best);
+    uint32_t node = 0;
+    int k = 0;
+    if (best.p != INT_MIN && best.v > DMIN) {
+        node = lo + (uint32_t)(-best.p - 2);
+        k = last;
+    }
+    int cnt = dd_walk(net, d, node, k, row);
+    for (int t = lane(); t < d.len; t += kWave) out_path[t] = rsol[t];
+    for (int t = lane(); t < cnt; t += kWave) out_path[d.len + t] = d.walk[cnt - 1 - t];
+    return d.len + cnt;
+}
+
+// ------------------------------------------------------------------------------------
+// Kernel 1: build + pool sweeps + finish, one wave per open node.
+__global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn in, Pool pool, BatchOut out,
+                                                double incumbent) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int slot = blockIdx.x;
+    if (slot >= in.n) return;
+    DD d;
+    dd_bind(d, smem, sc, slot);
+    d.g = in.gl[slot];
+    d.len = in.sol_len[slot];
+    const int16_t *rsol = in.sol + in.sol_off[slot];
+    d.aligned = (d.len == d.g) ? 1 : 0;
+    int status = kSuccess, last_cut = -1, cut_layer = 0;
+    double ub = in.ub[slot], lb = DMIN;
+    uint32_t nchild = 0, sweeps = 0, n_nodes = 0, n_arcs = 0;
+    d.T = 1; d.exact = 1;
+
+    if (!in.valid[slot] || d.len > d.g || d.g > net.L || d.len > sc.Lcap) {
+        status = kErrRecord;
+        goto done;
+    }
+    // coefficient slots of the root solution (layer t, decision sol[t])
+    for (int t = lane(); t < d.len; t += kWave) {
+        int dec = rsol[t];
+        int s = -1;
+        if (dec != -1) {
+            s = net.n_slots;
+            if (dec >= 0 && dec < net.m) {
+                int j = net.arc_head[dec];
+                for (int q = net.slot_off[t]; q < net.slot_off[t + 1]; q++)
+                    if (net.slot_head[q] == j) { s = q; break; }
+            }
+        }
+        d.rslot[t] = s;
+    }
+    if (!dd_build(net, d, sc, in.mask[slot], n_nodes, n_arcs)) {
+        status = kErrCapacity;
+        goto done;
+    }
+    {
+        // feasibility pool, newest first (NodeExplorer.cpp:935-938 / 975-978)
+        for (int c0 = 0; c0 < pool.nf; c0 += kWave) {
+            double rv = root_fold(pool, pool.f_order, pool.nf, c0, d);
+            int cnt = min(kWave, pool.nf - c0);
+            for (int j = 0; j < cnt; j++) {
+                int id = pool.f_order[c0 + j];
+                const double *row = pool.rows + (size_t)id * pool.stride;
+                dd_sweep(net, d, row, __shfl(rv, j, kWave));
+                last_cut = id;
+                sweeps++;
+                if (!dd_post_feasibility(net, d, row)) {
+                    status = kPrunedFeasibility;
+                    goto done;
+                }
+            }
+        }
+        // optimality pool, newest first (NodeExplorer.cpp:940-944 / 980-983)
+        for (int c0 = 0; c0 < pool.no; c0 += kWave) {
+            double rv = root_fold(pool, pool.o_order, pool.no, c0, d);
+            int cnt = min(kWave, pool.no - c0);
+            for (int j = 0; j < cnt; j++) {
+                int id = pool.o_order[c0 + j];
+                const double *row = pool.rows + (size_t)id * pool.stride;
+                dd_sweep(net, d, row, __shfl(rv, j, kWave));
+                last_cut = id;
+                sweeps++;
+                double v = dd_post_optimality(net, d, row, incumbent);
+                ub = d.exact ? v : smin(v, ub);
+                if (ub <= incumbent) {
+                    status = kPrunedOptimality;
+                    goto done;
+                }
+            }
+        }
+        const double *lrow = last_cut >= 0 ? pool.rows + (size_t)last_cut * pool.stride : nullptr;
+        if (d.exact) {
+            status = kNeedsSubproblem;
+            int plen = dd_solution_path(net, d, lrow, out.path + (size_t)slot * sc.Lcap, rsol);
+            if (lane() == 0) out.path_len[slot] = (uint16_t)plen;
+        } else {
+            int k = 3;
+            while (k < d.T && d.nalive[k] != 1) k++;
+            if (k >= d.T) {
+                status = kErrCutset;
+            } else {
+                cut_layer = k;
+                const uint32_t M = layer_single(d, k);
+                if (d.acnt[k]) {
+                    const uint32_t aoff = d.aoff[k], acnt = d.acnt[k];
+                    for (uint32_t base = 0; base < acnt; base += kWave) {
+                        uint32_t a = base + lane();
+                        nchild += wave_sum((a < acnt && (d.aflag[aoff + a] & kAlive)) ? 1u : 0u);
+                    }
+                } else {
+                    nchild = (d.nflag[M] & kInAlive) ? 1u : 0u;
+                }
+            }
+        }
+    }
+done:
+    if (status == kPrunedFeasibility || status == kPrunedOptimality || status >= kErrRecord) {
+        lb = DMIN;
+        ub = DMIN;
+    }
+    if (lane() == 0) {
+        out.status[slot] = status;
+        out.exact[slot] = (uint8_t)d.exact;
+        out.lb[slot] = lb;
+        out.ub[slot] = ub;
+        out.nchild[slot] = nchild;
+        out.sol_need[slot] = nchild * (uint32_t)(d.len + cut_layer);
+        out.dd_nodes[slot] = n_nodes;
+        out.dd_arcs[slot] = n_arcs;
+        out.dd_layers[slot] = (uint32_t)d.T + 1;
+        out.sweeps[slot] = sweeps;
+    }
+    store_meta_layers(d, sc, slot, last_cut, status, cut_layer, ub);
+}
+
+// ------------------------------------------------------------------------------------
+// Kernel 2: write cutset children (getCutset, DD.cpp:4179-4218) as frontier records.
+__global__ void __launch_bounds__(kWave) k_emit_children(NetDev net, Scratch sc, BatchIn in, Pool pool,
+                                                         BatchOut out, ChildOut co) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int slot = blockIdx.x;
+    if (slot >= in.n) return;
+    if (out.status[slot] != kSuccess || out.nchild[slot] == 0) return;
+    DD d;
+    dd_bind(d, smem, sc, slot);
+    load_meta_layers(d, sc, slot);
+    const int32_t *meta = sc.meta + (size_t)slot * 8;
+    const int last_cut = meta[5];
+    const int k = meta[7];
+    const double ub = sc.ubv[slot];
+    const double *row = last_cut >= 0 ? pool.rows + (size_t)last_cut * pool.stride : nullptr;
+    const int16_t *rsol = in.sol + in.sol_off[slot];
+    const int gl = d.g + k;
+    const int stride = d.len + k;
+    const bool changed = net.changed[gl] != 0;
+    uint32_t full = 0;
+    if (changed) {
+        int sl = net.set_len[net.layer_update[gl]];
+        full = (sl >= 32) ? 0xFFFFFFFFu : ((1u << sl) - 1u);
+    }
+    const uint64_t cbase = co.child_off[slot];
+    const uint64_t sbase = co.sol_base[slot];
+    const uint32_t pnoff = d.noff[k - 1];
+    const uint32_t M = layer_single(d, k);
+
+    // enumerate the alive in-arcs of M in order: (parent, rank)
+    const uint32_t acnt = d.acnt[k] ? d.acnt[k] : 1u;
+    uint32_t child = 0;
+    uint32_t cur_parent = 0xFFFFFFFFu;
+    int plen = 0;
+    for (uint32_t a = 0; a < acnt; a++) {
+        uint32_t p, r;
+        if (d.acnt[k]) {
+            if (!(d.aflag[d.aoff[k] + a] & kAlive)) continue;
+            uint32_t t = d.atopo[d.aoff[k] + a];
+            p = t & kParentMask;
+            r = t >> kRankShift;
+        } else {
+            if (!(d.nflag[M] & kInAlive)) continue;
+            uint32_t t = d.ntopo[M];
+            p = t & kParentMask;
+            r = t >> kRankShift;
+        }
+        if (p != cur_parent) {
+            cur_parent = p;
+            plen = dd_walk(net, d, pnoff + p, k - 1, row);
+        }
+        const uint64_t ci = cbase + child;
+        const int64_t so = (int64_t)(sbase + (uint64_t)child * (uint64_t)stride);
+        const int16_t dec = rank_value(net, d.g + k - 1, (int)r);
+        for (int t = lane(); t < d.len; t += kWave) co.sol[so + t] = rsol[t];
+        for (int t = lane(); t < plen; t += kWave) co.sol[so + d.len + t] = d.walk[plen - 1 - t];
+        if (lane() == 0) {
+            co.sol[so + d.len + plen] = dec;
+            uint32_t pm = d.nmask[pnoff + p];
+            co.gl[ci] = (uint16_t)gl;
+            co.lb[ci] = DMIN;
+            co.ub[ci] = ub;
+            co.mask[ci] = changed ? full : ((r == 0) ? pm : (pm & ~(1u << r)));
+            co.sol_off[ci] = so;
+            co.sol_len[ci] = (uint16_t)(d.len + plen + 1);
+        }
+        child++;
+        wave_lds_sync();
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Kernel 3: apply one freshly generated cut to exact DDs kept in their slots
+// (the refinement loop of NodeExplorer.cpp:946-969).
+__global__ void __launch_bounds__(kWave) k_refine(NetDev net, Scratch sc, BatchIn in, Pool pool, BatchOut out,
+                                                  const int32_t *slots, const int32_t *cut_ids,
+                                                  const uint8_t *cut_is_feas, int n, double incumbent) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int w = blockIdx.x;
+    if (w >= n) return;
+    const int slot = slots[w];
+    if (out.status[slot] != kNeedsSubproblem) return;
+    DD d;
+    dd_bind(d, smem, sc, slot);
+    load_meta_layers(d, sc, slot);
+    const int16_t *rsol = in.sol + in.sol_off[slot];
+    for (int t = lane(); t < d.len; t += kWave) {
+        int dec = rsol[t];
+        int s = -1;
+        if (dec != -1) {
+            s = net.n_slots;
+            if (dec >= 0 && dec < net.m) {
+                int j = net.arc_head[dec];
+                for (int q = net.slot_off[t]; q < net.slot_off[t + 1]; q++)
+                    if (net.slot_head[q] == j) { s = q; break; }
+            }
+        }
+        d.rslot[t] = s;
+    }
+    wave_lds_sync();
+    const int id = cut_ids[w];
+    const double *row = pool.rows + (size_t)id * pool.stride;
+    double rv = 0.0;
+    if (lane() == 0) {
+        rv = pool.rhs[id];
+        for (int t = 0; t < d.len; t++) {
+            int s = d.rslot[t];
+            if (s >= 0) rv = rv + row[s];
+        }
+    }
+    rv = __shfl(rv, 0, kWave);
+    dd_sweep(net, d, row, rv);
+    int status = kNeedsSubproblem;
+    double ub = sc.ubv[slot];
+    if (lane() == 0) out.sweeps[slot] += 1u;
+    if (cut_is_feas[w]) {
+        if (!dd_post_feasibility(net, d, row)) status = kPrunedFeasibility;
+    } else {
+        ub = dd_post_optimality(net, d, row, incumbent);
+        if (ub <= incumbent) status = kPrunedOptimality;
+    }
+    if (status == kNeedsSubproblem) {
+        int plen = dd_solution_path(net, d, row, out.path + (size_t)slot * sc.Lcap, rsol);
+        if (lane() == 0) out.path_len[slot] = (uint16_t)plen;
+    }
+    double lb = DMIN;
+    if (status != kNeedsSubproblem) ub = DMIN;
+    if (lane() == 0) {
+        out.status[slot] = status;
+        out.lb[slot] = lb;
+        out.ub[slot] = ub;
+    }
+    store_meta_layers(d, sc, slot, id, status, 0, ub);
+}
+
+// ------------------------------------------------------------------------------------
+// Exclusive scan of two u32 arrays into u64 offsets (n+1 entries), one 1024-thread block.
+__global__ void __launch_bounds__(1024) k_scan2(const uint32_t *a, const uint32_t *b, int n, uint64_t *oa,
+                                               uint64_t *ob) {
+    __shared__ uint64_t sa[1024], sb[1024];
+    const int t = threadIdx.x;
+    const int per = (n + 1023) / 1024;
+    const int lo = min(n, t * per), hi = min(n, lo + per);
+    uint64_t xa = 0, xb = 0;
+    for (int i = lo; i < hi; i++) { xa += a[i]; xb += b[i]; }
+    sa[t] = xa; sb[t] = xb;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        uint64_t ya = (t >= d) ? sa[t - d] : 0, yb = (t >= d) ? sb[t - d] : 0;
+        __syncthreads();
+        sa[t] += ya; sb[t] += yb;
+        __syncthreads();
+    }
+    uint64_t ra = sa[t] - xa, rb = sb[t] - xb;
+    for (int i = lo; i < hi; i++) {
+        oa[i] = ra; ob[i] = rb;
+        ra += a[i]; rb += b[i];
+    }
+    if (t == 1023) { oa[n] = sa[1023]; ob[n] = sb[1023]; }
+}
+
+// ------------------------------------------------------------------------------------
+// host-side launchers (called from capi.cpp)
+size_t relax_lds_bytes(int Tcap, int Lcap) { return lds_carve(Tcap, Lcap).bytes; }
+
+hipError_t launch_relax(const NetDev &net, const Scratch &sc, const BatchIn &in, const Pool &pool,
+                        const BatchOut &out, double incumbent, hipStream_t st) {
+    if (in.n <= 0) return hipSuccess;
+    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap);
+    hipLaunchKernelGGL(k_relax, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan(const uint32_t *a, const uint32_t *b, int n, uint64_t *oa, uint64_t *ob, hipStream_t st) {
+    hipLaunchKernelGGL(k_scan2, dim3(1), dim3(1024), 0, st, a, b, n, oa, ob);
+    return hipGetLastError();
+}
+
+hipError_t launch_emit(const NetDev &net, const Scratch &sc, const BatchIn &in, const Pool &pool,
+                       const BatchOut &out, const ChildOut &co, hipStream_t st) {
+    if (in.n <= 0) return hipSuccess;
+    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap);
+    hipLaunchKernelGGL(k_emit_children, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, co);
+    return hipGetLastError();
+}
+
+hipError_t launch_refine(const NetDev &net, const Scratch &sc, const BatchIn &in, const Pool &pool,
+                         const BatchOut &out, const int32_t *slots, const int32_t *cut_ids,
+                         const uint8_t *cut_is_feas, int n, double incumbent, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap);
+    hipLaunchKernelGGL(k_refine, dim3(n), dim3(kWave), lds, st, net, sc, in, pool, out, slots, cut_ids,
+                       cut_is_feas, n, incumbent);
+    return hipGetLastError();
+}
+
+}  // namespace sgufp

@@ -1,0 +1,344 @@
+"""ctypes binding of libsgufp_hip.so (include/sgufp_hip.h).
+
+The Python side is plumbing for tests, the bench and the multi-GPU driver; the
+relaxation itself runs in the HIP kernels.  There is deliberately no CPU fallback:
+if the library cannot be loaded the constructor raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .pools import NodeRecord, PoolCut, RelaxResult
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libsgufp_hip.so")
+
+SUCCESS, PRUNED_F, PRUNED_O, NEEDS_SUBPROBLEM = 0, 1, 2, 3
+ERR_RECORD, ERR_CAPACITY, ERR_CUTSET = 16, 17, 18
+
+EXPORTS = [
+    "sgufp_create_from_file", "sgufp_create", "sgufp_destroy", "sgufp_get_network_info",
+    "sgufp_processing_order", "sgufp_last_error", "sgufp_stream", "sgufp_cuts_append",
+    "sgufp_cuts_clear", "sgufp_cuts_count", "sgufp_batch_upload", "sgufp_batch_relax",
+    "sgufp_batch_sync", "sgufp_batch_results", "sgufp_batch_children_size", "sgufp_batch_children",
+    "sgufp_batch_paths", "sgufp_batch_stats", "sgufp_batch_refine", "sgufp_set_timing",
+    "sgufp_last_timing", "sgufp_probe_network",
+]
+
+
+class NetworkInfo(C.Structure):
+    _fields_ = [("n", C.c_int32), ("m", C.c_int32), ("scenarios", C.c_int32), ("total_layers", C.c_int32),
+                ("n_vbar", C.c_int32), ("max_states", C.c_int32), ("n_slots", C.c_int32),
+                ("max_batch", C.c_int32), ("node_capacity", C.c_int64), ("arc_capacity", C.c_int64),
+                ("scratch_bytes", C.c_int64)]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+    lib = C.CDLL(path)
+    P = C.c_void_p
+    lib.sgufp_create_from_file.restype = P
+    lib.sgufp_create_from_file.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_int)]
+    lib.sgufp_create.restype = P
+    lib.sgufp_destroy.argtypes = [P]
+    lib.sgufp_get_network_info.argtypes = [P, C.POINTER(NetworkInfo)]
+    lib.sgufp_processing_order.argtypes = [P, P, P]
+    lib.sgufp_last_error.restype = C.c_char_p
+    lib.sgufp_last_error.argtypes = [P]
+    lib.sgufp_stream.restype = P
+    lib.sgufp_stream.argtypes = [P]
+    lib.sgufp_cuts_append.argtypes = [P, C.c_int, C.c_int, P, P, P, P]
+    lib.sgufp_cuts_clear.argtypes = [P]
+    lib.sgufp_cuts_count.argtypes = [P, C.c_int]
+    lib.sgufp_batch_upload.argtypes = [P, C.c_int, P, P, P, P, P, P, P]
+    lib.sgufp_batch_relax.argtypes = [P, C.c_double]
+    lib.sgufp_batch_sync.argtypes = [P]
+    lib.sgufp_batch_results.argtypes = [P, P, P, P, P, P]
+    lib.sgufp_batch_children_size.argtypes = [P, P, P, P]
+    lib.sgufp_batch_children.argtypes = [P, P, P, P, P, P, P, P, P]
+    lib.sgufp_batch_paths.argtypes = [P, P, P]
+    lib.sgufp_batch_stats.argtypes = [P, P, P, P, P]
+    lib.sgufp_batch_refine.argtypes = [P, C.c_int, P, P, P, C.c_double]
+    lib.sgufp_set_timing.argtypes = [P, C.c_int]
+    lib.sgufp_last_timing.argtypes = [P, P, P]
+    lib.sgufp_probe_network.argtypes = [C.c_char_p, P, P, C.c_int32, P, P]
+    _lib = lib
+    return lib
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def key_of(q: int, i: int, j: int) -> int:
+    """Inavap::getKey (Cut.h:342-344)."""
+    return (q & 0xFFFF) | ((i & 0xFFFF) << 16) | ((j & 0xFFFF) << 32)
+
+
+def pack_cuts(cuts: Sequence[PoolCut]):
+    """cutToCut (Cut.h:406-421): (i,q,j) map order, zero coefficients dropped."""
+    rhs = np.array([c.rhs for c in cuts], dtype=np.float64)
+    off = [0]
+    keys: List[int] = []
+    vals: List[float] = []
+    for c in cuts:
+        for (i, q, j, v) in sorted(c.coeff, key=lambda t: (t[0], t[1], t[2])):
+            if v == 0.0:
+                continue
+            keys.append(key_of(q, i, j))
+            vals.append(v)
+        off.append(len(keys))
+    return rhs, np.array(off, dtype=np.int64), np.array(keys, dtype=np.uint64), np.array(vals, dtype=np.float64)
+
+
+def probe_network(path: str):
+    """Host-only parse through the product loader: (totalLayers, processingOrder arcs, V-bar order)."""
+    lib = load_library()
+    L, nv = C.c_int32(0), C.c_int32(0)
+    if lib.sgufp_probe_network(path.encode(), C.byref(L), C.byref(nv), 0, None, None) != 0:
+        raise RuntimeError(f"cannot parse {path}")
+    cap = max(L.value, nv.value, 1)
+    la = np.zeros(cap, dtype=np.int32)
+    vb = np.zeros(cap, dtype=np.int32)
+    lib.sgufp_probe_network(path.encode(), C.byref(L), C.byref(nv), cap, _ptr(la), _ptr(vb))
+    return L.value, la[:L.value].copy(), vb[:nv.value].copy()
+
+
+class BatchArrays:
+    """SoA view of a list of Inavap::Node records."""
+
+    def __init__(self, nodes: Sequence[NodeRecord]):
+        n = len(nodes)
+        self.n = n
+        self.gl = np.array([nd.gl for nd in nodes], dtype=np.uint16)
+        self.lb = np.array([nd.lb for nd in nodes], dtype=np.float64)
+        self.ub = np.array([nd.ub for nd in nodes], dtype=np.float64)
+        st_len = np.array([len(nd.states) for nd in nodes], dtype=np.int64)
+        so_len = np.array([len(nd.sol) for nd in nodes], dtype=np.int64)
+        self.states_off = np.zeros(n + 1, dtype=np.int64)
+        self.sol_off = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(st_len, out=self.states_off[1:])
+        np.cumsum(so_len, out=self.sol_off[1:])
+        self.states = np.array([s for nd in nodes for s in nd.states], dtype=np.int16)
+        self.sol = np.array([s for nd in nodes for s in nd.sol], dtype=np.int16)
+
+
+def batch_from_arrays(gl, lb, ub, states_off, states, sol_off, sol) -> BatchArrays:
+    b = BatchArrays.__new__(BatchArrays)
+    b.n = int(len(gl))
+    b.gl = np.ascontiguousarray(gl, dtype=np.uint16)
+    b.lb = np.ascontiguousarray(lb, dtype=np.float64)
+    b.ub = np.ascontiguousarray(ub, dtype=np.float64)
+    b.states_off = np.ascontiguousarray(states_off, dtype=np.int64)
+    b.states = np.ascontiguousarray(states, dtype=np.int16)
+    b.sol_off = np.ascontiguousarray(sol_off, dtype=np.int64)
+    b.sol = np.ascontiguousarray(sol, dtype=np.int16)
+    return b
+
+
+def batch_slice(b: BatchArrays, idx: np.ndarray) -> BatchArrays:
+    """Sub-batch of the records at positions ``idx`` (in that order)."""
+    idx = np.asarray(idx, dtype=np.int64)
+    st_len = b.states_off[idx + 1] - b.states_off[idx]
+    so_len = b.sol_off[idx + 1] - b.sol_off[idx]
+    st_off = np.zeros(len(idx) + 1, dtype=np.int64)
+    so_off = np.zeros(len(idx) + 1, dtype=np.int64)
+    np.cumsum(st_len, out=st_off[1:])
+    np.cumsum(so_len, out=so_off[1:])
+    st = np.concatenate([b.states[b.states_off[k]:b.states_off[k + 1]] for k in idx]) if len(idx) else b.states[:0]
+    so = np.concatenate([b.sol[b.sol_off[k]:b.sol_off[k + 1]] for k in idx]) if len(idx) else b.sol[:0]
+    return batch_from_arrays(b.gl[idx], b.lb[idx], b.ub[idx], st_off, st, so_off, so)
+
+
+def batch_concat(parts: Sequence[BatchArrays]) -> BatchArrays:
+    gl = np.concatenate([p.gl for p in parts])
+    lb = np.concatenate([p.lb for p in parts])
+    ub = np.concatenate([p.ub for p in parts])
+    st = np.concatenate([p.states for p in parts])
+    so = np.concatenate([p.sol for p in parts])
+    st_off = [np.zeros(1, dtype=np.int64)]
+    so_off = [np.zeros(1, dtype=np.int64)]
+    a = b_ = 0
+    for p in parts:
+        st_off.append(p.states_off[1:] + a)
+        so_off.append(p.sol_off[1:] + b_)
+        a += int(p.states_off[-1])
+        b_ += int(p.sol_off[-1])
+    return batch_from_arrays(gl, lb, ub, np.concatenate(st_off), st, np.concatenate(so_off), so)
+
+
+def batch_to_records(b: BatchArrays) -> List[NodeRecord]:
+    return [NodeRecord(int(b.gl[k]), float(b.lb[k]), float(b.ub[k]),
+                       [int(x) for x in b.states[b.states_off[k]:b.states_off[k + 1]]],
+                       [int(x) for x in b.sol[b.sol_off[k]:b.sol_off[k + 1]]]) for k in range(b.n)]
+
+
+class Engine:
+    """One device context: network tables, cut pools, a batch of DD slots."""
+
+    def __init__(self, network_path: str, device: int = 0, max_batch: int = 4096):
+        self.lib = load_library()
+        err = C.c_int(0)
+        self.ctx = self.lib.sgufp_create_from_file(network_path.encode(), device, max_batch, C.byref(err))
+        if not self.ctx:
+            raise RuntimeError(f"sgufp_create_from_file failed ({err.value})")
+        self.info = NetworkInfo()
+        self._check(self.lib.sgufp_get_network_info(self.ctx, C.byref(self.info)))
+        self.n_feas = 0
+        self.n_opt = 0
+        self.n = 0
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.sgufp_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int):
+        if rc != 0:
+            raise RuntimeError(f"sgufp call failed ({rc}): {self.lib.sgufp_last_error(self.ctx).decode()}")
+
+    # -- network -------------------------------------------------------------
+    def processing_order(self) -> Tuple[np.ndarray, np.ndarray]:
+        la = np.zeros(self.info.total_layers, dtype=np.int32)
+        vb = np.zeros(self.info.n_vbar, dtype=np.int32)
+        self._check(self.lib.sgufp_processing_order(self.ctx, _ptr(la), _ptr(vb)))
+        return la, vb
+
+    # -- cuts ----------------------------------------------------------------
+    def add_cuts(self, cuts: Sequence[PoolCut]):
+        """Append in insertion order, split by type (two Containers, DDSolver.h:415-416)."""
+        for t in (1, 0):
+            sel = [c for c in cuts if c.type == t]
+            if not sel:
+                continue
+            rhs, off, keys, vals = pack_cuts(sel)
+            self._check(self.lib.sgufp_cuts_append(self.ctx, t, len(sel), _ptr(rhs), _ptr(off), _ptr(keys), _ptr(vals)))
+            if t == 1:
+                self.n_feas += len(sel)
+            else:
+                self.n_opt += len(sel)
+
+    def clear_cuts(self):
+        self._check(self.lib.sgufp_cuts_clear(self.ctx))
+        self.n_feas = self.n_opt = 0
+
+    # -- batch ---------------------------------------------------------------
+    def upload(self, nodes: Sequence[NodeRecord] | BatchArrays):
+        b = nodes if isinstance(nodes, BatchArrays) else BatchArrays(nodes)
+        self._check(self.lib.sgufp_batch_upload(self.ctx, b.n, _ptr(b.gl), _ptr(b.lb), _ptr(b.ub), _ptr(b.states_off),
+                                                _ptr(b.states), _ptr(b.sol_off), _ptr(b.sol)))
+        self.n = b.n
+
+    def relax_async(self, incumbent: float):
+        self._check(self.lib.sgufp_batch_relax(self.ctx, C.c_double(incumbent)))
+
+    def sync(self):
+        self._check(self.lib.sgufp_batch_sync(self.ctx))
+
+    def set_timing(self, on: bool):
+        self._check(self.lib.sgufp_set_timing(self.ctx, 1 if on else 0))
+
+    def last_timing(self) -> Tuple[float, float]:
+        a, b = C.c_float(0), C.c_float(0)
+        self._check(self.lib.sgufp_last_timing(self.ctx, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def results_arrays(self):
+        n = self.n
+        st = np.zeros(n, dtype=np.int32)
+        ex = np.zeros(n, dtype=np.uint8)
+        lb = np.zeros(n, dtype=np.float64)
+        ub = np.zeros(n, dtype=np.float64)
+        nc = np.zeros(n, dtype=np.int32)
+        self._check(self.lib.sgufp_batch_results(self.ctx, _ptr(st), _ptr(ex), _ptr(lb), _ptr(ub), _ptr(nc)))
+        return st, ex, lb, ub, nc
+
+    def stats(self):
+        n = self.n
+        a = np.zeros(n, dtype=np.int64)
+        b = np.zeros(n, dtype=np.int64)
+        c = np.zeros(n, dtype=np.int32)
+        d = np.zeros(n, dtype=np.int32)
+        self._check(self.lib.sgufp_batch_stats(self.ctx, _ptr(a), _ptr(b), _ptr(c), _ptr(d)))
+        return a, b, c, d
+
+    def children_arrays(self):
+        n = self.n
+        nc, ns, nsol = C.c_int64(0), C.c_int64(0), C.c_int64(0)
+        self._check(self.lib.sgufp_batch_children_size(self.ctx, C.byref(nc), C.byref(ns), C.byref(nsol)))
+        k = nc.value
+        child_off = np.zeros(n + 1, dtype=np.int64)
+        gl = np.zeros(k, dtype=np.uint16)
+        lb = np.zeros(k, dtype=np.float64)
+        ub = np.zeros(k, dtype=np.float64)
+        soff = np.zeros(k + 1, dtype=np.int64)
+        states = np.zeros(max(ns.value, 1), dtype=np.int16)
+        poff = np.zeros(k + 1, dtype=np.int64)
+        sol = np.zeros(max(nsol.value, 1), dtype=np.int16)
+        self._check(self.lib.sgufp_batch_children(self.ctx, _ptr(child_off), _ptr(gl), _ptr(lb), _ptr(ub), _ptr(soff),
+                                                  _ptr(states), _ptr(poff), _ptr(sol)))
+        return child_off, gl, lb, ub, soff, states, poff, sol
+
+    def children_batch(self) -> BatchArrays:
+        """All cutset children of the last relaxed batch as a new batch (node order kept)."""
+        child_off, gl, lb, ub, soff, states, poff, sol = self.children_arrays()
+        return batch_from_arrays(gl, lb, ub, soff, states[:soff[-1]], poff, sol[:poff[-1]])
+
+    def paths(self):
+        n = self.n
+        off = np.zeros(n + 1, dtype=np.int64)
+        self._check(self.lib.sgufp_batch_paths(self.ctx, _ptr(off), None))
+        buf = np.zeros(max(int(off[-1]), 1), dtype=np.int16)
+        self._check(self.lib.sgufp_batch_paths(self.ctx, _ptr(off), _ptr(buf)))
+        return off, buf
+
+    def refine(self, node_idx: Sequence[int], is_feas: Sequence[int], cut_index: Sequence[int], incumbent: float):
+        ni = np.asarray(node_idx, dtype=np.int32)
+        fe = np.asarray(is_feas, dtype=np.uint8)
+        ci = np.asarray(cut_index, dtype=np.int32)
+        self._check(self.lib.sgufp_batch_refine(self.ctx, len(ni), _ptr(ni), _ptr(fe), _ptr(ci), C.c_double(incumbent)))
+
+    # -- convenience: NodeExplorer::process for a list of nodes ----------------
+    def relax(self, nodes: Sequence[NodeRecord], incumbent: float) -> List[RelaxResult]:
+        out: List[RelaxResult] = []
+        for s in range(0, len(nodes), self.info.max_batch):
+            chunk = nodes[s:s + self.info.max_batch]
+            self.upload(chunk)
+            self.relax_async(incumbent)
+            self.sync()
+            out.extend(self._collect())
+        return out
+
+    def _collect(self) -> List[RelaxResult]:
+        st, ex, lb, ub, nc = self.results_arrays()
+        dn, da, dl, _ = self.stats()
+        child_off, gl, clb, cub, soff, states, poff, sol = self.children_arrays()
+        p_off, pbuf = self.paths()
+        res = []
+        for k in range(self.n):
+            ch = []
+            for c in range(int(child_off[k]), int(child_off[k + 1])):
+                ch.append(NodeRecord(int(gl[c]), float(clb[c]), float(cub[c]),
+                                     [int(x) for x in states[soff[c]:soff[c + 1]]],
+                                     [int(x) for x in sol[poff[c]:poff[c + 1]]]))
+            path = [int(x) for x in pbuf[p_off[k]:p_off[k + 1]]]
+            res.append(RelaxResult(int(st[k]), int(ex[k]), float(lb[k]), float(ub[k]), ch, path,
+                                   int(dn[k]), int(da[k]), int(dl[k])))
+        return res

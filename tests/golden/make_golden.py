@@ -1,0 +1,134 @@
+"""Regenerate the golden fixtures from the reference compiled in this container.
+
+    make -C oracle            # builds oracle/_ref/ref_dd from /root/reference sources
+    python tests/golden/make_golden.py
+
+Each case directory holds the inputs (instance, cut pool, open nodes) and, per
+incumbent, the reference's NodeExplorer::process outcome for every node
+(ref_<k>.txt.gz, written by oracle/_ref/ref_dd "relax").  The frontier itself is
+produced by the reference (BFS or the solver's LIFO order over getCutset children).
+Only data lands in the repository; the reference sources never do.
+"""
+from __future__ import annotations
+
+import gzip
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from sgufp_solver_amd import instance, pools  # noqa: E402
+
+REF = os.path.join(ROOT, "oracle", "_ref", "ref_dd")
+DMIN = pools.DOUBLE_MIN
+
+# name, config, seed, scenarios, n_feas, n_opt, frontier (mode, count), incumbents
+CASES = [
+    ("c1_s1_bfs", "C1", 1, 1, 4, 12, ("bfs", 60), [DMIN, 0.0, 300.0]),
+    ("c1_s2_dfs", "C1", 2, 1, 4, 12, ("dfs", 120), [DMIN, -50.0, 0.0]),
+    ("c2_s1_bfs", "C2", 1, 1, 4, 12, ("bfs", 80), [DMIN, 300.0, 900.0]),
+    ("c2_s2_dfs", "C2", 2, 1, 4, 12, ("dfs", 160), [DMIN, 0.0, 300.0]),
+    ("c2_s3_dfs_big", "C2", 3, 1, 16, 64, ("dfs", 120), [DMIN, 300.0]),
+    ("c2_s4_opt_only", "C2", 4, 1, 0, 24, ("dfs", 120), [DMIN, 200.0, 600.0]),
+    ("c2_s5_feas_only", "C2", 5, 1, 12, 0, ("dfs", 120), [DMIN]),
+    ("c3_s1_dfs", "C3", 1, 2, 4, 12, ("dfs", 120), [DMIN, 0.0, 300.0]),
+    ("c3_s2_bfs", "C3", 2, 2, 4, 12, ("bfs", 40), [DMIN, 300.0]),
+    ("c3_s3_dfs", "C3", 3, 2, 8, 24, ("dfs", 160), [DMIN, 300.0]),
+]
+
+
+def run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"{cmd}: {r.stderr}")
+
+
+def edge_nodes(nodes, L):
+    """Records the reference accepts but a straight B&B rarely produces:
+    the root record, solution vectors shorter than the global layer (getPathForNode's
+    silent fallback, DD.cpp:3803,3814) and records whose layer resets the states."""
+    out = [pools.NodeRecord(0, DMIN, pools.DOUBLE_MAX, [], [])]
+    for nd in nodes[:6]:
+        if len(nd.sol) >= 2:
+            out.append(pools.NodeRecord(nd.gl, nd.lb, nd.ub, list(nd.states), list(nd.sol[:-1])))
+            out.append(pools.NodeRecord(nd.gl, nd.lb, nd.ub, list(nd.states), list(nd.sol[1:])))
+    return out
+
+
+REFINE = [("c1_s2_dfs", "C1", 2, 1), ("c2_s4_opt_only", "C2", 4, 1), ("c3_s1_dfs", "C3", 1, 2)]
+
+
+def add_refine():
+    """Refinement-loop fixtures: the exact DDs of a case continue with 3F + 5O extra cuts
+    (stand-ins for the subproblem's cuts, NodeExplorer.cpp:957-969)."""
+    entries = {}
+    for name, cfg, seed, S in REFINE:
+        d = os.path.join(HERE, name)
+        inst = instance.generate(instance.CONFIGS[cfg], seed, scenarios=S)
+        extra = pools.synthetic_pool(inst, 3, 5, seed * 31 + 5)
+        ep = os.path.join(d, "extra_cuts.txt")
+        pools.write_pool(ep, extra)
+        runs = []
+        for k, inc in enumerate([DMIN, 0.0]):
+            tmp = os.path.join(d, f"refine_{k}.txt")
+            run([REF, "refine", os.path.join(d, "net.txt"), os.path.join(d, "cuts.txt"), os.path.join(d, "nodes.txt"),
+                 inc.hex(), ep, tmp])
+            with open(tmp, "rb") as fi, gzip.open(tmp + ".gz", "wb", compresslevel=9) as fo:
+                fo.write(fi.read())
+            os.remove(tmp)
+            runs.append({"incumbent": inc.hex(), "file": f"refine_{k}.txt.gz"})
+        entries[name] = runs
+    with open(os.path.join(HERE, "refine_manifest.json"), "w") as fh:
+        json.dump(entries, fh, indent=1)
+
+
+def main():
+    if "--refine-only" in sys.argv:
+        add_refine()
+        return
+    if not os.path.exists(REF):
+        sys.exit("build oracle/_ref/ref_dd first (make -C oracle)")
+    manifest = []
+    for name, cfg, seed, S, nf, no, (mode, count), incs in CASES:
+        d = os.path.join(HERE, name)
+        shutil.rmtree(d, ignore_errors=True)
+        os.makedirs(d)
+        inst = instance.generate(instance.CONFIGS[cfg], seed, scenarios=S)
+        net = os.path.join(d, "net.txt")
+        inst.write(net)
+        pool = pools.synthetic_pool(inst, nf, no, seed * 7919 + 17)
+        cuts = os.path.join(d, "cuts.txt")
+        pools.write_pool(cuts, pool)
+        empty = os.path.join(d, "_empty.txt")
+        pools.write_pool(empty, [])
+        nodes_path = os.path.join(d, "nodes.txt")
+        run([REF, mode, net, empty, DMIN.hex(), str(count), nodes_path])
+        os.remove(empty)
+        nodes = pools.read_nodes(nodes_path)
+        nodes = nodes + edge_nodes(nodes, None)
+        pools.write_nodes(nodes_path, nodes)
+        outs = []
+        for k, inc in enumerate(incs):
+            tmp = os.path.join(d, f"ref_{k}.txt")
+            run([REF, "relax", net, cuts, nodes_path, inc.hex(), tmp])
+            with open(tmp, "rb") as fi, gzip.open(tmp + ".gz", "wb", compresslevel=9) as fo:
+                fo.write(fi.read())
+            os.remove(tmp)
+            outs.append({"incumbent": inc.hex(), "file": f"ref_{k}.txt.gz"})
+        order = os.path.join(d, "order.txt")
+        run([REF, "order", net, order])
+        manifest.append({"name": name, "config": cfg, "seed": seed, "scenarios": S, "n_feas": nf, "n_opt": no,
+                         "frontier": mode, "nodes": len(nodes), "runs": outs})
+        print(name, len(nodes), "nodes")
+    with open(os.path.join(HERE, "manifest.json"), "w") as fh:
+        json.dump(manifest, fh, indent=1)
+    add_refine()
+
+
+if __name__ == "__main__":
+    main()

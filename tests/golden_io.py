@@ -1,0 +1,83 @@
+"""Fixture access and bit-exact comparison helpers for the parity tests."""
+from __future__ import annotations
+
+import gzip
+import json
+import os
+import struct
+from typing import List
+
+from sgufp_solver_amd import pools
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+
+
+def manifest():
+    with open(os.path.join(GOLDEN, "manifest.json")) as fh:
+        return json.load(fh)
+
+
+def case_dir(name: str) -> str:
+    return os.path.join(GOLDEN, name)
+
+
+def read_golden(name: str, fname: str) -> str:
+    with gzip.open(os.path.join(case_dir(name), fname), "rb") as fh:
+        return fh.read().decode()
+
+
+def parse_results_text(text: str) -> List[pools.RelaxResult]:
+    import tempfile
+    with tempfile.NamedTemporaryFile("w", suffix=".txt", delete=False) as fh:
+        fh.write(text)
+        p = fh.name
+    try:
+        return pools.read_results(p)
+    finally:
+        os.remove(p)
+
+
+def bits(x: float) -> int:
+    return struct.unpack("<q", struct.pack("<d", x))[0]
+
+
+def node_key(nd: pools.NodeRecord):
+    return (nd.gl, bits(nd.lb), bits(nd.ub), tuple(nd.states), tuple(nd.sol))
+
+
+def compare_results(got: List[pools.RelaxResult], want: List[pools.RelaxResult], check_stats: bool = True):
+    """Bit-exact comparison; returns a list of human-readable mismatches (empty = parity)."""
+    bad = []
+    if len(got) != len(want):
+        return [f"result count {len(got)} != {len(want)}"]
+    for k, (g, w) in enumerate(zip(got, want)):
+        if g.status != w.status:
+            bad.append(f"node {k}: status {g.status} != {w.status}")
+            continue
+        if g.exact != w.exact:
+            bad.append(f"node {k}: exact {g.exact} != {w.exact}")
+        if bits(g.lb) != bits(w.lb) or bits(g.ub) != bits(w.ub):
+            bad.append(f"node {k}: bounds ({g.lb!r},{g.ub!r}) != ({w.lb!r},{w.ub!r})")
+        if g.path != w.path:
+            bad.append(f"node {k}: path differs (len {len(g.path)} vs {len(w.path)})")
+        if len(g.children) != len(w.children):
+            bad.append(f"node {k}: {len(g.children)} children != {len(w.children)}")
+        else:
+            for c, (a, b) in enumerate(zip(g.children, w.children)):
+                if node_key(a) != node_key(b):
+                    bad.append(f"node {k} child {c}: {node_key(a)[:4]} != {node_key(b)[:4]}")
+                    break
+        if check_stats and (g.dd_nodes, g.dd_arcs, g.dd_layers) != (w.dd_nodes, w.dd_arcs, w.dd_layers):
+            bad.append(f"node {k}: DD size {(g.dd_nodes, g.dd_arcs, g.dd_layers)} != {(w.dd_nodes, w.dd_arcs, w.dd_layers)}")
+        if len(bad) > 20:
+            break
+    return bad
+
+
+def refine_manifest():
+    p = os.path.join(GOLDEN, "refine_manifest.json")
+    if not os.path.exists(p):
+        return {}
+    with open(p) as fh:
+        return json.load(fh)

@@ -1,0 +1,155 @@
+"""CPU suite: oracle pinned to the reference's fixtures, host logic, C-ABI exports.
+
+No compute call touches a GPU here.  The oracle (oracle/dd_oracle.cpp) is test
+infrastructure; these tests pin it so it can serve as the checker of the HIP path.
+"""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from sgufp_solver_amd import instance, pools
+from tests import golden_io
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CASES = [(c["name"], r) for c in golden_io.manifest() for r in c["runs"]]
+
+
+@pytest.mark.parametrize("name,run", CASES, ids=[f"{c}-{r['file']}" for c, r in CASES])
+def test_oracle_matches_reference_fixture(oracle_bin, tmp_path, name, run):
+    d = golden_io.case_dir(name)
+    out = tmp_path / "o.txt"
+    subprocess.run([oracle_bin, "relax", f"{d}/net.txt", f"{d}/cuts.txt", f"{d}/nodes.txt", run["incumbent"], str(out)],
+                   check=True)
+    want = golden_io.read_golden(name, run["file"])
+    got = out.read_text()
+    if got != want:
+        bad = golden_io.compare_results(golden_io.parse_results_text(got), golden_io.parse_results_text(want))
+        pytest.fail("\n".join(bad[:10]))
+
+
+REFINE = golden_io.refine_manifest()
+
+
+@pytest.mark.parametrize("name,run", [(n, r) for n, rs in REFINE.items() for r in rs])
+def test_oracle_refinement_loop_matches_reference(oracle_bin, tmp_path, name, run):
+    d = golden_io.case_dir(name)
+    out = tmp_path / "o.txt"
+    subprocess.run([oracle_bin, "refine", f"{d}/net.txt", f"{d}/cuts.txt", f"{d}/nodes.txt", run["incumbent"],
+                    f"{d}/extra_cuts.txt", str(out)], check=True)
+    assert out.read_text() == golden_io.read_golden(name, run["file"])
+
+
+def test_fixtures_cover_every_outcome():
+    """The fixtures exercise every process() exit: children, both prunes, exact DDs."""
+    seen = set()
+    exact = 0
+    misaligned = 0
+    for c in golden_io.manifest():
+        nodes = pools.read_nodes(os.path.join(golden_io.case_dir(c["name"]), "nodes.txt"))
+        misaligned += sum(1 for nd in nodes if len(nd.sol) != nd.gl)
+        for r in c["runs"]:
+            res = golden_io.parse_results_text(golden_io.read_golden(c["name"], r["file"]))
+            seen |= {x.status for x in res}
+            exact += sum(x.exact for x in res)
+    assert seen >= {0, 1, 2, 3}
+    assert exact > 100 and misaligned > 20
+
+
+def test_cut_key_packing_known_answer():
+    """tests2.cpp:209-231 (ConstantCut): map -> cutToCut -> Cut::get by getKey(q,i,j)."""
+    from sgufp_solver_amd.engine import key_of, pack_cuts
+    coeff = [(2, 30, 123, 432.0), (2, 30, 124, 456.67), (1, 18, 123, 1234.56), (4, 1, 90, -1298.98),
+             (5, 6, 7, -1298.98)]
+    rhs, off, keys, vals = pack_cuts([pools.PoolCut(1, 3012.0321, coeff)])
+
+    def get(key):
+        for k, v in zip(keys, vals):
+            if (int(k) & 0xFFFFFFFFFFFF) == (key & 0xFFFFFFFFFFFF):
+                return float(v)
+        return 0.0
+
+    assert get(key_of(30, 2, 123)) == 432.0
+    assert get(key_of(30, 2, 124)) == 456.67
+    assert get(key_of(6, 5, 7)) == -1298.98
+    assert get(key_of(6, 5, 1)) == 0.0
+    # map order (i, q, j) and zero coefficients dropped, like cutToCut (Cut.h:406-421)
+    rhs2, off2, keys2, _ = pack_cuts([pools.PoolCut(0, 1.0, [(3, 4, 5, 0.0), (1, 2, 3, 2.0)])])
+    assert list(keys2) == [key_of(2, 1, 3)] and rhs[0] == 3012.0321
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C5"])
+def test_instance_generator(cfg):
+    c = instance.CONFIGS[cfg]
+    a = instance.generate(c, 3, scenarios=2)
+    b = instance.generate(c, 3, scenarios=2)
+    assert a.to_text() == b.to_text()
+    assert instance.generate(c, 4, scenarios=2).to_text() != a.to_text()
+    assert a.m == c.n_arcs
+    pairs = set(zip(a.tails.tolist(), a.heads.tolist()))
+    assert len(pairs) == a.m, "parallel arcs"
+    indeg = np.bincount(a.heads, minlength=a.n)
+    outdeg = np.bincount(a.tails, minlength=a.n)
+    assert (indeg[1:] > 0).all() and (outdeg[:-1] > 0).all()
+    assert (a.reward == a.reward[:, :1]).all(), "rewards must be scenario-invariant"
+    assert (a.lb <= a.ub).all()
+
+
+def test_library_exports_every_declared_symbol(native_lib):
+    with open(os.path.join(ROOT, "include", "sgufp_hip.h")) as fh:
+        header = fh.read()
+    declared = set(re.findall(r"\b(sgufp_[a-z_]+)\s*\(", header))
+    assert declared, "no declarations parsed"
+    missing = [s for s in sorted(declared) if not hasattr(native_lib, s)]
+    assert not missing, missing
+    from sgufp_solver_amd import engine
+    assert set(engine.EXPORTS) <= declared
+
+
+@pytest.mark.parametrize("name", [c["name"] for c in golden_io.manifest()])
+def test_product_loader_matches_reference_order(native_lib, name):
+    """Network loader (network.cpp) vs Network::Network + shuffleVBarNodes (Network.cpp:10-186)."""
+    from sgufp_solver_amd import engine
+    d = golden_io.case_dir(name)
+    L, layer_arcs, vbar = engine.probe_network(f"{d}/net.txt")
+    with open(f"{d}/order.txt") as fh:
+        head = fh.readline().split()
+        order = [int(x) for x in fh.readline().split()]
+        vb = [int(x) for x in fh.readline().split()]
+    assert L == int(head[0])
+    assert layer_arcs.tolist() == order
+    assert vbar.tolist() == vb
+
+
+def test_product_loader_rejects_bad_files(native_lib, tmp_path):
+    from sgufp_solver_amd import engine
+    p = tmp_path / "bad.txt"
+    p.write_text("3 2 1\n0 1 0 5 1\n")
+    with pytest.raises(RuntimeError):
+        engine.probe_network(str(p))
+    with pytest.raises(RuntimeError):
+        engine.probe_network(str(tmp_path / "missing.txt"))
+
+
+REF_BIN = os.path.join(ROOT, "oracle", "_ref", "ref_dd")
+
+
+@pytest.mark.skipif(not os.path.exists(REF_BIN), reason="reference build (oracle/_ref) absent")
+@pytest.mark.parametrize("seed", [11, 12])
+def test_oracle_vs_reference_fresh_instances(oracle_bin, tmp_path, seed):
+    """Differential run on instances not in the fixtures (tests2.cpp:470-527 recipe)."""
+    inst = instance.generate(instance.CONFIGS["C2"], seed, scenarios=1)
+    net = tmp_path / "net.txt"
+    inst.write(str(net))
+    pools.write_pool(str(tmp_path / "cuts.txt"), pools.synthetic_pool(inst, 6, 18, seed))
+    pools.write_pool(str(tmp_path / "none.txt"), [])
+    subprocess.run([REF_BIN, "dfs", str(net), str(tmp_path / "none.txt"), pools.DOUBLE_MIN.hex(), "60",
+                    str(tmp_path / "nodes.txt")], check=True)
+    for inc in [pools.DOUBLE_MIN, 250.0]:
+        subprocess.run([REF_BIN, "relax", str(net), str(tmp_path / "cuts.txt"), str(tmp_path / "nodes.txt"), inc.hex(),
+                        str(tmp_path / "a.txt")], check=True)
+        subprocess.run([oracle_bin, "relax", str(net), str(tmp_path / "cuts.txt"), str(tmp_path / "nodes.txt"),
+                        inc.hex(), str(tmp_path / "b.txt")], check=True)
+        assert (tmp_path / "a.txt").read_text() == (tmp_path / "b.txt").read_text()
