@@ -105,6 +105,9 @@ def main():
 
     n = args.nodes
     eng = E.Engine(net, local, max(n, 1024))
+    if rank == 0:
+        print(f"[bench] L={eng.info.total_layers} slots={eng.info.max_batch} node_cap={eng.info.node_capacity} "
+              f"arc_cap={eng.info.arc_capacity} scratch={eng.info.scratch_bytes / 2**30:.2f} GiB", file=sys.stderr)
     full = frontier.bfs_frontier(eng, n * world)          # identical on every rank
     eng.add_cuts(pool)
     # incumbent: 40th percentile of the (finite) bounds of the first 1024 records

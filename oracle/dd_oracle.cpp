@@ -524,6 +524,22 @@ int main(int argc, char **argv) {
     using namespace oracle;
     if (argc < 2) return 2;
     std::string mode = argv[1];
+    if (mode == "widths" && argc == 4) {
+        // diagnostic: tree layer widths (and merged in-arc counts) of each node's DD
+        Net net;
+        if (!load_network(argv[2], net)) return 2;
+        auto nodes = read_nodes(argv[3]);
+        DD dd; dd.net = &net;
+        for (auto &nd : nodes) {
+            dd.build(nd);
+            for (size_t k = 0; k + 1 < dd.tree.size(); k++) {
+                int id = dd.tree[k][0];
+                std::printf("%zu%s ", dd.tree[k].size(), (dd.tree[k].size() == 1 && dd.nodes[id].in.size() > 1) ? "m" : "");
+            }
+            std::printf("\n");
+        }
+        return 0;
+    }
     if (mode == "refine" && argc == 8) {
         // process() then the refinement loop (NodeExplorer.cpp:957-969) fed with <extra>
         Net net;

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -16,8 +17,8 @@
 
 namespace sgufp {
 // dd_kernels.hip
-size_t relax_lds_bytes(int Tcap, int Lcap);
-hipError_t launch_relax(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &, double,
+size_t relax_lds_bytes(int Tcap, int Lcap, int cb);
+hipError_t launch_relax(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &, double, int,
                         hipStream_t);
 hipError_t launch_scan(const uint32_t *, const uint32_t *, int, uint64_t *, uint64_t *, hipStream_t);
 hipError_t launch_emit(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &,
@@ -55,7 +56,9 @@ struct sgufp_ctx {
 
     // cut pool
     int row_cap = 0, n_rows = 0;
-    double *d_rows = nullptr, *d_rhs = nullptr;
+    double *d_rows = nullptr, *d_rhs = nullptr, *d_coefT = nullptr;
+    int ustride = 1;
+    int cb = 16;                              // cuts per batched sweep
     std::vector<int32_t> f_rows, o_rows;      // insertion order, row ids
     int32_t *d_forder = nullptr, *d_oorder = nullptr;
     int order_cap = 0;
@@ -147,6 +150,7 @@ struct sgufp_ctx {
         p.rows = d_rows; p.rhs = d_rhs; p.stride = net.n_slots + 1;
         p.f_order = d_forder; p.nf = (int)f_rows.size();
         p.o_order = d_oorder; p.no = (int)o_rows.size();
+        p.coefT = d_coefT; p.ustride = ustride;
         return p;
     }
     BatchIn batch() const {
@@ -162,7 +166,7 @@ namespace {
 // Upper bound on DD nodes: every layer outside the last five has < 120 nodes or is a
 // single merged node (collapse rule, DD.cpp:3614); the last five expand exactly, and a
 // node with c states (-1 included) has one child with c states and c-1 with c-1.
-int64_t node_bound(const Network &net) {
+int64_t node_bound(const Network &net, int64_t *tail = nullptr) {
     const int L = net.L;
     auto set_size = [&](int sid) { return sid >= 0 ? (int)net.sets[sid].size() : 1; };
     int start = std::max(0, L - 5);
@@ -170,6 +174,7 @@ int64_t node_bound(const Network &net) {
     int c0 = set_size(net.layer_universe[start]);
     h[c0] = (L > 5) ? kRelaxedMaxWidth - 1 : 1;
     int64_t total = (int64_t)(kRelaxedMaxWidth - 1) * (start + 1);
+    int64_t tail_nodes = 0;
     for (int l = start; l < L; l++) {
         if (net.layer_update[l] >= 0) {
             int64_t w = 0;
@@ -187,7 +192,9 @@ int64_t node_bound(const Network &net) {
         int64_t w = 0;
         for (auto x : h) w += x;
         total += w;
+        tail_nodes += w;
     }
+    if (tail) *tail = std::max<int64_t>(tail_nodes, 128) + 8;
     return total + 8;
 }
 
@@ -243,12 +250,18 @@ bool sgufp_ctx::init() {
     const int maxU = std::max(1, net.max_states);
     sc.Tcap = L + 2;
     sc.Lcap = L + 1;
-    int64_t ncap = node_bound(net);
+    int64_t tail = 0;
+    int64_t ncap = node_bound(net, &tail);
+    ustride = std::max(1, net.max_states);
+    if (const char *e = getenv("SGUFP_CUT_BATCH")) cb = atoi(e);
+    if (cb != 1 && cb != 4 && cb != 8 && cb != 16) cb = 16;
     int64_t acap = std::max<int64_t>(1, (int64_t)std::max(0, L - 4) * (kRelaxedMaxWidth - 1) * maxU);
     if (ncap > (int64_t)kParentMask || acap > (int64_t)0x7FFFFFFF) { err = "DD capacity beyond 22-bit indices"; return false; }
     sc.Ncap = (int)ncap;
     sc.Acap = (int)acap;
-    if (relax_lds_bytes(sc.Tcap, sc.Lcap) > 64 * 1024) { err = "too many layers for the LDS layer table"; return false; }
+    if (relax_lds_bytes(sc.Tcap, sc.Lcap, cb) > 64 * 1024) { err = "too many layers for the LDS layer table"; return false; }
+    sc.tail_cap = (int)tail;
+    sc.cb_max = cb;
     const size_t B = (size_t)max_batch;
     if (!alloc(sc.ntopo, B * sc.Ncap, "scratch") || !alloc(sc.nflag, B * sc.Ncap, "scratch") ||
         !alloc(sc.nmask, B * sc.Ncap, "scratch") || !alloc(sc.outcnt, B * sc.Ncap, "scratch") ||
@@ -256,6 +269,9 @@ bool sgufp_ctx::init() {
         !alloc(sc.atopo, B * sc.Acap, "scratch") || !alloc(sc.aflag, B * sc.Acap, "scratch") ||
         !alloc(sc.lay, B * sc.Tcap * 5, "scratch") || !alloc(sc.rslot, B * sc.Lcap, "scratch") ||
         !alloc(sc.meta, B * 8, "scratch") || !alloc(sc.ubv, B, "scratch"))
+        return false;
+    if (cb > 1 && (!alloc(sc.s2b, B * sc.tail_cap * cb, "scratch") || !alloc(sc.sm, B * sc.Tcap * cb, "scratch") ||
+                   !alloc(sc.xm, B * sc.Tcap * cb, "scratch")))
         return false;
     // outputs
     if (!alloc(out.status, B, "out") || !alloc(out.exact, B, "out") || !alloc(out.lb, B, "out") ||
@@ -279,18 +295,24 @@ bool sgufp_ctx::grow_rows(int need) {
     if (need <= row_cap) return true;
     int cap = std::max(need, row_cap * 2);
     const size_t stride = (size_t)net.n_slots + 1;
-    double *rows = nullptr, *rhs = nullptr;
-    if (!alloc(rows, (size_t)cap * stride, "cut rows") || !alloc(rhs, (size_t)cap, "cut rhs")) return false;
+    const size_t tstride = (size_t)std::max(net.L, 1) * ustride;
+    double *rows = nullptr, *rhs = nullptr, *coefT = nullptr;
+    if (!alloc(rows, (size_t)cap * stride, "cut rows") || !alloc(rhs, (size_t)cap, "cut rhs") ||
+        !alloc(coefT, (size_t)cap * tstride, "cut coefT"))
+        return false;
     if (n_rows) {
         if (!hip_ok(hipMemcpyAsync(rows, d_rows, (size_t)n_rows * stride * 8, hipMemcpyDeviceToDevice, stream), "D2D") ||
-            !hip_ok(hipMemcpyAsync(rhs, d_rhs, (size_t)n_rows * 8, hipMemcpyDeviceToDevice, stream), "D2D"))
+            !hip_ok(hipMemcpyAsync(rhs, d_rhs, (size_t)n_rows * 8, hipMemcpyDeviceToDevice, stream), "D2D") ||
+            !hip_ok(hipMemcpyAsync(coefT, d_coefT, (size_t)n_rows * tstride * 8, hipMemcpyDeviceToDevice, stream), "D2D"))
             return false;
         if (!sync()) return false;
     }
     release(d_rows);
     release(d_rhs);
+    release(d_coefT);
     d_rows = rows;
     d_rhs = rhs;
+    d_coefT = coefT;
     row_cap = cap;
     return true;
 }
@@ -439,9 +461,21 @@ int sgufp_cuts_append(sgufp_ctx *ctx, int is_feasibility, int n_cuts, const doub
             }
         }
     }
+    // per (layer, state rank) coefficients for the batched sweeps: coefT[l][r] = row[slot_tab[l][r]]
+    const Network &net = ctx->net;
+    const int us = ctx->ustride;
+    const size_t tstride = (size_t)std::max(net.L, 1) * us;
+    std::vector<double> coefT((size_t)n_cuts * tstride, 0.0);
+    for (int c = 0; c < n_cuts; c++)
+        for (int l = 0; l < net.L; l++)
+            for (int r = 0; r < us; r++) {
+                int sl = net.slot_tab[(size_t)l * kMaxStates + r];
+                if (sl >= 0) coefT[(size_t)c * tstride + (size_t)l * us + r] = rows[(size_t)c * stride + sl];
+            }
     int first = ctx->n_rows;
     if (!ctx->grow_rows(first + n_cuts)) return SGUFP_ERR_HIP;
-    if (!ctx->upload(ctx->d_rows + (size_t)first * stride, rows.data(), rows.size()) ||
+    if (!ctx->upload(ctx->d_coefT + (size_t)first * tstride, coefT.data(), coefT.size()) ||
+        !ctx->upload(ctx->d_rows + (size_t)first * stride, rows.data(), rows.size()) ||
         !ctx->upload(ctx->d_rhs + first, rhs, (size_t)n_cuts) || !ctx->sync())
         return SGUFP_ERR_HIP;
     for (int c = 0; c < n_cuts; c++) (is_feasibility ? ctx->f_rows : ctx->o_rows).push_back(first + c);
@@ -529,7 +563,8 @@ int sgufp_batch_relax(sgufp_ctx *ctx, double optimal_lb) {
     const Pool pool = ctx->pool();
     hipStream_t st = ctx->stream;
     if (ctx->timing) hipEventRecord(ctx->ev[0], st);
-    if (!ctx->hip_ok(launch_relax(ctx->nd, ctx->sc, in, pool, ctx->out, optimal_lb, st), "k_relax")) return SGUFP_ERR_HIP;
+    if (!ctx->hip_ok(launch_relax(ctx->nd, ctx->sc, in, pool, ctx->out, optimal_lb, ctx->cb, st), "k_relax"))
+        return SGUFP_ERR_HIP;
     if (ctx->timing) hipEventRecord(ctx->ev[1], st);
     if (in.n > 0 &&
         !ctx->hip_ok(launch_scan(ctx->out.nchild, ctx->out.sol_need, in.n, ctx->d_coff, ctx->d_soff, st), "k_scan2"))

@@ -63,6 +63,12 @@ struct Scratch {
     int32_t *rslot;    // [Lcap] coefficient slot of each root-solution decision (-1: decision -1)
     int32_t *meta;     // [8] g, sol_len, T, exact, aligned, last_cut, status, cut_layer
     double *ubv;       // [1] running upper bound
+    // multi-cut sweeps (k_relax with CB > 1)
+    int tail_cap;      // nodes of the HBM-resident tail layers (wide layers + last layer)
+    int cb_max;        // cuts per batched sweep the buffers are sized for
+    double *s2b;       // [tail_cap * cb_max]
+    double *sm;        // [Tcap * cb_max]
+    double *xm;        // [Tcap * cb_max]
 };
 
 // Staged batch of open nodes (Inavap::Node records, DD.h:456-478), SoA.
@@ -86,6 +92,8 @@ struct Pool {
     int nf;
     const int32_t *o_order;    // optimality cuts, newest first
     int no;
+    const double *coefT;       // [cap][L][ustride]: coefficient of state rank r at layer l
+    int ustride;               // max state-set size of the network
 };
 
 struct BatchOut {

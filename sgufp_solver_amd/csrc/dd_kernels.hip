@@ -122,25 +122,30 @@ struct DD {
 
 struct LdsCarve {
     size_t bytes;
-    size_t o_lay, o_rslot, o_buf, o_coef, o_walk;
+    size_t o_lay, o_rslot, o_buf, o_coef, o_walk, o_bcoef, o_w1, o_ids;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-__host__ __device__ inline LdsCarve lds_carve(int Tcap, int Lcap) {
+// cb = cuts per batched sweep (1 = single-cut kernels only)
+__host__ __device__ inline LdsCarve lds_carve(int Tcap, int Lcap, int cb) {
     LdsCarve c;
     size_t o = 0;
+    size_t single = (size_t)2 * kLdsWidth * 8, batch = (size_t)2 * 128 * (cb > 1 ? cb : 0) * 8;
     c.o_lay = o; o = align16(o + (size_t)Tcap * 5 * 4);
     c.o_rslot = o; o = align16(o + (size_t)Lcap * 4);
-    c.o_buf = o; o = align16(o + (size_t)2 * kLdsWidth * 8);
+    c.o_buf = o; o = align16(o + (single > batch ? single : batch));
     c.o_coef = o; o = align16(o + (size_t)kMaxU * 8);
     c.o_walk = o; o = align16(o + (size_t)Tcap * 2);
+    c.o_bcoef = o; o = align16(o + (cb > 1 ? (size_t)cb * kMaxU * 8 : 0));
+    c.o_w1 = o; o = align16(o + (cb > 1 ? (size_t)Tcap : 0));
+    c.o_ids = o; o = align16(o + (cb > 1 ? (size_t)cb * 4 : 0));
     c.bytes = o;
     return c;
 }
 
-__device__ inline void dd_bind(DD &d, uint8_t *smem, const Scratch &sc, int slot) {
-    LdsCarve c = lds_carve(sc.Tcap, sc.Lcap);
+__device__ inline void dd_bind(DD &d, uint8_t *smem, const Scratch &sc, int slot, int cb = 1) {
+    LdsCarve c = lds_carve(sc.Tcap, sc.Lcap, cb);
     uint32_t *lay = (uint32_t *)(smem + c.o_lay);
     d.noff = lay;
     d.nn = lay + sc.Tcap;
@@ -475,8 +480,17 @@ __device__ bool dd_prune(const NetDev &net, DD &d, const double *row, int first,
     return true;
 }
 
-// applyFeasibilityCut after the sweep: last-layer removal + cascade, then pruning.
-__device__ bool dd_post_feasibility(const NetDev &net, DD &d, const double *row) {
+// Values of the last layer for the cut being post-processed: v(i) = p[i * stride].
+struct LastVals {
+    const double *p;
+    int stride;
+    __device__ double operator()(uint32_t i) const { return p[(size_t)i * stride]; }
+};
+
+// Last-layer removal (state2 < -0.01, DD.cpp:3880-3893) and the bottom-up deletion
+// cascade (removeNode / bottomUpDelete / updateTree, DD.cpp:4040-4153).  Returns false
+// when every alive last-layer node would go (the reference returns false there).
+__device__ bool dd_remove_last(DD &d, const LastVals &lv) {
     const int last = d.T - 1;
     const uint32_t lo = d.noff[last], ln = d.nn[last];
     uint32_t rm = 0;
@@ -485,7 +499,7 @@ __device__ bool dd_post_feasibility(const NetDev &net, DD &d, const double *row)
         bool kill = false;
         if (i < ln) {
             uint8_t f = d.nflag[lo + i];
-            if ((f & kAlive) && d.s2[lo + i] < -0.01) {
+            if ((f & kAlive) && lv(i) < -0.01) {
                 kill = true;
                 d.nflag[lo + i] = f | kKill;
             }
@@ -495,7 +509,7 @@ __device__ bool dd_post_feasibility(const NetDev &net, DD &d, const double *row)
     if (rm == d.nalive[last]) return false;
     if (rm) {
         wave_mem_sync();
-        // bottom-up deletion: a parent dies when its last alive out-arc dies in this batch
+        // a parent dies when its last alive out-arc dies in this batch
         for (int k = last; k >= 1; k--) {
             const uint32_t noff = d.noff[k], n = d.nn[k], pnoff = d.noff[k - 1];
             const uint32_t acnt = d.acnt[k];
@@ -549,31 +563,195 @@ __device__ bool dd_post_feasibility(const NetDev &net, DD &d, const double *row)
             if (!parent_killed) break;
         }
     }
-    if (!d.exact) return dd_prune(net, d, row, 1, last, -0.01);
     return true;
 }
 
-// applyOptimalityCut after the sweep.  Returns the terminal state (or DOUBLE_MIN).
-__device__ double dd_post_optimality(const NetDev &net, DD &d, const double *row, double optimal) {
+// Terminal arcs of an optimality cut: weight = min(weight, parent.state2), terminal
+// state = max over them (DD.cpp:3975-3984).
+__device__ double dd_terminal(DD &d, const LastVals &lv) {
     const int last = d.T - 1;
     const uint32_t lo = d.noff[last], ln = d.nn[last];
     VP best{0.0, INT_MIN};
     for (uint32_t base = 0; base < ln; base += kWave) {
         uint32_t i = base + lane();
         if (i < ln && (d.nflag[lo + i] & kAlive)) {
-            double w = smin(d.tw[lo + i], d.s2[lo + i]);
+            double w = smin(d.tw[lo + i], lv(i));
             d.tw[lo + i] = w;
             best = vp_pick(best, VP{w, prio_old((int)i)});
         }
     }
     best = wave_vp(best);
-    const double term = (best.p == INT_MIN) ? DMIN : smax(DMIN, best.v);
     wave_mem_sync();
+    return (best.p == INT_MIN) ? DMIN : smax(DMIN, best.v);
+}
+
+// applyFeasibilityCut after a single-cut sweep.
+__device__ bool dd_post_feasibility(const NetDev &net, DD &d, const double *row) {
+    const uint32_t lo = d.noff[d.T - 1];
+    if (!dd_remove_last(d, LastVals{d.s2 + lo, 1})) return false;
+    if (!d.exact) return dd_prune(net, d, row, 1, d.T - 1, -0.01);
+    return true;
+}
+
+// applyOptimalityCut after a single-cut sweep.  Returns the terminal state (or DOUBLE_MIN).
+__device__ double dd_post_optimality(const NetDev &net, DD &d, const double *row, double optimal) {
+    const int last = d.T - 1;
+    const double term = dd_terminal(d, LastVals{d.s2 + d.noff[last], 1});
     if (term <= optimal) return term;
     if (!d.exact) {
         if (!dd_prune(net, d, row, 3, last - 1, optimal - 0.01)) return DMIN;
     }
     return term;
+}
+
+// ------------------------------------------------------------------------------------
+// Multi-cut sweeps.  Deleting nodes never changes state2 of the nodes that stay (an
+// alive node keeps every non-pruned in-arc and the tails of those arcs stay alive), so
+// the sweeps of CB consecutive pool cuts can run together over the same DD and their
+// removal / terminal / early-exit logic be replayed in pool order afterwards.  Only
+// width-1 arc pruning changes later sweeps: per (width-1 layer, cut) the sweep records
+// the single node's state2 and the smallest parent.state2 + weight over its in-arcs;
+// since rounding is monotone, "some arc is pruned" <=> fl(xmin + gain) <= threshold.
+// When that fires (or deletions make a new width-1 layer), the cut is redone with the
+// exact single-cut path and the batch restarts after it.
+constexpr int kLdsBatchWidth = 128;   // layers up to this width keep their CB values in LDS
+
+struct BatchView {
+    double *vb;        // LDS [2][kLdsBatchWidth][CB]
+    double *coef;      // LDS [CB][ustride]
+    uint8_t *w1;       // LDS [Tcap]: layer had one alive node when the batch started
+    int32_t *ids;      // LDS [CB]: pool row of each batch cut
+    double *s2b;       // HBM [tail_cap][CB]: layers >= kg
+    double *sm, *xm;   // HBM [Tcap][CB]
+    int kg;            // first layer kept in HBM (a wide layer, or the last layer)
+    uint32_t gbase;    // noff[kg]
+};
+
+template <int CB>
+__device__ void dd_sweep_batch(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int nb, double rv) {
+    constexpr int G = kWave / CB;
+    const int c = lane() % CB, grp = lane() / CB;
+    const bool cv = c < nb;
+    const int us = pool.ustride;
+    const size_t ltab = (size_t)net.L * us;
+    // layer 0: the root fold of each cut
+    if (lane() < CB && cv) {
+        if (bv.kg == 0) bv.s2b[c] = rv;
+        else bv.vb[c] = rv;
+        if (c == nb - 1) d.s2[0] = rv;
+    }
+    wave_mem_sync();
+    for (int k = 1; k < d.T; k++) {
+        const uint32_t noff = d.noff[k], n = d.nn[k];
+        const uint32_t pnoff = d.noff[k - 1];
+        const bool prev_g = (k - 1) >= bv.kg, cur_g = k >= bv.kg;
+        const double *pbuf = bv.vb + (size_t)((k - 1) & 1) * kLdsBatchWidth * CB;
+        double *cbuf = bv.vb + (size_t)(k & 1) * kLdsBatchWidth * CB;
+        const int ls = d.g + k - 1;
+        for (int idx = lane(); idx < nb * us; idx += kWave) {
+            int cc = idx / us, r = idx - cc * us;
+            bv.coef[cc * us + r] = pool.coefT[(size_t)bv.ids[cc] * ltab + (size_t)ls * us + r];
+        }
+        wave_lds_sync();
+        auto prevv = [&](uint32_t p) -> double {
+            return prev_g ? bv.s2b[(size_t)(pnoff + p - bv.gbase) * CB + c] : pbuf[p * CB + c];
+        };
+        const uint32_t acnt = d.acnt[k];
+        if (acnt) {
+            const uint32_t aoff = d.aoff[k];
+            VP best{0.0, INT_MIN};
+            double xmin = DMAX;
+            bool any = false;
+            for (uint32_t a = grp; a < acnt; a += G) {
+                if (cv && (d.aflag[aoff + a] & kAlive)) {
+                    uint32_t t = d.atopo[aoff + a];
+                    uint32_t p = t & kParentMask, r = t >> kRankShift;
+                    double x = prevv(p);
+                    VP e;
+                    double y;
+                    if (r != 0) { e.v = x + bv.coef[c * us + r]; e.p = prio_new((int)a); y = e.v; }
+                    else { e.v = x; e.p = prio_old((int)a); y = x + 0.0; }
+                    best = vp_pick(best, e);
+                    xmin = fmin(xmin, y);
+                    any = true;
+                }
+            }
+#pragma unroll
+            for (int sft = CB; sft < kWave; sft <<= 1) {
+                VP o;
+                o.v = __shfl_xor(best.v, sft, kWave);
+                o.p = __shfl_xor(best.p, sft, kWave);
+                best = vp_pick(best, o);
+                xmin = fmin(xmin, __shfl_xor(xmin, sft, kWave));
+                any = any || (__shfl_xor((int)any, sft, kWave) != 0);
+            }
+            if (grp == 0 && cv) {
+                double v = (best.p == INT_MIN) ? DMIN : smax(best.v, DMIN);
+                if (cur_g) bv.s2b[(size_t)(noff - bv.gbase) * CB + c] = v;
+                else cbuf[c] = v;
+                if (c == nb - 1) d.s2[noff] = v;
+                if (bv.w1[k]) {
+                    bv.sm[(size_t)k * CB + c] = v;
+                    bv.xm[(size_t)k * CB + c] = any ? xmin : DMAX;
+                }
+            }
+        } else {
+            const bool w1 = bv.w1[k] != 0;
+            for (uint32_t base = 0; base < n; base += G) {
+                uint32_t i = base + grp;
+                if (i < n && cv) {
+                    uint32_t node = noff + i;
+                    uint8_t f = d.nflag[node];
+                    if (f & kAlive) {
+                        uint32_t t = d.ntopo[node];
+                        uint32_t p = t & kParentMask, r = t >> kRankShift;
+                        double x, y = DMAX;
+                        if (!(f & kInAlive)) x = DMIN;
+                        else {
+                            double px = prevv(p);
+                            if (r != 0) { x = px + bv.coef[c * us + r]; y = x; }
+                            else { x = px; y = px + 0.0; }
+                        }
+                        if (cur_g) bv.s2b[(size_t)(node - bv.gbase) * CB + c] = x;
+                        else cbuf[i * CB + c] = x;
+                        if (c == nb - 1) d.s2[node] = x;
+                        if (w1) {
+                            bv.sm[(size_t)k * CB + c] = x;
+                            bv.xm[(size_t)k * CB + c] = y;
+                        }
+                    }
+                }
+            }
+        }
+        if (prev_g || cur_g) wave_mem_sync();
+        else wave_lds_sync();
+    }
+    wave_mem_sync();
+}
+
+// Pruning test of one cut from the batch summaries over layers [first, end):
+// 0 = nothing pruned, 1 = redo this cut exactly (some arc is pruned, or a width-1
+// layer has no summary because deletions made it width-1 inside the batch).
+template <int CB>
+__device__ int dd_prune_check(const DD &d, const BatchView &bv, const LastVals &lv, int c, int first, int end,
+                              double thresh) {
+    const int last = d.T - 1;
+    VP mx = layer_max_first(d, last, [&](uint32_t node) { return lv(node - d.noff[last]); });
+    const double maxState = (mx.p == INT_MIN) ? DMIN : smax(DMIN, mx.v);
+    for (int k = first; k < end; k++) {
+        if (d.nalive[k] != 1) continue;
+        if (!bv.w1[k]) return 1;
+        const double gain = maxState - bv.sm[(size_t)k * CB + c];
+        if ((bv.xm[(size_t)k * CB + c] + gain) <= thresh) return 1;
+    }
+    return 0;
+}
+
+// any layer in [first, end) that became width-1 after the batch started
+__device__ inline bool dd_new_width1(const DD &d, const BatchView &bv, int first, int end) {
+    for (int k = first; k < end; k++)
+        if (d.nalive[k] == 1 && !bv.w1[k]) return true;
+    return false;
 }
 
 // getPathForNode (DD.cpp:3796-3820): walk up, first in-arc whose parent.state2 + weight
@@ -658,22 +836,6 @@ __device__ inline void store_meta_layers(const DD &d, const Scratch &sc, int slo
     }
 }
 
-// root fold of 64 cuts at once: lane c folds cut order[c0 + c] over the root solution
-__device__ inline double root_fold(const Pool &pool, const int32_t *order, int cnt, int c0, const DD &d) {
-    int c = c0 + lane();
-    double v = 0.0;
-    if (c < cnt) {
-        int id = order[c];
-        const double *row = pool.rows + (size_t)id * pool.stride;
-        v = pool.rhs[id];
-        for (int t = 0; t < d.len; t++) {
-            int s = d.rslot[t];
-            if (s >= 0) v = v + row[s];
-        }
-    }
-    return v;
-}
-
 // exact DD: argmax terminal arc (strict >, first wins) then the path of its tail
 __device__ int dd_solution_path(const NetDev &net, DD &d, const double *row, int16_t *out_path,
                                 const int16_t *rsol) {
@@ -698,25 +860,139 @@ __device__ int dd_solution_path(const NetDev &net, DD &d, const double *row, int
 }
 
 // ------------------------------------------------------------------------------------
+// Pool order: the feasibility list then the optimality list, each newest first
+// (NodeExplorer.cpp:935-944 / 975-983).
+__device__ inline int seq_id(const Pool &pool, int s) { return s < pool.nf ? pool.f_order[s] : pool.o_order[s - pool.nf]; }
+
+// root fold (DD.cpp:3938-3949) of the cuts at pool positions s0 + lane
+__device__ inline double root_fold_seq(const Pool &pool, const DD &d, int s0, int total) {
+    int s = s0 + lane();
+    double v = 0.0;
+    if (s < total) {
+        int id = seq_id(pool, s);
+        const double *row = pool.rows + (size_t)id * pool.stride;
+        v = pool.rhs[id];
+        for (int t = 0; t < d.len; t++) {
+            int sl = d.rslot[t];
+            if (sl >= 0) v = v + row[sl];
+        }
+    }
+    return v;
+}
+
+struct LoopState {
+    int status;
+    double ub;
+    int last_cut;
+    uint32_t applied;
+};
+
+// one cut at a time from pool position s onwards
+__device__ void cut_loop_single(const NetDev &net, DD &d, const Pool &pool, double incumbent, int s, LoopState &st) {
+    const int total = pool.nf + pool.no;
+    for (int s0 = s; s0 < total; s0 += kWave) {
+        double rv = root_fold_seq(pool, d, s0, total);
+        int cnt = min(kWave, total - s0);
+        for (int j = 0; j < cnt; j++) {
+            const int seq = s0 + j;
+            const int id = seq_id(pool, seq);
+            const double *row = pool.rows + (size_t)id * pool.stride;
+            dd_sweep(net, d, row, __shfl(rv, j, kWave));
+            st.last_cut = id;
+            st.applied++;
+            if (seq < pool.nf) {
+                if (!dd_post_feasibility(net, d, row)) { st.status = kPrunedFeasibility; return; }
+            } else {
+                double v = dd_post_optimality(net, d, row, incumbent);
+                st.ub = d.exact ? v : smin(v, st.ub);
+                if (st.ub <= incumbent) { st.status = kPrunedOptimality; return; }
+            }
+        }
+    }
+}
+
+// CB cuts per sweep, replayed in pool order (see dd_sweep_batch)
+template <int CB>
+__device__ void cut_loop_batched(const NetDev &net, DD &d, const Scratch &sc, BatchView &bv, const Pool &pool,
+                                 double incumbent, LoopState &st) {
+    const int total = pool.nf + pool.no;
+    int s = 0;
+    while (s < total) {
+        const int nb = min(CB, total - s);
+        if (lane() < nb) bv.ids[lane()] = seq_id(pool, s + lane());
+        for (int k = lane(); k < d.T; k += kWave) bv.w1[k] = (d.nalive[k] == 1) ? 1 : 0;
+        // first layer held in HBM: the first one wider than the LDS buffers, else the last
+        int kg = d.T - 1;
+        for (int base = 0; base < d.T - 1; base += kWave) {
+            int k = base + lane();
+            uint64_t b = __ballot(k < d.T - 1 && d.nn[k] > (uint32_t)kLdsBatchWidth);
+            if (b) { kg = base + (int)(__ffsll((unsigned long long)b) - 1); break; }
+        }
+        bv.kg = kg;
+        bv.gbase = d.noff[kg];
+        if (d.noff[d.T - 1] + d.nn[d.T - 1] - bv.gbase > (uint32_t)sc.tail_cap) {
+            cut_loop_single(net, d, pool, incumbent, s, st);   // tail too large for the buffers
+            return;
+        }
+        double rv = root_fold_seq(pool, d, s, total);
+        wave_lds_sync();
+        dd_sweep_batch<CB>(net, d, bv, pool, nb, rv);
+        const int last = d.T - 1;
+        const double *lbase = bv.s2b + (size_t)(d.noff[last] - bv.gbase) * CB;
+        int next = s + nb;
+        for (int c = 0; c < nb; c++) {
+            const int seq = s + c;
+            const int id = bv.ids[c];
+            const double *row = pool.rows + (size_t)id * pool.stride;
+            const LastVals lv{lbase + c, CB};
+            st.last_cut = id;
+            st.applied++;
+            bool redo = false;
+            if (seq < pool.nf) {
+                if (!dd_remove_last(d, lv)) { st.status = kPrunedFeasibility; return; }
+                if (!d.exact && dd_prune_check<CB>(d, bv, lv, c, 1, last, -0.01)) {
+                    dd_sweep(net, d, row, __shfl(rv, c, kWave));
+                    if (!dd_prune(net, d, row, 1, last, -0.01)) { st.status = kPrunedFeasibility; return; }
+                    redo = true;
+                }
+            } else {
+                double v = dd_terminal(d, lv);
+                if (v > incumbent && !d.exact && dd_prune_check<CB>(d, bv, lv, c, 3, last - 1, incumbent - 0.01)) {
+                    dd_sweep(net, d, row, __shfl(rv, c, kWave));
+                    if (!dd_prune(net, d, row, 3, last - 1, incumbent - 0.01)) v = DMIN;
+                    redo = true;
+                }
+                st.ub = d.exact ? v : smin(v, st.ub);
+                if (st.ub <= incumbent) { st.status = kPrunedOptimality; return; }
+            }
+            if (redo) { next = seq + 1; break; }
+        }
+        s = next;
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Kernel 1: build + pool sweeps + finish, one wave per open node.
+template <int CB>
 __global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn in, Pool pool, BatchOut out,
                                                 double incumbent) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int slot = blockIdx.x;
     if (slot >= in.n) return;
     DD d;
-    dd_bind(d, smem, sc, slot);
+    dd_bind(d, smem, sc, slot, CB);
     d.g = in.gl[slot];
     d.len = in.sol_len[slot];
     const int16_t *rsol = in.sol + in.sol_off[slot];
     d.aligned = (d.len == d.g) ? 1 : 0;
-    int status = kSuccess, last_cut = -1, cut_layer = 0;
-    double ub = in.ub[slot], lb = DMIN;
-    uint32_t nchild = 0, sweeps = 0, n_nodes = 0, n_arcs = 0;
+    int cut_layer = 0;
+    LoopState st{kSuccess, in.ub[slot], -1, 0};
+    double lb = DMIN;
+    uint32_t nchild = 0, n_nodes = 0, n_arcs = 0;
     d.T = 1; d.exact = 1;
 
     if (!in.valid[slot] || d.len > d.g || d.g > net.L || d.len > sc.Lcap) {
-        status = kErrRecord;
+        st.status = kErrRecord;
         goto done;
     }
     // coefficient slots of the root solution (layer t, decision sol[t])
@@ -734,54 +1010,34 @@ __global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn
         d.rslot[t] = s;
     }
     if (!dd_build(net, d, sc, in.mask[slot], n_nodes, n_arcs)) {
-        status = kErrCapacity;
+        st.status = kErrCapacity;
         goto done;
     }
-    {
-        // feasibility pool, newest first (NodeExplorer.cpp:935-938 / 975-978)
-        for (int c0 = 0; c0 < pool.nf; c0 += kWave) {
-            double rv = root_fold(pool, pool.f_order, pool.nf, c0, d);
-            int cnt = min(kWave, pool.nf - c0);
-            for (int j = 0; j < cnt; j++) {
-                int id = pool.f_order[c0 + j];
-                const double *row = pool.rows + (size_t)id * pool.stride;
-                dd_sweep(net, d, row, __shfl(rv, j, kWave));
-                last_cut = id;
-                sweeps++;
-                if (!dd_post_feasibility(net, d, row)) {
-                    status = kPrunedFeasibility;
-                    goto done;
-                }
-            }
-        }
-        // optimality pool, newest first (NodeExplorer.cpp:940-944 / 980-983)
-        for (int c0 = 0; c0 < pool.no; c0 += kWave) {
-            double rv = root_fold(pool, pool.o_order, pool.no, c0, d);
-            int cnt = min(kWave, pool.no - c0);
-            for (int j = 0; j < cnt; j++) {
-                int id = pool.o_order[c0 + j];
-                const double *row = pool.rows + (size_t)id * pool.stride;
-                dd_sweep(net, d, row, __shfl(rv, j, kWave));
-                last_cut = id;
-                sweeps++;
-                double v = dd_post_optimality(net, d, row, incumbent);
-                ub = d.exact ? v : smin(v, ub);
-                if (ub <= incumbent) {
-                    status = kPrunedOptimality;
-                    goto done;
-                }
-            }
-        }
-        const double *lrow = last_cut >= 0 ? pool.rows + (size_t)last_cut * pool.stride : nullptr;
+    if (CB > 1 && d.aligned) {
+        LdsCarve cv = lds_carve(sc.Tcap, sc.Lcap, CB);
+        BatchView bv;
+        bv.vb = (double *)(smem + cv.o_buf);
+        bv.coef = (double *)(smem + cv.o_bcoef);
+        bv.w1 = smem + cv.o_w1;
+        bv.ids = (int32_t *)(smem + cv.o_ids);
+        bv.s2b = sc.s2b + (size_t)slot * sc.tail_cap * CB;
+        bv.sm = sc.sm + (size_t)slot * sc.Tcap * CB;
+        bv.xm = sc.xm + (size_t)slot * sc.Tcap * CB;
+        cut_loop_batched<CB>(net, d, sc, bv, pool, incumbent, st);
+    } else {
+        cut_loop_single(net, d, pool, incumbent, 0, st);
+    }
+    if (st.status == kSuccess) {
+        const double *lrow = st.last_cut >= 0 ? pool.rows + (size_t)st.last_cut * pool.stride : nullptr;
         if (d.exact) {
-            status = kNeedsSubproblem;
+            st.status = kNeedsSubproblem;
             int plen = dd_solution_path(net, d, lrow, out.path + (size_t)slot * sc.Lcap, rsol);
             if (lane() == 0) out.path_len[slot] = (uint16_t)plen;
         } else {
             int k = 3;
             while (k < d.T && d.nalive[k] != 1) k++;
             if (k >= d.T) {
-                status = kErrCutset;
+                st.status = kErrCutset;
             } else {
                 cut_layer = k;
                 const uint32_t M = layer_single(d, k);
@@ -798,23 +1054,23 @@ __global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn
         }
     }
 done:
-    if (status == kPrunedFeasibility || status == kPrunedOptimality || status >= kErrRecord) {
+    if (st.status == kPrunedFeasibility || st.status == kPrunedOptimality || st.status >= kErrRecord) {
         lb = DMIN;
-        ub = DMIN;
+        st.ub = DMIN;
     }
     if (lane() == 0) {
-        out.status[slot] = status;
+        out.status[slot] = st.status;
         out.exact[slot] = (uint8_t)d.exact;
         out.lb[slot] = lb;
-        out.ub[slot] = ub;
+        out.ub[slot] = st.ub;
         out.nchild[slot] = nchild;
         out.sol_need[slot] = nchild * (uint32_t)(d.len + cut_layer);
         out.dd_nodes[slot] = n_nodes;
         out.dd_arcs[slot] = n_arcs;
         out.dd_layers[slot] = (uint32_t)d.T + 1;
-        out.sweeps[slot] = sweeps;
+        out.sweeps[slot] = st.applied;
     }
-    store_meta_layers(d, sc, slot, last_cut, status, cut_layer, ub);
+    store_meta_layers(d, sc, slot, st.last_cut, st.status, cut_layer, st.ub);
 }
 
 // ------------------------------------------------------------------------------------
@@ -981,13 +1237,18 @@ __global__ void __launch_bounds__(1024) k_scan2(const uint32_t *a, const uint32_
 
 // ------------------------------------------------------------------------------------
 // host-side launchers (called from capi.cpp)
-size_t relax_lds_bytes(int Tcap, int Lcap) { return lds_carve(Tcap, Lcap).bytes; }
+size_t relax_lds_bytes(int Tcap, int Lcap, int cb) { return lds_carve(Tcap, Lcap, cb).bytes; }
 
 hipError_t launch_relax(const NetDev &net, const Scratch &sc, const BatchIn &in, const Pool &pool,
-                        const BatchOut &out, double incumbent, hipStream_t st) {
+                        const BatchOut &out, double incumbent, int cb, hipStream_t st) {
     if (in.n <= 0) return hipSuccess;
-    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap);
-    hipLaunchKernelGGL(k_relax, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent);
+    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, cb);
+    switch (cb) {
+        case 4: hipLaunchKernelGGL(k_relax<4>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent); break;
+        case 8: hipLaunchKernelGGL(k_relax<8>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent); break;
+        case 16: hipLaunchKernelGGL(k_relax<16>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent); break;
+        default: hipLaunchKernelGGL(k_relax<1>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent); break;
+    }
     return hipGetLastError();
 }
 
@@ -999,7 +1260,7 @@ hipError_t launch_scan(const uint32_t *a, const uint32_t *b, int n, uint64_t *oa
 hipError_t launch_emit(const NetDev &net, const Scratch &sc, const BatchIn &in, const Pool &pool,
                        const BatchOut &out, const ChildOut &co, hipStream_t st) {
     if (in.n <= 0) return hipSuccess;
-    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap);
+    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, 1);
     hipLaunchKernelGGL(k_emit_children, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, co);
     return hipGetLastError();
 }
@@ -1008,7 +1269,7 @@ hipError_t launch_refine(const NetDev &net, const Scratch &sc, const BatchIn &in
                          const BatchOut &out, const int32_t *slots, const int32_t *cut_ids,
                          const uint8_t *cut_is_feas, int n, double incumbent, hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap);
+    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, 1);
     hipLaunchKernelGGL(k_refine, dim3(n), dim3(kWave), lds, st, net, sc, in, pool, out, slots, cut_ids,
                        cut_is_feas, n, incumbent);
     return hipGetLastError();

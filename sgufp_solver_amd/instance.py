@@ -151,6 +151,12 @@ def generate(cfg: InstanceConfig, seed: int, scenarios: int | None = None) -> In
     tails = np.array([a[0] for a in arcs], dtype=np.int32)
     heads = np.array([a[1] for a in arcs], dtype=np.int32)
 
+    # V-bar is drawn before any scenario data so that the network structure (and the DD
+    # built on it) is the same for every scenario count: C3 and C4 differ only in S.
+    vbar = [v for v in range(1, n - 1) if rng.random() < cfg.vbar_prob]
+    if not vbar:
+        vbar = [node(K - 1, 0)]
+
     ub = rng.integers(5, 51, size=(m, S)).astype(np.int32)
     lb = np.zeros((m, S), dtype=np.int32)
     sink_arcs = heads == sink
@@ -160,9 +166,6 @@ def generate(cfg: InstanceConfig, seed: int, scenarios: int | None = None) -> In
     r = rng.integers(-5, 31, size=m).astype(np.int32)
     reward = np.repeat(r[:, None], S, axis=1)
 
-    vbar = [v for v in range(1, n - 1) if rng.random() < cfg.vbar_prob]
-    if not vbar:
-        vbar = [node(K - 1, 0)]
     return Instance(n=n, tails=tails, heads=heads, lb=lb, ub=ub, reward=reward, vbar=vbar)
 
 

@@ -38,7 +38,7 @@ CASES = [
     ("c2_s5_feas_only", "C2", 5, 1, 12, 0, ("dfs", 120), [DMIN]),
     ("c3_s1_dfs", "C3", 1, 2, 4, 12, ("dfs", 120), [DMIN, 0.0, 300.0]),
     ("c3_s2_bfs", "C3", 2, 2, 4, 12, ("bfs", 40), [DMIN, 300.0]),
-    ("c3_s3_dfs", "C3", 3, 2, 8, 24, ("dfs", 160), [DMIN, 300.0]),
+    ("c3_s4_dfs", "C3", 4, 2, 8, 24, ("dfs", 160), [DMIN, 300.0]),
 ]
 
 
