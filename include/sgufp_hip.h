@@ -121,6 +121,10 @@ int sgufp_batch_stats(sgufp_ctx *ctx, int64_t *dd_nodes, int64_t *dd_arcs, int32
 int sgufp_batch_refine(sgufp_ctx *ctx, int n, const int32_t *node_idx, const uint8_t *is_feasibility,
                        const int32_t *cut_index, double optimal_lb);
 
+/* Diagnostics of the last relax: wall_clock64 ticks (100 MHz) of each node's wave and
+ * the number of batched-sweep restarts (exact single-cut redo after pruning). */
+int sgufp_batch_debug(sgufp_ctx *ctx, int64_t *ticks, int32_t *redo);
+
 /* -- timing (hipEvents on the ctx stream around each kernel of the last relax) -- */
 int sgufp_set_timing(sgufp_ctx *ctx, int enabled);
 int sgufp_last_timing(const sgufp_ctx *ctx, float *ms_relax, float *ms_emit);

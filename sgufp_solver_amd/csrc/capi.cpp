@@ -277,7 +277,8 @@ bool sgufp_ctx::init() {
     if (!alloc(out.status, B, "out") || !alloc(out.exact, B, "out") || !alloc(out.lb, B, "out") ||
         !alloc(out.ub, B, "out") || !alloc(out.nchild, B, "out") || !alloc(out.sol_need, B, "out") ||
         !alloc(out.dd_nodes, B, "out") || !alloc(out.dd_arcs, B, "out") || !alloc(out.dd_layers, B, "out") ||
-        !alloc(out.sweeps, B, "out") || !alloc(out.path, B * sc.Lcap, "out") || !alloc(out.path_len, B, "out"))
+        !alloc(out.sweeps, B, "out") || !alloc(out.path, B * sc.Lcap, "out") || !alloc(out.path_len, B, "out") ||
+        !alloc(out.ticks, B, "out") || !alloc(out.redo, B, "out"))
         return false;
     // batch input
     if (!alloc(d_gl, B, "batch") || !alloc(d_sollen, B, "batch") || !alloc(d_lb, B, "batch") ||
@@ -729,6 +730,20 @@ int sgufp_batch_refine(sgufp_ctx *ctx, int n, const int32_t *node_idx, const uin
                      "k_refine"))
         return SGUFP_ERR_HIP;
     return ctx->sync() ? SGUFP_OK : SGUFP_ERR_HIP;
+}
+
+int sgufp_batch_debug(sgufp_ctx *ctx, int64_t *ticks, int32_t *redo) {
+    if (!ctx || !ctx->relaxed) return ctx ? SGUFP_ERR_STATE : SGUFP_ERR_ARG;
+    const int n = ctx->n;
+    std::vector<uint64_t> t(n);
+    std::vector<uint32_t> r(n);
+    if (!ctx->download(t.data(), ctx->out.ticks, n) || !ctx->download(r.data(), ctx->out.redo, n) || !ctx->sync())
+        return SGUFP_ERR_HIP;
+    for (int k = 0; k < n; k++) {
+        if (ticks) ticks[k] = (int64_t)t[k];
+        if (redo) redo[k] = (int32_t)r[k];
+    }
+    return SGUFP_OK;
 }
 
 int sgufp_set_timing(sgufp_ctx *ctx, int enabled) {

@@ -109,6 +109,8 @@ struct BatchOut {
     uint32_t *sweeps;          // cuts swept over this node's DD
     int16_t *path;             // [max_batch * Lcap] argmax path of exact DDs
     uint16_t *path_len;
+    uint64_t *ticks;           // wall_clock64 ticks (100 MHz) spent by each node's wave
+    uint32_t *redo;            // batched sweeps restarted after an exact single-cut redo
 };
 
 // Children written by the emit kernel (device-resident frontier format).

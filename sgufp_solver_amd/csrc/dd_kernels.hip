@@ -107,6 +107,9 @@ struct DD {
     double *buf0, *buf1;
     double *coef;     // [kMaxU] per-rank coefficients of the layer being swept
     int16_t *walk;    // [Tcap] decisions collected by a path walk
+    double *sm1;      // [Tcap] width-1 layers: state2 of the single node (last single sweep)
+    double *xm1;      // [Tcap] width-1 layers: min over its in-arcs of parent.state2 + weight
+    uint8_t *v1;      // [Tcap] summary valid (layer had one alive node during that sweep)
     // HBM (slot base applied)
     uint32_t *ntopo;
     uint8_t *nflag;
@@ -122,7 +125,7 @@ struct DD {
 
 struct LdsCarve {
     size_t bytes;
-    size_t o_lay, o_rslot, o_buf, o_coef, o_walk, o_bcoef, o_w1, o_ids;
+    size_t o_lay, o_rslot, o_buf, o_coef, o_walk, o_bcoef, o_w1, o_ids, o_sm1, o_xm1, o_v1;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -140,6 +143,9 @@ __host__ __device__ inline LdsCarve lds_carve(int Tcap, int Lcap, int cb) {
     c.o_bcoef = o; o = align16(o + (cb > 1 ? (size_t)cb * kMaxU * 8 : 0));
     c.o_w1 = o; o = align16(o + (cb > 1 ? (size_t)Tcap : 0));
     c.o_ids = o; o = align16(o + (cb > 1 ? (size_t)cb * 4 : 0));
+    c.o_sm1 = o; o = align16(o + (size_t)Tcap * 8);
+    c.o_xm1 = o; o = align16(o + (size_t)Tcap * 8);
+    c.o_v1 = o; o = align16(o + (size_t)Tcap);
     c.bytes = o;
     return c;
 }
@@ -157,6 +163,9 @@ __device__ inline void dd_bind(DD &d, uint8_t *smem, const Scratch &sc, int slot
     d.buf1 = d.buf0 + kLdsWidth;
     d.coef = (double *)(smem + c.o_coef);
     d.walk = (int16_t *)(smem + c.o_walk);
+    d.sm1 = (double *)(smem + c.o_sm1);
+    d.xm1 = (double *)(smem + c.o_xm1);
+    d.v1 = smem + c.o_v1;
     size_t N = (size_t)slot * sc.Ncap, A = (size_t)slot * sc.Acap;
     d.ntopo = sc.ntopo + N;
     d.nflag = sc.nflag + N;
@@ -339,12 +348,14 @@ __device__ void dd_sweep(const NetDev &net, DD &d, const double *row, double roo
         d.s2[0] = root_value;
         d.buf0[0] = root_value;
     }
+    for (int k = lane(); k < d.T; k += kWave) d.v1[k] = 0;
     wave_lds_sync();
     for (int k = 1; k < d.T; k++) {
         const uint32_t noff = d.noff[k], n = d.nn[k];
         const uint32_t pnoff = d.noff[k - 1], pn = d.nn[k - 1];
         const bool prev_lds = pn <= (uint32_t)kLdsWidth;
         const bool cur_lds = n <= (uint32_t)kLdsWidth;
+        const bool w1 = d.nalive[k] == 1;
         double *pbuf = (k & 1) ? d.buf0 : d.buf1;
         double *cbuf = (k & 1) ? d.buf1 : d.buf0;
         load_layer_coef(net, d, k, row);
@@ -354,6 +365,7 @@ __device__ void dd_sweep(const NetDev &net, DD &d, const double *row, double roo
             // merged node: max over its alive incoming arcs, in creation order
             const uint32_t aoff = d.aoff[k];
             VP best{0.0, INT_MIN};
+            double xmin = DMAX;
             for (uint32_t base = 0; base < acnt; base += kWave) {
                 uint32_t a = base + lane();
                 if (a < acnt && (d.aflag[aoff + a] & kAlive)) {
@@ -361,17 +373,19 @@ __device__ void dd_sweep(const NetDev &net, DD &d, const double *row, double roo
                     uint32_t p = t & kParentMask, r = t >> kRankShift;
                     double x = prev_lds ? pbuf[p] : d.s2[pnoff + p];
                     VP c;
-                    if (r != 0) { c.v = x + d.coef[r]; c.p = prio_new((int)a); }
-                    else { c.v = x; c.p = prio_old((int)a); }
+                    if (r != 0) { c.v = x + d.coef[r]; c.p = prio_new((int)a); xmin = fmin(xmin, c.v); }
+                    else { c.v = x; c.p = prio_old((int)a); xmin = fmin(xmin, x + 0.0); }
                     best = vp_pick(best, c);
                 }
             }
             best = wave_vp(best);
+#pragma unroll
+            for (int sft = kWave / 2; sft; sft >>= 1) xmin = fmin(xmin, __shfl_xor(xmin, sft, kWave));
             double v = (best.p == INT_MIN) ? DMIN : smax(best.v, DMIN);
-            // an empty fold leaves DOUBLE_MIN; a -1 arc equal to DOUBLE_MIN keeps the initial value (same bits)
             if (lane() == 0) {
                 d.s2[noff] = v;
                 cbuf[0] = v;
+                if (w1) { d.sm1[k] = v; d.xm1[k] = xmin; d.v1[k] = 1; }
             }
         } else {
             for (uint32_t base = 0; base < n; base += kWave) {
@@ -382,14 +396,16 @@ __device__ void dd_sweep(const NetDev &net, DD &d, const double *row, double roo
                     if (f & kAlive) {
                         uint32_t t = d.ntopo[node];
                         uint32_t p = t & kParentMask, r = t >> kRankShift;
-                        double x;
+                        double x, y = DMAX;
                         if (!(f & kInAlive)) x = DMIN;
                         else {
-                            x = prev_lds ? pbuf[p] : d.s2[pnoff + p];
-                            if (r != 0) x = x + d.coef[r];
+                            double px = prev_lds ? pbuf[p] : d.s2[pnoff + p];
+                            if (r != 0) { x = px + d.coef[r]; y = x; }
+                            else { x = px; y = px + 0.0; }
                         }
                         d.s2[node] = x;
                         if (cur_lds) cbuf[i] = x;
+                        if (w1) { d.sm1[k] = x; d.xm1[k] = y; d.v1[k] = 1; }
                     }
                 }
             }
@@ -424,58 +440,83 @@ __device__ inline uint32_t layer_single(const DD &d, int k) {
     return found;
 }
 
-// Width-1 arc pruning over layers [first, end) (DD.cpp:3895-3928, 3987-4021).
-// Returns false when a width-1 layer would lose all of its incoming arcs.
-__device__ bool dd_prune(const NetDev &net, DD &d, const double *row, int first, int end, double thresh) {
-    const int last = d.T - 1;
-    VP mx = layer_max_first(d, last, [&](uint32_t node) { return d.s2[node]; });
-    const double maxState = (mx.p == INT_MIN) ? DMIN : smax(DMIN, mx.v);
-    for (int k = first; k < end; k++) {
-        if (d.nalive[k] != 1) continue;
-        const uint32_t M = layer_single(d, k);
-        const double gain = maxState - d.s2[M];
-        const uint32_t pnoff = d.noff[k - 1];
-        load_layer_coef(net, d, k, row);
-        wave_lds_sync();
-        const uint32_t acnt = d.acnt[k];
-        uint32_t total = 0, pruned = 0;
-        if (acnt) {
-            const uint32_t aoff = d.aoff[k];
-            for (uint32_t base = 0; base < acnt; base += kWave) {
-                uint32_t a = base + lane();
-                bool alive = a < acnt && (d.aflag[aoff + a] & kAlive);
-                bool pr = false;
-                if (alive) {
-                    uint32_t t = d.atopo[aoff + a];
-                    uint32_t p = t & kParentMask, r = t >> kRankShift;
-                    double w = (r == 0) ? 0.0 : d.coef[r];
-                    pr = ((d.s2[pnoff + p] + w) + gain) <= thresh;
-                    if (pr) {
-                        d.aflag[aoff + a] = 0;
-                        atomicSub(&d.outcnt[pnoff + p], 1u);
-                    }
-                }
-                total += wave_sum(alive ? 1u : 0u);
-                pruned += wave_sum(pr ? 1u : 0u);
-            }
-        } else {
-            uint32_t t = d.ntopo[M];
-            uint8_t f = d.nflag[M];
-            uint32_t p = t & kParentMask, r = t >> kRankShift;
-            if (f & kInAlive) {
-                total = 1;
+// Exact pruning of one width-1 layer (the body of the loops at DD.cpp:3899-3924 /
+// 3991-4016): every alive in-arc with parent.state2 + weight + gain <= thresh goes.
+// Returns false when all of them would go (the caller returns false / DOUBLE_MIN).
+__device__ bool dd_prune_layer(const NetDev &net, DD &d, const double *row, int k, double maxState, double thresh) {
+    const uint32_t M = layer_single(d, k);
+    const double gain = maxState - d.s2[M];
+    const uint32_t pnoff = d.noff[k - 1];
+    load_layer_coef(net, d, k, row);
+    wave_lds_sync();
+    const uint32_t acnt = d.acnt[k];
+    uint32_t total = 0, pruned = 0;
+    if (acnt) {
+        const uint32_t aoff = d.aoff[k];
+        for (uint32_t base = 0; base < acnt; base += kWave) {
+            uint32_t a = base + lane();
+            bool alive = a < acnt && (d.aflag[aoff + a] & kAlive);
+            bool pr = false;
+            if (alive) {
+                uint32_t t = d.atopo[aoff + a];
+                uint32_t p = t & kParentMask, r = t >> kRankShift;
                 double w = (r == 0) ? 0.0 : d.coef[r];
-                if (((d.s2[pnoff + p] + w) + gain) <= thresh) {
-                    pruned = 1;
-                    if (lane() == 0) {
-                        d.nflag[M] = f & (uint8_t)~kInAlive;
-                        d.outcnt[pnoff + p] -= 1u;
-                    }
+                pr = ((d.s2[pnoff + p] + w) + gain) <= thresh;
+                if (pr) {
+                    d.aflag[aoff + a] = 0;
+                    atomicSub(&d.outcnt[pnoff + p], 1u);
+                }
+            }
+            total += wave_sum(alive ? 1u : 0u);
+            pruned += wave_sum(pr ? 1u : 0u);
+        }
+    } else {
+        uint32_t t = d.ntopo[M];
+        uint8_t f = d.nflag[M];
+        uint32_t p = t & kParentMask, r = t >> kRankShift;
+        if (f & kInAlive) {
+            total = 1;
+            double w = (r == 0) ? 0.0 : d.coef[r];
+            if (((d.s2[pnoff + p] + w) + gain) <= thresh) {
+                pruned = 1;
+                if (lane() == 0) {
+                    d.nflag[M] = f & (uint8_t)~kInAlive;
+                    d.outcnt[pnoff + p] -= 1u;
                 }
             }
         }
-        wave_mem_sync();
-        if (total == pruned) return false;
+    }
+    wave_mem_sync();
+    return total != pruned;
+}
+
+// Does any width-1 layer in [first, end) prune something?  From per-layer summaries:
+// rounding is monotone, so some arc satisfies fl(fl(s + w) + gain) <= thresh exactly
+// when fl(xmin + gain) <= thresh.  Layers without a summary count as firing.
+// Returns a 64-bit mask of firing layers for the 64-layer window starting at `base`.
+__device__ inline uint64_t prune_fire(const DD &d, int base, int end, double maxState, double thresh,
+                                      const double *sm, const double *xm, int stride, const uint8_t *valid) {
+    int k = base + lane();
+    bool fire = false;
+    if (k < end && d.nalive[k] == 1) {
+        if (!valid[k]) fire = true;
+        else fire = (xm[(size_t)k * stride] + (maxState - sm[(size_t)k * stride])) <= thresh;
+    }
+    return __ballot(fire);
+}
+
+// Width-1 arc pruning over layers [first, end) (DD.cpp:3895-3928, 3987-4021), after a
+// single-cut sweep (s2 and the sm1/xm1 summaries hold this cut).  Returns false when a
+// width-1 layer would lose all of its incoming arcs.
+__device__ bool dd_prune(const NetDev &net, DD &d, const double *row, int first, int end, double thresh,
+                         double maxState) {
+    for (int base = first; base < end; base += kWave) {
+        uint64_t b = prune_fire(d, base, end, maxState, thresh, d.sm1, d.xm1, 1, d.v1);
+        while (b) {
+            int k = base + (int)(__ffsll((unsigned long long)b) - 1);
+            b &= b - 1;
+            if (!dd_prune_layer(net, d, row, k, maxState, thresh)) return false;
+        }
     }
     return true;
 }
@@ -490,22 +531,39 @@ struct LastVals {
 // Last-layer removal (state2 < -0.01, DD.cpp:3880-3893) and the bottom-up deletion
 // cascade (removeNode / bottomUpDelete / updateTree, DD.cpp:4040-4153).  Returns false
 // when every alive last-layer node would go (the reference returns false there).
-__device__ bool dd_remove_last(DD &d, const LastVals &lv) {
+// maxState = max state2 over the surviving last layer (the value the pruning uses).
+constexpr int kUnroll = 4;
+
+__device__ bool dd_remove_last(DD &d, const LastVals &lv, double &maxState) {
     const int last = d.T - 1;
     const uint32_t lo = d.noff[last], ln = d.nn[last];
     uint32_t rm = 0;
-    for (uint32_t base = 0; base < ln; base += kWave) {
-        uint32_t i = base + lane();
-        bool kill = false;
-        if (i < ln) {
-            uint8_t f = d.nflag[lo + i];
-            if ((f & kAlive) && lv(i) < -0.01) {
-                kill = true;
-                d.nflag[lo + i] = f | kKill;
+    VP mx{0.0, INT_MIN};
+    for (uint32_t base = 0; base < ln; base += kUnroll * kWave) {
+        uint8_t f[kUnroll];
+        double v[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {
+            uint32_t i = base + u * kWave + lane();
+            f[u] = i < ln ? d.nflag[lo + i] : 0;
+            v[u] = i < ln ? lv(i) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {
+            uint32_t i = base + u * kWave + lane();
+            if (f[u] & kAlive) {
+                if (v[u] < -0.01) {
+                    d.nflag[lo + i] = f[u] | kKill;
+                    rm++;
+                } else {
+                    mx = vp_pick(mx, VP{v[u], prio_old((int)i)});
+                }
             }
         }
-        rm += wave_sum(kill ? 1u : 0u);
     }
+    rm = wave_sum(rm);
+    mx = wave_vp(mx);
+    maxState = (mx.p == INT_MIN) ? DMIN : smax(DMIN, mx.v);
     if (rm == d.nalive[last]) return false;
     if (rm) {
         wave_mem_sync();
@@ -567,39 +625,55 @@ __device__ bool dd_remove_last(DD &d, const LastVals &lv) {
 }
 
 // Terminal arcs of an optimality cut: weight = min(weight, parent.state2), terminal
-// state = max over them (DD.cpp:3975-3984).
-__device__ double dd_terminal(DD &d, const LastVals &lv) {
+// state = max over them (DD.cpp:3975-3984); also maxState over the last layer.
+__device__ double dd_terminal(DD &d, const LastVals &lv, double &maxState) {
     const int last = d.T - 1;
     const uint32_t lo = d.noff[last], ln = d.nn[last];
-    VP best{0.0, INT_MIN};
-    for (uint32_t base = 0; base < ln; base += kWave) {
-        uint32_t i = base + lane();
-        if (i < ln && (d.nflag[lo + i] & kAlive)) {
-            double w = smin(d.tw[lo + i], lv(i));
-            d.tw[lo + i] = w;
-            best = vp_pick(best, VP{w, prio_old((int)i)});
+    VP best{0.0, INT_MIN}, mx{0.0, INT_MIN};
+    for (uint32_t base = 0; base < ln; base += kUnroll * kWave) {
+        uint8_t f[kUnroll];
+        double v[kUnroll], w[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {
+            uint32_t i = base + u * kWave + lane();
+            f[u] = i < ln ? d.nflag[lo + i] : 0;
+            v[u] = i < ln ? lv(i) : 0.0;
+            w[u] = i < ln ? d.tw[lo + i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {
+            uint32_t i = base + u * kWave + lane();
+            if (f[u] & kAlive) {
+                double nw = smin(w[u], v[u]);
+                d.tw[lo + i] = nw;
+                best = vp_pick(best, VP{nw, prio_old((int)i)});
+                mx = vp_pick(mx, VP{v[u], prio_old((int)i)});
+            }
         }
     }
     best = wave_vp(best);
+    mx = wave_vp(mx);
     wave_mem_sync();
+    maxState = (mx.p == INT_MIN) ? DMIN : smax(DMIN, mx.v);
     return (best.p == INT_MIN) ? DMIN : smax(DMIN, best.v);
 }
 
 // applyFeasibilityCut after a single-cut sweep.
 __device__ bool dd_post_feasibility(const NetDev &net, DD &d, const double *row) {
-    const uint32_t lo = d.noff[d.T - 1];
-    if (!dd_remove_last(d, LastVals{d.s2 + lo, 1})) return false;
-    if (!d.exact) return dd_prune(net, d, row, 1, d.T - 1, -0.01);
+    double maxState;
+    if (!dd_remove_last(d, LastVals{d.s2 + d.noff[d.T - 1], 1}, maxState)) return false;
+    if (!d.exact) return dd_prune(net, d, row, 1, d.T - 1, -0.01, maxState);
     return true;
 }
 
 // applyOptimalityCut after a single-cut sweep.  Returns the terminal state (or DOUBLE_MIN).
 __device__ double dd_post_optimality(const NetDev &net, DD &d, const double *row, double optimal) {
     const int last = d.T - 1;
-    const double term = dd_terminal(d, LastVals{d.s2 + d.noff[last], 1});
+    double maxState;
+    const double term = dd_terminal(d, LastVals{d.s2 + d.noff[last], 1}, maxState);
     if (term <= optimal) return term;
     if (!d.exact) {
-        if (!dd_prune(net, d, row, 3, last - 1, optimal - 0.01)) return DMIN;
+        if (!dd_prune(net, d, row, 3, last - 1, optimal - 0.01, maxState)) return DMIN;
     }
     return term;
 }
@@ -730,27 +804,13 @@ __device__ void dd_sweep_batch(const NetDev &net, DD &d, BatchView &bv, const Po
 }
 
 // Pruning test of one cut from the batch summaries over layers [first, end):
-// 0 = nothing pruned, 1 = redo this cut exactly (some arc is pruned, or a width-1
-// layer has no summary because deletions made it width-1 inside the batch).
+// true = redo this cut exactly (some arc is pruned, or a width-1 layer has no summary
+// because deletions made it width-1 inside the batch).
 template <int CB>
-__device__ int dd_prune_check(const DD &d, const BatchView &bv, const LastVals &lv, int c, int first, int end,
-                              double thresh) {
-    const int last = d.T - 1;
-    VP mx = layer_max_first(d, last, [&](uint32_t node) { return lv(node - d.noff[last]); });
-    const double maxState = (mx.p == INT_MIN) ? DMIN : smax(DMIN, mx.v);
-    for (int k = first; k < end; k++) {
-        if (d.nalive[k] != 1) continue;
-        if (!bv.w1[k]) return 1;
-        const double gain = maxState - bv.sm[(size_t)k * CB + c];
-        if ((bv.xm[(size_t)k * CB + c] + gain) <= thresh) return 1;
-    }
-    return 0;
-}
-
-// any layer in [first, end) that became width-1 after the batch started
-__device__ inline bool dd_new_width1(const DD &d, const BatchView &bv, int first, int end) {
-    for (int k = first; k < end; k++)
-        if (d.nalive[k] == 1 && !bv.w1[k]) return true;
+__device__ bool dd_prune_check(const DD &d, const BatchView &bv, int c, int first, int end, double thresh,
+                               double maxState) {
+    for (int base = first; base < end; base += kWave)
+        if (prune_fire(d, base, end, maxState, thresh, bv.sm + c, bv.xm + c, CB, bv.w1)) return true;
     return false;
 }
 
@@ -885,6 +945,7 @@ struct LoopState {
     double ub;
     int last_cut;
     uint32_t applied;
+    uint32_t redo;
 };
 
 // one cut at a time from pool position s onwards
@@ -948,24 +1009,25 @@ __device__ void cut_loop_batched(const NetDev &net, DD &d, const Scratch &sc, Ba
             st.last_cut = id;
             st.applied++;
             bool redo = false;
+            double maxState;
             if (seq < pool.nf) {
-                if (!dd_remove_last(d, lv)) { st.status = kPrunedFeasibility; return; }
-                if (!d.exact && dd_prune_check<CB>(d, bv, lv, c, 1, last, -0.01)) {
+                if (!dd_remove_last(d, lv, maxState)) { st.status = kPrunedFeasibility; return; }
+                if (!d.exact && dd_prune_check<CB>(d, bv, c, 1, last, -0.01, maxState)) {
                     dd_sweep(net, d, row, __shfl(rv, c, kWave));
-                    if (!dd_prune(net, d, row, 1, last, -0.01)) { st.status = kPrunedFeasibility; return; }
+                    if (!dd_prune(net, d, row, 1, last, -0.01, maxState)) { st.status = kPrunedFeasibility; return; }
                     redo = true;
                 }
             } else {
-                double v = dd_terminal(d, lv);
-                if (v > incumbent && !d.exact && dd_prune_check<CB>(d, bv, lv, c, 3, last - 1, incumbent - 0.01)) {
+                double v = dd_terminal(d, lv, maxState);
+                if (v > incumbent && !d.exact && dd_prune_check<CB>(d, bv, c, 3, last - 1, incumbent - 0.01, maxState)) {
                     dd_sweep(net, d, row, __shfl(rv, c, kWave));
-                    if (!dd_prune(net, d, row, 3, last - 1, incumbent - 0.01)) v = DMIN;
+                    if (!dd_prune(net, d, row, 3, last - 1, incumbent - 0.01, maxState)) v = DMIN;
                     redo = true;
                 }
                 st.ub = d.exact ? v : smin(v, st.ub);
                 if (st.ub <= incumbent) { st.status = kPrunedOptimality; return; }
             }
-            if (redo) { next = seq + 1; break; }
+            if (redo) { next = seq + 1; st.redo++; break; }
         }
         s = next;
     }
@@ -979,6 +1041,7 @@ __global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int slot = blockIdx.x;
     if (slot >= in.n) return;
+    const uint64_t t_start = wall_clock64();
     DD d;
     dd_bind(d, smem, sc, slot, CB);
     d.g = in.gl[slot];
@@ -986,7 +1049,7 @@ __global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn
     const int16_t *rsol = in.sol + in.sol_off[slot];
     d.aligned = (d.len == d.g) ? 1 : 0;
     int cut_layer = 0;
-    LoopState st{kSuccess, in.ub[slot], -1, 0};
+    LoopState st{kSuccess, in.ub[slot], -1, 0, 0};
     double lb = DMIN;
     uint32_t nchild = 0, n_nodes = 0, n_arcs = 0;
     d.T = 1; d.exact = 1;
@@ -1069,8 +1132,10 @@ done:
         out.dd_arcs[slot] = n_arcs;
         out.dd_layers[slot] = (uint32_t)d.T + 1;
         out.sweeps[slot] = st.applied;
+        out.redo[slot] = st.redo;
     }
     store_meta_layers(d, sc, slot, st.last_cut, st.status, cut_layer, st.ub);
+    if (lane() == 0) out.ticks[slot] = wall_clock64() - t_start;
 }
 
 // ------------------------------------------------------------------------------------

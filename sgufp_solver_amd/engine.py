@@ -26,7 +26,7 @@ EXPORTS = [
     "sgufp_cuts_clear", "sgufp_cuts_count", "sgufp_batch_upload", "sgufp_batch_relax",
     "sgufp_batch_sync", "sgufp_batch_results", "sgufp_batch_children_size", "sgufp_batch_children",
     "sgufp_batch_paths", "sgufp_batch_stats", "sgufp_batch_refine", "sgufp_set_timing",
-    "sgufp_last_timing", "sgufp_probe_network",
+    "sgufp_last_timing", "sgufp_probe_network", "sgufp_batch_debug",
 ]
 
 
@@ -73,6 +73,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.sgufp_set_timing.argtypes = [P, C.c_int]
     lib.sgufp_last_timing.argtypes = [P, P, P]
     lib.sgufp_probe_network.argtypes = [C.c_char_p, P, P, C.c_int32, P, P]
+    lib.sgufp_batch_debug.argtypes = [P, P, P]
     _lib = lib
     return lib
 
@@ -295,6 +296,12 @@ class Engine:
         self._check(self.lib.sgufp_batch_children(self.ctx, _ptr(child_off), _ptr(gl), _ptr(lb), _ptr(ub), _ptr(soff),
                                                   _ptr(states), _ptr(poff), _ptr(sol)))
         return child_off, gl, lb, ub, soff, states, poff, sol
+
+    def debug(self):
+        t = np.zeros(self.n, dtype=np.int64)
+        r = np.zeros(self.n, dtype=np.int32)
+        self._check(self.lib.sgufp_batch_debug(self.ctx, _ptr(t), _ptr(r)))
+        return t, r
 
     def children_batch(self) -> BatchArrays:
         """All cutset children of the last relaxed batch as a new batch (node order kept)."""
