@@ -17,7 +17,7 @@
 
 namespace sgufp {
 // dd_kernels.hip
-size_t relax_lds_bytes(int Tcap, int Lcap, int cb);
+size_t relax_lds_bytes(int Tcap, int Lcap, int cb, int mcap);
 hipError_t launch_relax(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &, double, int,
                         hipStream_t);
 hipError_t launch_scan(const uint32_t *, const uint32_t *, int, uint64_t *, uint64_t *, hipStream_t);
@@ -58,7 +58,7 @@ struct sgufp_ctx {
     int row_cap = 0, n_rows = 0;
     double *d_rows = nullptr, *d_rhs = nullptr, *d_coefT = nullptr;
     int ustride = 1;
-    int cb = 16;                              // cuts per batched sweep
+    int cb = 8;                               // cuts per batched sweep
     std::vector<int32_t> f_rows, o_rows;      // insertion order, row ids
     int32_t *d_forder = nullptr, *d_oorder = nullptr;
     int order_cap = 0;
@@ -254,12 +254,18 @@ bool sgufp_ctx::init() {
     int64_t ncap = node_bound(net, &tail);
     ustride = std::max(1, net.max_states);
     if (const char *e = getenv("SGUFP_CUT_BATCH")) cb = atoi(e);
-    if (cb != 1 && cb != 4 && cb != 8 && cb != 16) cb = 16;
+    if (cb != 1 && cb != 4 && cb != 8 && cb != 16) cb = 8;
     int64_t acap = std::max<int64_t>(1, (int64_t)std::max(0, L - 4) * (kRelaxedMaxWidth - 1) * maxU);
     if (ncap > (int64_t)kParentMask || acap > (int64_t)0x7FFFFFFF) { err = "DD capacity beyond 22-bit indices"; return false; }
     sc.Ncap = (int)ncap;
     sc.Acap = (int)acap;
-    if (relax_lds_bytes(sc.Tcap, sc.Lcap, cb) > 64 * 1024) { err = "too many layers for the LDS layer table"; return false; }
+    // LDS per relax workgroup: SGUFP_LDS_KB (default 64); what the fixed carve leaves is
+    // the narrow-layer topology mirror
+    size_t lds_budget = 64 * 1024;
+    if (const char *e = getenv("SGUFP_LDS_KB")) lds_budget = (size_t)atoi(e) * 1024;
+    size_t base_lds = relax_lds_bytes(sc.Tcap, sc.Lcap, cb, 0);
+    if (base_lds > lds_budget || base_lds > 160 * 1024) { err = "too many layers for the LDS layer table"; return false; }
+    sc.mir_cap = cb > 1 ? (int)((lds_budget - base_lds) / 2) : 0;
     sc.tail_cap = (int)tail;
     sc.cb_max = cb;
     const size_t B = (size_t)max_batch;

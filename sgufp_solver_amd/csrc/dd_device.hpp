@@ -66,6 +66,7 @@ struct Scratch {
     // multi-cut sweeps (k_relax with CB > 1)
     int tail_cap;      // nodes of the HBM-resident tail layers (wide layers + last layer)
     int cb_max;        // cuts per batched sweep the buffers are sized for
+    int mir_cap;       // LDS mirror entries (16-bit) of the narrow-layer topology
     double *s2b;       // [tail_cap * cb_max]
     double *sm;        // [Tcap * cb_max]
     double *xm;        // [Tcap * cb_max]

@@ -119,19 +119,37 @@ struct DD {
     double *tw;
     uint32_t *atopo;
     uint8_t *aflag;
+    uint16_t *mir;    // LDS mirror of the narrow layers' topology (see build_mirror)
     // scalars
     int g, len, T, exact, aligned;
+    int kg;           // first layer wider than kLdsBatchWidth (or the last layer)
+    uint32_t Nn;      // nodes in layers < kg (mirrored node words)
+    uint32_t Amir;    // merged-layer arcs (all in layers < kg)
+    int mirror;       // mirror valid
 };
+
+constexpr int kLdsBatchWidth = 128;
+constexpr uint16_t kMirParent = 127, kMirRankShift = 7, kMirAlive = 1u << 12, kMirIn = 1u << 13;
+
+// LDS mirror of the narrow layers: node word = parent:7 | rank:5 | alive | in-arc alive,
+// merged-arc word = parent:7 | rank:5 | alive.  HBM stays the master copy; every edit of
+// a narrow node / arc flag is applied to both.
+__device__ inline void mir_node_clear(DD &d, uint32_t node, uint16_t bits) {
+    if (d.mirror && node < d.Nn) d.mir[node] &= (uint16_t)~bits;
+}
+__device__ inline void mir_arc_clear(DD &d, uint32_t a) {
+    if (d.mirror) d.mir[d.Nn + a] &= (uint16_t)~kMirAlive;
+}
 
 struct LdsCarve {
     size_t bytes;
-    size_t o_lay, o_rslot, o_buf, o_coef, o_walk, o_bcoef, o_w1, o_ids, o_sm1, o_xm1, o_v1;
+    size_t o_lay, o_rslot, o_buf, o_coef, o_walk, o_bcoef, o_w1, o_ids, o_sm1, o_xm1, o_v1, o_mir;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // cb = cuts per batched sweep (1 = single-cut kernels only)
-__host__ __device__ inline LdsCarve lds_carve(int Tcap, int Lcap, int cb) {
+__host__ __device__ inline LdsCarve lds_carve(int Tcap, int Lcap, int cb, int mcap = 0) {
     LdsCarve c;
     size_t o = 0;
     size_t single = (size_t)2 * kLdsWidth * 8, batch = (size_t)2 * 128 * (cb > 1 ? cb : 0) * 8;
@@ -146,6 +164,7 @@ __host__ __device__ inline LdsCarve lds_carve(int Tcap, int Lcap, int cb) {
     c.o_sm1 = o; o = align16(o + (size_t)Tcap * 8);
     c.o_xm1 = o; o = align16(o + (size_t)Tcap * 8);
     c.o_v1 = o; o = align16(o + (size_t)Tcap);
+    c.o_mir = o; o = align16(o + (cb > 1 ? (size_t)mcap * 2 : 0));
     c.bytes = o;
     return c;
 }
@@ -220,7 +239,7 @@ __device__ inline void load_layer_coef(const NetDev &net, const DD &d, int k, co
 // ------------------------------------------------------------------------------------
 // Build (buildTree + buildNextLayer).  Returns false on capacity overflow.
 __device__ bool dd_build(const NetDev &net, DD &d, const Scratch &sc, uint32_t root_mask, uint32_t &n_nodes,
-                         uint32_t &n_arcs) {
+                         uint32_t &n_arcs, uint32_t &n_merged) {
     const int L = net.L;
     if (lane() == 0) {
         d.ntopo[0] = kNoRank << kRankShift;
@@ -337,6 +356,7 @@ __device__ bool dd_build(const NetDev &net, DD &d, const Scratch &sc, uint32_t r
     }
     n_nodes = total_nodes + 1;                                            // + terminal
     n_arcs = (total_nodes - 1 - merged_nodes) + total_arcs + ln;          // exact in-arcs + merged + terminal
+    n_merged = total_arcs;
     wave_mem_sync();
     return true;
 }
@@ -464,6 +484,7 @@ __device__ bool dd_prune_layer(const NetDev &net, DD &d, const double *row, int 
                 pr = ((d.s2[pnoff + p] + w) + gain) <= thresh;
                 if (pr) {
                     d.aflag[aoff + a] = 0;
+                    mir_arc_clear(d, aoff + a);
                     atomicSub(&d.outcnt[pnoff + p], 1u);
                 }
             }
@@ -481,6 +502,7 @@ __device__ bool dd_prune_layer(const NetDev &net, DD &d, const double *row, int 
                 pruned = 1;
                 if (lane() == 0) {
                     d.nflag[M] = f & (uint8_t)~kInAlive;
+                    mir_node_clear(d, M, kMirIn);
                     d.outcnt[pnoff + p] -= 1u;
                 }
             }
@@ -583,6 +605,7 @@ __device__ bool dd_remove_last(DD &d, const LastVals &lv, double &maxState) {
                         if (a < acnt && (d.aflag[aoff + a] & kAlive)) {
                             uint32_t p = d.atopo[aoff + a] & kParentMask;
                             d.aflag[aoff + a] = 0;
+                            mir_arc_clear(d, aoff + a);
                             if (atomicSub(&d.outcnt[pnoff + p], 1u) == 1u) {
                                 d.nflag[pnoff + p] |= kKill;
                                 pk = true;
@@ -591,7 +614,10 @@ __device__ bool dd_remove_last(DD &d, const LastVals &lv, double &maxState) {
                         parent_killed += wave_sum(pk ? 1u : 0u);
                     }
                     wave_mem_sync();
-                    if (lane() == 0) d.nflag[M] = 0;
+                    if (lane() == 0) {
+                        d.nflag[M] = 0;
+                        mir_node_clear(d, M, kMirAlive | kMirIn);
+                    }
                 }
             } else {
                 for (uint32_t base = 0; base < n; base += kWave) {
@@ -610,6 +636,7 @@ __device__ bool dd_remove_last(DD &d, const LastVals &lv, double &maxState) {
                                 }
                             }
                             d.nflag[noff + i] = 0;
+                            mir_node_clear(d, noff + i, kMirAlive | kMirIn);
                         }
                     }
                     killed += wave_sum(kk ? 1u : 0u);
@@ -681,14 +708,19 @@ __device__ double dd_post_optimality(const NetDev &net, DD &d, const double *row
 // ------------------------------------------------------------------------------------
 // Multi-cut sweeps.  Deleting nodes never changes state2 of the nodes that stay (an
 // alive node keeps every non-pruned in-arc and the tails of those arcs stay alive), so
-// the sweeps of CB consecutive pool cuts can run together over the same DD and their
-// removal / terminal / early-exit logic be replayed in pool order afterwards.  Only
-// width-1 arc pruning changes later sweeps: per (width-1 layer, cut) the sweep records
-// the single node's state2 and the smallest parent.state2 + weight over its in-arcs;
-// since rounding is monotone, "some arc is pruned" <=> fl(xmin + gain) <= threshold.
-// When that fires (or deletions make a new width-1 layer), the cut is redone with the
-// exact single-cut path and the batch restarts after it.
-constexpr int kLdsBatchWidth = 128;   // layers up to this width keep their CB values in LDS
+// the sweeps of CB consecutive pool cuts of one type can run together over the same DD
+// and their removal / terminal / early-exit logic be replayed in pool order afterwards.
+// Only width-1 arc pruning changes later sweeps: per (width-1 layer, cut) the sweep
+// records the single node's state2 and the smallest parent.state2 + weight over its
+// in-arcs; since rounding is monotone, "some arc is pruned" <=> fl(xmin + gain) <=
+// threshold.  When that fires (or deletions make a new width-1 layer) the cut is redone
+// with the exact single-cut path and the batch restarts after it.
+//
+// Layout during a batch: the narrow layers (< 128 nodes: every layer but the last
+// few) keep their CB values per node in LDS, and -- when it fits -- their topology in
+// an LDS mirror of 16-bit words, so that a layer step touches no HBM; the wide tail
+// layers stream through HBM (s2b, CB values per node); for optimality batches the last
+// layer is never materialised: two fused passes compute the leaf values on the fly.
 
 struct BatchView {
     double *vb;        // LDS [2][kLdsBatchWidth][CB]
@@ -697,39 +729,93 @@ struct BatchView {
     int32_t *ids;      // LDS [CB]: pool row of each batch cut
     double *s2b;       // HBM [tail_cap][CB]: layers >= kg
     double *sm, *xm;   // HBM [Tcap][CB]
-    int kg;            // first layer kept in HBM (a wide layer, or the last layer)
     uint32_t gbase;    // noff[kg]
 };
 
-template <int CB>
-__device__ void dd_sweep_batch(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int nb, double rv) {
+
+__device__ inline void build_mirror(DD &d, uint32_t n_merged_arcs, int mcap) {
+    int kg = d.T - 1;
+    for (int base = 0; base < d.T - 1; base += kWave) {
+        int k = base + lane();
+        uint64_t b = __ballot(k < d.T - 1 && d.nn[k] > (uint32_t)kLdsBatchWidth);
+        if (b) { kg = base + (int)(__ffsll((unsigned long long)b) - 1); break; }
+    }
+    d.kg = kg;
+    d.Nn = d.noff[kg];
+    d.Amir = n_merged_arcs;
+    d.mirror = (mcap > 0 && d.Nn + d.Amir <= (uint32_t)mcap) ? 1 : 0;
+    if (!d.mirror) return;
+    for (uint32_t i = lane(); i < d.Nn; i += kWave) {
+        uint32_t t = d.ntopo[i];
+        uint8_t f = d.nflag[i];
+        d.mir[i] = (uint16_t)((t & kMirParent) | (((t >> kRankShift) & 31u) << kMirRankShift) |
+                              ((f & kAlive) ? kMirAlive : 0) | ((f & kInAlive) ? kMirIn : 0));
+    }
+    for (uint32_t a = lane(); a < d.Amir; a += kWave) {
+        uint32_t t = d.atopo[a];
+        d.mir[d.Nn + a] = (uint16_t)((t & kMirParent) | (((t >> kRankShift) & 31u) << kMirRankShift) |
+                                     ((d.aflag[a] & kAlive) ? kMirAlive : 0));
+    }
+    wave_lds_sync();
+}
+
+// coefficients of DD layer k for the batch cuts: bv.coef[c][r] (one load per entry)
+__device__ inline void batch_coef_direct(const NetDev &net, const DD &d, BatchView &bv, const Pool &pool, int k,
+                                         int nb) {
+    const int us = pool.ustride, ls = d.g + k - 1;
+    const size_t ltab = (size_t)net.L * us;
+    for (int idx = lane(); idx < nb * us; idx += kWave) {
+        int cc = idx / us, r = idx - cc * us;
+        bv.coef[idx] = pool.coefT[(size_t)bv.ids[cc] * ltab + (size_t)ls * us + r];
+    }
+    wave_lds_sync();
+}
+
+// Narrow layers 1 .. kg-1: values in LDS, topology from the mirror (MIR) or HBM.
+// s2 (single values of the batch's last cut, read later by path walks) is written for
+// layers < kS only: the cutset layer can only move up, and exact-layer steps of a walk
+// read no state2.
+template <int CB, bool MIR>
+__device__ void sweep_narrow(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int nb, double rv, int kS) {
     constexpr int G = kWave / CB;
+    constexpr int PF = (CB * kMaxU + kWave - 1) / kWave;
     const int c = lane() % CB, grp = lane() / CB;
     const bool cv = c < nb;
     const int us = pool.ustride;
     const size_t ltab = (size_t)net.L * us;
-    // layer 0: the root fold of each cut
     if (lane() < CB && cv) {
-        if (bv.kg == 0) bv.s2b[c] = rv;
-        else bv.vb[c] = rv;
+        bv.vb[c] = rv;
         if (c == nb - 1) d.s2[0] = rv;
     }
-    wave_mem_sync();
-    for (int k = 1; k < d.T; k++) {
-        const uint32_t noff = d.noff[k], n = d.nn[k];
-        const uint32_t pnoff = d.noff[k - 1];
-        const bool prev_g = (k - 1) >= bv.kg, cur_g = k >= bv.kg;
-        const double *pbuf = bv.vb + (size_t)((k - 1) & 1) * kLdsBatchWidth * CB;
-        double *cbuf = bv.vb + (size_t)(k & 1) * kLdsBatchWidth * CB;
+    // coefficient prefetch one layer ahead (registers)
+    double pf[PF];
+    auto issue = [&](int k) {
         const int ls = d.g + k - 1;
-        for (int idx = lane(); idx < nb * us; idx += kWave) {
-            int cc = idx / us, r = idx - cc * us;
-            bv.coef[cc * us + r] = pool.coefT[(size_t)bv.ids[cc] * ltab + (size_t)ls * us + r];
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            int idx = lane() + j * kWave;
+            pf[j] = 0.0;
+            if (k < d.kg && idx < nb * us) {
+                int cc = idx / us, r = idx - cc * us;
+                pf[j] = pool.coefT[(size_t)bv.ids[cc] * ltab + (size_t)ls * us + r];
+            }
+        }
+    };
+    if (d.kg > 1) issue(1);
+    for (int k = 1; k < d.kg; k++) {
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            int idx = lane() + j * kWave;
+            if (idx < nb * us) bv.coef[idx] = pf[j];
         }
         wave_lds_sync();
-        auto prevv = [&](uint32_t p) -> double {
-            return prev_g ? bv.s2b[(size_t)(pnoff + p - bv.gbase) * CB + c] : pbuf[p * CB + c];
-        };
+        issue(k + 1);
+        const uint32_t noff = d.noff[k], n = d.nn[k];
+        const uint32_t pnoff = d.noff[k - 1];
+        const double *pbuf = bv.vb + (size_t)((k - 1) & 1) * kLdsBatchWidth * CB;
+        double *cbuf = bv.vb + (size_t)(k & 1) * kLdsBatchWidth * CB;
+        const bool wr = k < kS;
+        const bool w1 = bv.w1[k] != 0;
         const uint32_t acnt = d.acnt[k];
         if (acnt) {
             const uint32_t aoff = d.aoff[k];
@@ -737,10 +823,17 @@ __device__ void dd_sweep_batch(const NetDev &net, DD &d, BatchView &bv, const Po
             double xmin = DMAX;
             bool any = false;
             for (uint32_t a = grp; a < acnt; a += G) {
-                if (cv && (d.aflag[aoff + a] & kAlive)) {
+                uint32_t p, r;
+                bool alive;
+                if (MIR) {
+                    uint16_t wd = d.mir[d.Nn + aoff + a];
+                    p = wd & kMirParent; r = (wd >> kMirRankShift) & 31u; alive = (wd & kMirAlive) != 0;
+                } else {
                     uint32_t t = d.atopo[aoff + a];
-                    uint32_t p = t & kParentMask, r = t >> kRankShift;
-                    double x = prevv(p);
+                    p = t & kParentMask; r = t >> kRankShift; alive = (d.aflag[aoff + a] & kAlive) != 0;
+                }
+                if (cv && alive) {
+                    double x = pbuf[p * CB + c];
                     VP e;
                     double y;
                     if (r != 0) { e.v = x + bv.coef[c * us + r]; e.p = prio_new((int)a); y = e.v; }
@@ -761,34 +854,40 @@ __device__ void dd_sweep_batch(const NetDev &net, DD &d, BatchView &bv, const Po
             }
             if (grp == 0 && cv) {
                 double v = (best.p == INT_MIN) ? DMIN : smax(best.v, DMIN);
-                if (cur_g) bv.s2b[(size_t)(noff - bv.gbase) * CB + c] = v;
-                else cbuf[c] = v;
-                if (c == nb - 1) d.s2[noff] = v;
-                if (bv.w1[k]) {
+                cbuf[c] = v;
+                if (wr && c == nb - 1) d.s2[noff] = v;
+                if (w1) {
                     bv.sm[(size_t)k * CB + c] = v;
                     bv.xm[(size_t)k * CB + c] = any ? xmin : DMAX;
                 }
             }
         } else {
-            const bool w1 = bv.w1[k] != 0;
             for (uint32_t base = 0; base < n; base += G) {
                 uint32_t i = base + grp;
                 if (i < n && cv) {
                     uint32_t node = noff + i;
-                    uint8_t f = d.nflag[node];
-                    if (f & kAlive) {
+                    uint32_t p, r;
+                    bool alive, inal;
+                    if (MIR) {
+                        uint16_t wd = d.mir[node];
+                        p = wd & kMirParent; r = (wd >> kMirRankShift) & 31u;
+                        alive = (wd & kMirAlive) != 0; inal = (wd & kMirIn) != 0;
+                    } else {
                         uint32_t t = d.ntopo[node];
-                        uint32_t p = t & kParentMask, r = t >> kRankShift;
+                        uint8_t f = d.nflag[node];
+                        p = t & kParentMask; r = t >> kRankShift;
+                        alive = (f & kAlive) != 0; inal = (f & kInAlive) != 0;
+                    }
+                    if (alive) {
                         double x, y = DMAX;
-                        if (!(f & kInAlive)) x = DMIN;
+                        if (!inal) x = DMIN;
                         else {
-                            double px = prevv(p);
+                            double px = pbuf[p * CB + c];
                             if (r != 0) { x = px + bv.coef[c * us + r]; y = x; }
                             else { x = px; y = px + 0.0; }
                         }
-                        if (cur_g) bv.s2b[(size_t)(node - bv.gbase) * CB + c] = x;
-                        else cbuf[i * CB + c] = x;
-                        if (c == nb - 1) d.s2[node] = x;
+                        cbuf[i * CB + c] = x;
+                        if (wr && c == nb - 1) d.s2[node] = x;
                         if (w1) {
                             bv.sm[(size_t)k * CB + c] = x;
                             bv.xm[(size_t)k * CB + c] = y;
@@ -797,21 +896,131 @@ __device__ void dd_sweep_batch(const NetDev &net, DD &d, BatchView &bv, const Po
                 }
             }
         }
-        if (prev_g || cur_g) wave_mem_sync();
-        else wave_lds_sync();
+        wave_lds_sync();
+    }
+}
+
+// value of node p of layer k for batch cut c (LDS for narrow layers, HBM for the tail)
+template <int CB>
+__device__ inline double batch_value(const DD &d, const BatchView &bv, int k, uint32_t p, int c) {
+    if (k >= d.kg) return bv.s2b[(size_t)(d.noff[k] + p - bv.gbase) * CB + c];
+    return bv.vb[(size_t)(k & 1) * kLdsBatchWidth * CB + p * CB + c];
+}
+
+// One tail layer (k >= kg, exact expansion) into HBM: several independent nodes per
+// lane per step so that the loads overlap.
+template <int CB>
+__device__ void sweep_tail_layer(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int k, int nb, int kS) {
+    constexpr int G = kWave / CB;
+    constexpr int U = 4;
+    batch_coef_direct(net, d, bv, pool, k, nb);
+    const int c = lane() % CB, grp = lane() / CB;
+    const bool cv = c < nb;
+    const int us = pool.ustride;
+    const uint32_t noff = d.noff[k], n = d.nn[k];
+    const bool w1 = bv.w1[k] != 0, wr = k < kS;
+    for (uint32_t base = 0; base < n; base += G * U) {
+        uint32_t t[U];
+        uint8_t f[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            uint32_t i = base + u * G + grp;
+            bool ok = i < n && cv;
+            t[u] = ok ? d.ntopo[noff + i] : 0u;
+            f[u] = ok ? d.nflag[noff + i] : (uint8_t)0;
+        }
+        double px[U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            px[u] = (f[u] & kAlive) ? batch_value<CB>(d, bv, k - 1, t[u] & kParentMask, c) : 0.0;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (!(f[u] & kAlive)) continue;
+            uint32_t i = base + u * G + grp;
+            uint32_t node = noff + i, r = t[u] >> kRankShift;
+            double x, y = DMAX;
+            if (!(f[u] & kInAlive)) x = DMIN;
+            else if (r != 0) { x = px[u] + bv.coef[c * us + r]; y = x; }
+            else { x = px[u]; y = px[u] + 0.0; }
+            bv.s2b[(size_t)(node - bv.gbase) * CB + c] = x;
+            if (wr && c == nb - 1) d.s2[node] = x;
+            if (w1) {
+                bv.sm[(size_t)k * CB + c] = x;
+                bv.xm[(size_t)k * CB + c] = y;
+            }
+        }
     }
     wave_mem_sync();
 }
 
-// Pruning test of one cut from the batch summaries over layers [first, end):
-// true = redo this cut exactly (some arc is pruned, or a width-1 layer has no summary
-// because deletions made it width-1 inside the batch).
+// Pruning test of one cut from the batch summaries over layers [first, end): true =
+// redo this cut exactly (some arc is pruned, or a width-1 layer has no summary because
+// deletions made it width-1 inside the batch).
 template <int CB>
 __device__ bool dd_prune_check(const DD &d, const BatchView &bv, int c, int first, int end, double thresh,
                                double maxState) {
     for (int base = first; base < end; base += kWave)
         if (prune_fire(d, base, end, maxState, thresh, bv.sm + c, bv.xm + c, CB, bv.w1)) return true;
     return false;
+}
+
+// Fused last layer of an optimality batch.  Pass A: per cut the terminal state after
+// the running-min update and maxState, without storing anything; pass B: commit the
+// terminal weights of cuts 0 .. capply.  Leaf value = parent value + coefficient.
+template <int CB>
+__device__ void fused_leaf_pass(const DD &d, BatchView &bv, const Pool &pool, int nb, int capply, VP *term, VP *mxs) {
+    const int last = d.T - 1;
+    const uint32_t lo = d.noff[last], ln = d.nn[last];
+    const int us = pool.ustride;
+    const bool commit = capply >= 0;
+#pragma unroll
+    for (int c = 0; c < CB; c++) { term[c] = VP{0.0, INT_MIN}; mxs[c] = VP{0.0, INT_MIN}; }
+    constexpr int U = 2;
+    for (uint32_t base = 0; base < ln; base += U * kWave) {
+        uint32_t t[U];
+        uint8_t f[U];
+        double w[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            uint32_t i = base + u * kWave + lane();
+            bool ok = i < ln;
+            t[u] = ok ? d.ntopo[lo + i] : 0u;
+            f[u] = ok ? d.nflag[lo + i] : (uint8_t)0;
+            w[u] = ok ? d.tw[lo + i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (!(f[u] & kAlive)) continue;
+            const uint32_t i = base + u * kWave + lane();
+            const uint32_t p = t[u] & kParentMask, r = t[u] >> kRankShift;
+            const bool inal = (f[u] & kInAlive) != 0;
+            double ww = w[u];
+#pragma unroll
+            for (int c = 0; c < CB; c++) {
+                if (c >= nb || (commit && c > capply)) break;
+                double v;
+                if (!inal) v = DMIN;
+                else {
+                    double px = batch_value<CB>(d, bv, last - 1, p, c);
+                    v = (r != 0) ? px + bv.coef[c * us + r] : px;
+                }
+                ww = smin(ww, v);
+                if (!commit) {
+                    term[c] = vp_pick(term[c], VP{ww, prio_old((int)i)});
+                    mxs[c] = vp_pick(mxs[c], VP{v, prio_old((int)i)});
+                }
+            }
+            if (commit) d.tw[lo + i] = ww;
+        }
+    }
+    if (!commit) {
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            term[c] = wave_vp(term[c]);
+            mxs[c] = wave_vp(mxs[c]);
+        }
+    }
+    wave_mem_sync();
 }
 
 // getPathForNode (DD.cpp:3796-3820): walk up, first in-arc whose parent.state2 + weight
@@ -821,8 +1030,8 @@ __device__ int dd_walk(const NetDev &net, DD &d, uint32_t node, int k, const dou
     int cnt = 0;
     while (k > 0) {
         const uint32_t pnoff = d.noff[k - 1];
-        const double cur = d.s2[node];
         const uint32_t acnt = d.acnt[k];
+        const double cur = acnt ? d.s2[node] : 0.0;
         uint32_t parent;
         int found = 0;
         int16_t dec = 0;
@@ -851,10 +1060,13 @@ __device__ int dd_walk(const NetDev &net, DD &d, uint32_t node, int k, const dou
                 dec = rank_value(net, d.g + k - 1, (int)(t >> kRankShift));
             }
         } else {
+            // A single incoming arc: its parent.state2 + weight is exactly how this node's
+            // state2 was computed in the same sweep, so the reference's equality test
+            // (DD.cpp:3808) always holds for it; no state2 is read here.
             uint32_t t = d.ntopo[node];
             uint32_t p = t & kParentMask, r = t >> kRankShift;
             parent = pnoff + p;
-            if ((d.s2[parent] + arc_weight(net, d, k, (int)r, row)) == cur) {
+            if (d.nflag[node] & kInAlive) {
                 found = 1;
                 dec = rank_value(net, d.g + k - 1, (int)r);
             }
@@ -972,62 +1184,92 @@ __device__ void cut_loop_single(const NetDev &net, DD &d, const Pool &pool, doub
     }
 }
 
-// CB cuts per sweep, replayed in pool order (see dd_sweep_batch)
+// CB cuts of one type per sweep, replayed in pool order (see "Multi-cut sweeps")
 template <int CB>
 __device__ void cut_loop_batched(const NetDev &net, DD &d, const Scratch &sc, BatchView &bv, const Pool &pool,
                                  double incumbent, LoopState &st) {
     const int total = pool.nf + pool.no;
+    const int last = d.T - 1;
+    bv.gbase = d.noff[d.kg];
+    if (d.T < 2 || d.noff[last] + d.nn[last] - bv.gbase > (uint32_t)sc.tail_cap) {
+        cut_loop_single(net, d, pool, incumbent, 0, st);
+        return;
+    }
     int s = 0;
     while (s < total) {
-        const int nb = min(CB, total - s);
+        const bool feas = s < pool.nf;
+        const int nb = min(CB, (feas ? pool.nf : total) - s);
         if (lane() < nb) bv.ids[lane()] = seq_id(pool, s + lane());
         for (int k = lane(); k < d.T; k += kWave) bv.w1[k] = (d.nalive[k] == 1) ? 1 : 0;
-        // first layer held in HBM: the first one wider than the LDS buffers, else the last
-        int kg = d.T - 1;
-        for (int base = 0; base < d.T - 1; base += kWave) {
+        int kS = d.T;
+        for (int base = 3; base < d.T; base += kWave) {
             int k = base + lane();
-            uint64_t b = __ballot(k < d.T - 1 && d.nn[k] > (uint32_t)kLdsBatchWidth);
-            if (b) { kg = base + (int)(__ffsll((unsigned long long)b) - 1); break; }
+            uint64_t b = __ballot(k < d.T && d.nalive[k] == 1);
+            if (b) { kS = base + (int)(__ffsll((unsigned long long)b) - 1) + 1; break; }
         }
-        bv.kg = kg;
-        bv.gbase = d.noff[kg];
-        if (d.noff[d.T - 1] + d.nn[d.T - 1] - bv.gbase > (uint32_t)sc.tail_cap) {
-            cut_loop_single(net, d, pool, incumbent, s, st);   // tail too large for the buffers
-            return;
-        }
-        double rv = root_fold_seq(pool, d, s, total);
+        const double rv = root_fold_seq(pool, d, s, total);
         wave_lds_sync();
-        dd_sweep_batch<CB>(net, d, bv, pool, nb, rv);
-        const int last = d.T - 1;
-        const double *lbase = bv.s2b + (size_t)(d.noff[last] - bv.gbase) * CB;
+        if (d.mirror) sweep_narrow<CB, true>(net, d, bv, pool, nb, rv, kS);
+        else sweep_narrow<CB, false>(net, d, bv, pool, nb, rv, kS);
+        if (d.kg == 0 && lane() < nb) bv.s2b[lane()] = rv;
+        for (int k = max(d.kg, 1); k < last; k++) sweep_tail_layer<CB>(net, d, bv, pool, k, nb, kS);
         int next = s + nb;
-        for (int c = 0; c < nb; c++) {
-            const int seq = s + c;
-            const int id = bv.ids[c];
-            const double *row = pool.rows + (size_t)id * pool.stride;
-            const LastVals lv{lbase + c, CB};
-            st.last_cut = id;
-            st.applied++;
-            bool redo = false;
-            double maxState;
-            if (seq < pool.nf) {
-                if (!dd_remove_last(d, lv, maxState)) { st.status = kPrunedFeasibility; return; }
+        if (feas) {
+            // feasibility cuts: last layer materialised, removal + cascade replayed per cut
+            sweep_tail_layer<CB>(net, d, bv, pool, last, nb, kS);
+            const double *lbase = bv.s2b + (size_t)(d.noff[last] - bv.gbase) * CB;
+            for (int c = 0; c < nb; c++) {
+                const int seq = s + c;
+                const double *row = pool.rows + (size_t)bv.ids[c] * pool.stride;
+                st.last_cut = bv.ids[c];
+                st.applied++;
+                double maxState;
+                if (!dd_remove_last(d, LastVals{lbase + c, CB}, maxState)) { st.status = kPrunedFeasibility; return; }
                 if (!d.exact && dd_prune_check<CB>(d, bv, c, 1, last, -0.01, maxState)) {
                     dd_sweep(net, d, row, __shfl(rv, c, kWave));
                     if (!dd_prune(net, d, row, 1, last, -0.01, maxState)) { st.status = kPrunedFeasibility; return; }
-                    redo = true;
+                    next = seq + 1;
+                    st.redo++;
+                    break;
                 }
-            } else {
-                double v = dd_terminal(d, lv, maxState);
-                if (v > incumbent && !d.exact && dd_prune_check<CB>(d, bv, c, 3, last - 1, incumbent - 0.01, maxState)) {
-                    dd_sweep(net, d, row, __shfl(rv, c, kWave));
-                    if (!dd_prune(net, d, row, 3, last - 1, incumbent - 0.01, maxState)) v = DMIN;
-                    redo = true;
+            }
+        } else {
+            // optimality cuts: fused last layer (pass A: terminal states, pass B: commit)
+            batch_coef_direct(net, d, bv, pool, last, nb);
+            VP term[CB], mxs[CB];
+            fused_leaf_pass<CB>(d, bv, pool, nb, -1, term, mxs);
+            int capply = nb - 1, redo = -1;
+            for (int c = 0; c < nb; c++) {
+                double v = (term[c].p == INT_MIN) ? DMIN : smax(DMIN, term[c].v);
+                if (v > incumbent && !d.exact) {
+                    double maxState = (mxs[c].p == INT_MIN) ? DMIN : smax(DMIN, mxs[c].v);
+                    if (dd_prune_check<CB>(d, bv, c, 3, last - 1, incumbent - 0.01, maxState)) {
+                        capply = c;
+                        redo = c;
+                        break;
+                    }
                 }
+                st.applied++;
+                st.last_cut = bv.ids[c];
                 st.ub = d.exact ? v : smin(v, st.ub);
                 if (st.ub <= incumbent) { st.status = kPrunedOptimality; return; }
             }
-            if (redo) { next = seq + 1; st.redo++; break; }
+            VP dummy_t[CB], dummy_m[CB];
+            fused_leaf_pass<CB>(d, bv, pool, nb, capply, dummy_t, dummy_m);
+            if (redo >= 0) {
+                const int c = redo;
+                const double *row = pool.rows + (size_t)bv.ids[c] * pool.stride;
+                double v = (term[c].p == INT_MIN) ? DMIN : smax(DMIN, term[c].v);
+                double maxState = (mxs[c].p == INT_MIN) ? DMIN : smax(DMIN, mxs[c].v);
+                dd_sweep(net, d, row, __shfl(rv, c, kWave));
+                if (!dd_prune(net, d, row, 3, last - 1, incumbent - 0.01, maxState)) v = DMIN;
+                st.applied++;
+                st.last_cut = bv.ids[c];
+                st.ub = d.exact ? v : smin(v, st.ub);
+                if (st.ub <= incumbent) { st.status = kPrunedOptimality; return; }
+                next = s + c + 1;
+                st.redo++;
+            }
         }
         s = next;
     }
@@ -1044,6 +1286,10 @@ __global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn
     const uint64_t t_start = wall_clock64();
     DD d;
     dd_bind(d, smem, sc, slot, CB);
+    d.mirror = 0;
+    d.kg = 0;
+    d.Nn = 0;
+    d.Amir = 0;
     d.g = in.gl[slot];
     d.len = in.sol_len[slot];
     const int16_t *rsol = in.sol + in.sol_off[slot];
@@ -1051,7 +1297,7 @@ __global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn
     int cut_layer = 0;
     LoopState st{kSuccess, in.ub[slot], -1, 0, 0};
     double lb = DMIN;
-    uint32_t nchild = 0, n_nodes = 0, n_arcs = 0;
+    uint32_t nchild = 0, n_nodes = 0, n_arcs = 0, n_merged = 0;
     d.T = 1; d.exact = 1;
 
     if (!in.valid[slot] || d.len > d.g || d.g > net.L || d.len > sc.Lcap) {
@@ -1072,12 +1318,14 @@ __global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn
         }
         d.rslot[t] = s;
     }
-    if (!dd_build(net, d, sc, in.mask[slot], n_nodes, n_arcs)) {
+    if (!dd_build(net, d, sc, in.mask[slot], n_nodes, n_arcs, n_merged)) {
         st.status = kErrCapacity;
         goto done;
     }
     if (CB > 1 && d.aligned) {
-        LdsCarve cv = lds_carve(sc.Tcap, sc.Lcap, CB);
+        LdsCarve cv = lds_carve(sc.Tcap, sc.Lcap, CB, sc.mir_cap);
+        d.mir = (uint16_t *)(smem + cv.o_mir);
+        build_mirror(d, n_merged, sc.mir_cap);
         BatchView bv;
         bv.vb = (double *)(smem + cv.o_buf);
         bv.coef = (double *)(smem + cv.o_bcoef);
@@ -1132,7 +1380,7 @@ done:
         out.dd_arcs[slot] = n_arcs;
         out.dd_layers[slot] = (uint32_t)d.T + 1;
         out.sweeps[slot] = st.applied;
-        out.redo[slot] = st.redo;
+        out.redo[slot] = st.redo | (d.mirror ? 0x80000000u : 0u) | ((d.Nn + d.Amir) << 8);
     }
     store_meta_layers(d, sc, slot, st.last_cut, st.status, cut_layer, st.ub);
     if (lane() == 0) out.ticks[slot] = wall_clock64() - t_start;
@@ -1302,12 +1550,12 @@ __global__ void __launch_bounds__(1024) k_scan2(const uint32_t *a, const uint32_
 
 // ------------------------------------------------------------------------------------
 // host-side launchers (called from capi.cpp)
-size_t relax_lds_bytes(int Tcap, int Lcap, int cb) { return lds_carve(Tcap, Lcap, cb).bytes; }
+size_t relax_lds_bytes(int Tcap, int Lcap, int cb, int mcap) { return lds_carve(Tcap, Lcap, cb, mcap).bytes; }
 
 hipError_t launch_relax(const NetDev &net, const Scratch &sc, const BatchIn &in, const Pool &pool,
                         const BatchOut &out, double incumbent, int cb, hipStream_t st) {
     if (in.n <= 0) return hipSuccess;
-    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, cb);
+    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, cb, sc.mir_cap);
     switch (cb) {
         case 4: hipLaunchKernelGGL(k_relax<4>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent); break;
         case 8: hipLaunchKernelGGL(k_relax<8>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent); break;
@@ -1325,7 +1573,7 @@ hipError_t launch_scan(const uint32_t *a, const uint32_t *b, int n, uint64_t *oa
 hipError_t launch_emit(const NetDev &net, const Scratch &sc, const BatchIn &in, const Pool &pool,
                        const BatchOut &out, const ChildOut &co, hipStream_t st) {
     if (in.n <= 0) return hipSuccess;
-    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, 1);
+    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, 1, 0);
     hipLaunchKernelGGL(k_emit_children, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, co);
     return hipGetLastError();
 }
@@ -1334,7 +1582,7 @@ hipError_t launch_refine(const NetDev &net, const Scratch &sc, const BatchIn &in
                          const BatchOut &out, const int32_t *slots, const int32_t *cut_ids,
                          const uint8_t *cut_is_feas, int n, double incumbent, hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, 1);
+    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, 1, 0);
     hipLaunchKernelGGL(k_refine, dim3(n), dim3(kWave), lds, st, net, sc, in, pool, out, slots, cut_ids,
                        cut_is_feas, n, incumbent);
     return hipGetLastError();
