@@ -124,6 +124,8 @@ int sgufp_batch_refine(sgufp_ctx *ctx, int n, const int32_t *node_idx, const uin
 /* Diagnostics of the last relax: wall_clock64 ticks (100 MHz) of each node's wave and
  * the number of batched-sweep restarts (exact single-cut redo after pruning). */
 int sgufp_batch_debug(sgufp_ctx *ctx, int64_t *ticks, int32_t *redo);
+/* ticks per phase [n * 8]: build, narrow sweep, tail layers, last layer, replay/post, redo, finish, tail */
+int sgufp_batch_phases(sgufp_ctx *ctx, int64_t *phase);
 
 /* -- timing (hipEvents on the ctx stream around each kernel of the last relax) -- */
 int sgufp_set_timing(sgufp_ctx *ctx, int enabled);

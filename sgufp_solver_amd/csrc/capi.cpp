@@ -12,6 +12,7 @@
 #include <unordered_map>
 #include <vector>
 
+#define SGUFP_HOST_ONLY 1  // no device code here: plain pointers in the device pass too
 #include "dd_device.hpp"
 #include "network.hpp"
 
@@ -58,7 +59,7 @@ struct sgufp_ctx {
     int row_cap = 0, n_rows = 0;
     double *d_rows = nullptr, *d_rhs = nullptr, *d_coefT = nullptr;
     int ustride = 1;
-    int cb = 8;                               // cuts per batched sweep
+    int cb = 4;                               // cuts per batched sweep
     std::vector<int32_t> f_rows, o_rows;      // insertion order, row ids
     int32_t *d_forder = nullptr, *d_oorder = nullptr;
     int order_cap = 0;
@@ -254,17 +255,19 @@ bool sgufp_ctx::init() {
     int64_t ncap = node_bound(net, &tail);
     ustride = std::max(1, net.max_states);
     if (const char *e = getenv("SGUFP_CUT_BATCH")) cb = atoi(e);
-    if (cb != 1 && cb != 4 && cb != 8 && cb != 16) cb = 8;
+    if (cb != 1 && cb != 4 && cb != 8 && cb != 16) cb = 4;
     int64_t acap = std::max<int64_t>(1, (int64_t)std::max(0, L - 4) * (kRelaxedMaxWidth - 1) * maxU);
     if (ncap > (int64_t)kParentMask || acap > (int64_t)0x7FFFFFFF) { err = "DD capacity beyond 22-bit indices"; return false; }
     sc.Ncap = (int)ncap;
     sc.Acap = (int)acap;
-    // LDS per relax workgroup: SGUFP_LDS_KB (default 64); what the fixed carve leaves is
-    // the narrow-layer topology mirror
-    size_t lds_budget = 64 * 1024;
+    // LDS per relax workgroup: SGUFP_LDS_KB (default 40: four single-wave workgroups per
+    // CU, one per SIMD); what the fixed carve leaves is the narrow-layer topology mirror.
+    // A budget below the fixed carve only turns the mirror off.
+    size_t lds_budget = 40 * 1024;
     if (const char *e = getenv("SGUFP_LDS_KB")) lds_budget = (size_t)atoi(e) * 1024;
     size_t base_lds = relax_lds_bytes(sc.Tcap, sc.Lcap, cb, 0);
-    if (base_lds > lds_budget || base_lds > 160 * 1024) { err = "too many layers for the LDS layer table"; return false; }
+    if (base_lds > 160 * 1024) { err = "too many layers for the LDS layer table"; return false; }
+    lds_budget = std::max(lds_budget, base_lds);
     sc.mir_cap = cb > 1 ? (int)((lds_budget - base_lds) / 2) : 0;
     sc.tail_cap = (int)tail;
     sc.cb_max = cb;
@@ -284,7 +287,7 @@ bool sgufp_ctx::init() {
         !alloc(out.ub, B, "out") || !alloc(out.nchild, B, "out") || !alloc(out.sol_need, B, "out") ||
         !alloc(out.dd_nodes, B, "out") || !alloc(out.dd_arcs, B, "out") || !alloc(out.dd_layers, B, "out") ||
         !alloc(out.sweeps, B, "out") || !alloc(out.path, B * sc.Lcap, "out") || !alloc(out.path_len, B, "out") ||
-        !alloc(out.ticks, B, "out") || !alloc(out.redo, B, "out"))
+        !alloc(out.ticks, B, "out") || !alloc(out.redo, B, "out") || !alloc(out.phase, B * 8, "out"))
         return false;
     // batch input
     if (!alloc(d_gl, B, "batch") || !alloc(d_sollen, B, "batch") || !alloc(d_lb, B, "batch") ||
@@ -736,6 +739,14 @@ int sgufp_batch_refine(sgufp_ctx *ctx, int n, const int32_t *node_idx, const uin
                      "k_refine"))
         return SGUFP_ERR_HIP;
     return ctx->sync() ? SGUFP_OK : SGUFP_ERR_HIP;
+}
+
+int sgufp_batch_phases(sgufp_ctx *ctx, int64_t *phase) {
+    if (!ctx || !ctx->relaxed || !phase) return ctx ? SGUFP_ERR_STATE : SGUFP_ERR_ARG;
+    std::vector<uint64_t> t((size_t)ctx->n * 8);
+    if (!ctx->download(t.data(), ctx->out.phase, t.size()) || !ctx->sync()) return SGUFP_ERR_HIP;
+    for (size_t k = 0; k < t.size(); k++) phase[k] = (int64_t)t[k];
+    return SGUFP_OK;
 }
 
 int sgufp_batch_debug(sgufp_ctx *ctx, int64_t *ticks, int32_t *redo) {

@@ -4,6 +4,17 @@
 
 #include <cstdint>
 
+// Device code sees every HBM pointer of the structs below in the global address space, so
+// the compiler emits global_load/global_store (vmcnt only) instead of flat_* accesses, which
+// would make every LDS access wait for all outstanding HBM loads.  The host sees plain
+// pointers; both are 64-bit with the same value, so the kernel-argument layout is identical.
+// Host-only translation units (capi.cpp) define SGUFP_HOST_ONLY for their device pass.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(SGUFP_HOST_ONLY)
+#define SGUFP_GBL __attribute__((address_space(1)))
+#else
+#define SGUFP_GBL
+#endif
+
 namespace sgufp {
 
 constexpr int kWave = 64;          // one DD per 64-lane wavefront (one single-wave workgroup)
@@ -36,95 +47,96 @@ struct NetDev {
     unsigned L5;           // (unsigned)(totalLayers - 5), the reference's unsigned arithmetic
     int m;
     int n_slots;           // cut row = n_slots coefficients + 1 zero slot
-    const int32_t *layer_update;    // [L+1]
-    const int32_t *layer_universe;  // [L+1]
-    const uint8_t *changed;         // [L+1]
-    const int32_t *set_off;         // [n_sets]
-    const int32_t *set_len;         // [n_sets]
-    const int16_t *set_val;         // concatenated sorted sets
-    const int32_t *slot_tab;        // [L * kMaxU]
-    const int32_t *slot_off;        // [L+1]
-    const int32_t *slot_head;       // [n_slots]
-    const int32_t *arc_head;        // [m]
+    const int32_t SGUFP_GBL *layer_update;    // [L+1]
+    const int32_t SGUFP_GBL *layer_universe;  // [L+1]
+    const uint8_t SGUFP_GBL *changed;         // [L+1]
+    const int32_t SGUFP_GBL *set_off;         // [n_sets]
+    const int32_t SGUFP_GBL *set_len;         // [n_sets]
+    const int16_t SGUFP_GBL *set_val;         // concatenated sorted sets
+    const int32_t SGUFP_GBL *slot_tab;        // [L * kMaxU]
+    const int32_t SGUFP_GBL *slot_off;        // [L+1]
+    const int32_t SGUFP_GBL *slot_head;       // [n_slots]
+    const int32_t SGUFP_GBL *arc_head;        // [m]
 };
 
 // Per-slot DD scratch.  Every array is [max_batch * cap], slot-major.
 struct Scratch {
     int Ncap, Acap, Tcap, Lcap;
-    uint32_t *ntopo;   // [Ncap]
-    uint8_t *nflag;    // [Ncap]
-    uint32_t *nmask;   // [Ncap]
-    uint32_t *outcnt;  // [Ncap]
-    double *s2;        // [Ncap]  state2 of the last sweep
-    double *tw;        // [Ncap]  terminal-arc weight (running min over optimality cuts), last layer only
-    uint32_t *atopo;   // [Acap]  merged-layer incoming arcs
-    uint8_t *aflag;    // [Acap]
-    uint32_t *lay;     // [Tcap * 5] noff, n, alive, aoff, acnt
-    int32_t *rslot;    // [Lcap] coefficient slot of each root-solution decision (-1: decision -1)
-    int32_t *meta;     // [8] g, sol_len, T, exact, aligned, last_cut, status, cut_layer
-    double *ubv;       // [1] running upper bound
+    uint32_t SGUFP_GBL *ntopo;   // [Ncap]
+    uint8_t SGUFP_GBL *nflag;    // [Ncap]
+    uint32_t SGUFP_GBL *nmask;   // [Ncap]
+    uint32_t SGUFP_GBL *outcnt;  // [Ncap]
+    double SGUFP_GBL *s2;        // [Ncap]  state2 of the last sweep
+    double SGUFP_GBL *tw;        // [Ncap]  terminal-arc weight (running min over optimality cuts), last layer only
+    uint32_t SGUFP_GBL *atopo;   // [Acap]  merged-layer incoming arcs
+    uint8_t SGUFP_GBL *aflag;    // [Acap]
+    uint32_t SGUFP_GBL *lay;     // [Tcap * 5] noff, n, alive, aoff, acnt
+    int32_t SGUFP_GBL *rslot;    // [Lcap] coefficient slot of each root-solution decision (-1: decision -1)
+    int32_t SGUFP_GBL *meta;     // [8] g, sol_len, T, exact, aligned, last_cut, status, cut_layer
+    double SGUFP_GBL *ubv;       // [1] running upper bound
     // multi-cut sweeps (k_relax with CB > 1)
     int tail_cap;      // nodes of the HBM-resident tail layers (wide layers + last layer)
     int cb_max;        // cuts per batched sweep the buffers are sized for
     int mir_cap;       // LDS mirror entries (16-bit) of the narrow-layer topology
-    double *s2b;       // [tail_cap * cb_max]
-    double *sm;        // [Tcap * cb_max]
-    double *xm;        // [Tcap * cb_max]
+    double SGUFP_GBL *s2b;       // [tail_cap * cb_max]
+    double SGUFP_GBL *sm;        // [Tcap * cb_max]
+    double SGUFP_GBL *xm;        // [Tcap * cb_max]
 };
 
 // Staged batch of open nodes (Inavap::Node records, DD.h:456-478), SoA.
 struct BatchIn {
     int n;
-    const uint16_t *gl;
-    const double *lb;
-    const double *ub;
-    const uint32_t *mask;      // states as a mask over the universe in force at gl
-    const uint8_t *valid;      // host-side record validation
-    const int64_t *sol_off;
-    const uint16_t *sol_len;
-    const int16_t *sol;
+    const uint16_t SGUFP_GBL *gl;
+    const double SGUFP_GBL *lb;
+    const double SGUFP_GBL *ub;
+    const uint32_t SGUFP_GBL *mask;      // states as a mask over the universe in force at gl
+    const uint8_t SGUFP_GBL *valid;      // host-side record validation
+    const int64_t SGUFP_GBL *sol_off;
+    const uint16_t SGUFP_GBL *sol_len;
+    const int16_t SGUFP_GBL *sol;
 };
 
 struct Pool {
-    const double *rows;        // [cap][n_slots + 1]
-    const double *rhs;         // [cap]
+    const double SGUFP_GBL *rows;        // [cap][n_slots + 1]
+    const double SGUFP_GBL *rhs;         // [cap]
     int stride;                // n_slots + 1
-    const int32_t *f_order;    // feasibility cuts, newest first
+    const int32_t SGUFP_GBL *f_order;    // feasibility cuts, newest first
     int nf;
-    const int32_t *o_order;    // optimality cuts, newest first
+    const int32_t SGUFP_GBL *o_order;    // optimality cuts, newest first
     int no;
-    const double *coefT;       // [cap][L][ustride]: coefficient of state rank r at layer l
+    const double SGUFP_GBL *coefT;       // [cap][L][ustride]: coefficient of state rank r at layer l
     int ustride;               // max state-set size of the network
 };
 
 struct BatchOut {
-    int32_t *status;
-    uint8_t *exact;
-    double *lb;
-    double *ub;
-    uint32_t *nchild;
-    uint32_t *sol_need;        // solution entries the children need (upper bound)
-    uint32_t *dd_nodes;
-    uint32_t *dd_arcs;
-    uint32_t *dd_layers;
-    uint32_t *sweeps;          // cuts swept over this node's DD
-    int16_t *path;             // [max_batch * Lcap] argmax path of exact DDs
-    uint16_t *path_len;
-    uint64_t *ticks;           // wall_clock64 ticks (100 MHz) spent by each node's wave
-    uint32_t *redo;            // batched sweeps restarted after an exact single-cut redo
+    int32_t SGUFP_GBL *status;
+    uint8_t SGUFP_GBL *exact;
+    double SGUFP_GBL *lb;
+    double SGUFP_GBL *ub;
+    uint32_t SGUFP_GBL *nchild;
+    uint32_t SGUFP_GBL *sol_need;        // solution entries the children need (upper bound)
+    uint32_t SGUFP_GBL *dd_nodes;
+    uint32_t SGUFP_GBL *dd_arcs;
+    uint32_t SGUFP_GBL *dd_layers;
+    uint32_t SGUFP_GBL *sweeps;          // cuts swept over this node's DD
+    int16_t SGUFP_GBL *path;             // [max_batch * Lcap] argmax path of exact DDs
+    uint16_t SGUFP_GBL *path_len;
+    uint64_t SGUFP_GBL *ticks;           // wall_clock64 ticks (100 MHz) spent by each node's wave
+    uint64_t SGUFP_GBL *phase;           // [max_batch * 8] ticks per phase: build, narrow, tail, last, post, redo, finish
+    uint32_t SGUFP_GBL *redo;            // batched sweeps restarted after an exact single-cut redo
 };
 
 // Children written by the emit kernel (device-resident frontier format).
 struct ChildOut {
-    const uint64_t *child_off;  // [n+1] exclusive scan of nchild
-    const uint64_t *sol_base;   // [n+1] exclusive scan of sol_need
-    uint16_t *gl;
-    double *lb;
-    double *ub;
-    uint32_t *mask;
-    int64_t *sol_off;
-    uint16_t *sol_len;
-    int16_t *sol;
+    const uint64_t SGUFP_GBL *child_off;  // [n+1] exclusive scan of nchild
+    const uint64_t SGUFP_GBL *sol_base;   // [n+1] exclusive scan of sol_need
+    uint16_t SGUFP_GBL *gl;
+    double SGUFP_GBL *lb;
+    double SGUFP_GBL *ub;
+    uint32_t SGUFP_GBL *mask;
+    int64_t SGUFP_GBL *sol_off;
+    uint16_t SGUFP_GBL *sol_len;
+    int16_t SGUFP_GBL *sol;
 };
 
 }  // namespace sgufp

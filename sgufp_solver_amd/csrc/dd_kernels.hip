@@ -30,6 +30,11 @@
 
 namespace sgufp {
 
+// Address spaces spelled out so that the compiler emits ds_* for LDS and global_* for
+// HBM: a generic (flat) access waits on both counters and serialises LDS behind HBM.
+#define LDS __attribute__((address_space(3)))
+#define GBL SGUFP_GBL
+
 #define DMIN (-__DBL_MAX__)
 #define DMAX (__DBL_MAX__)
 
@@ -38,6 +43,9 @@ constexpr uint32_t kCollapseWidth = 120;  // RELAXED_MAX_WIDTH (DD.h:732)
 __device__ __forceinline__ int lane() { return (int)threadIdx.x; }
 __device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }  // std::max
 __device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b : a; }  // std::min
+__device__ __forceinline__ uint32_t gsub(GBL uint32_t *p, uint32_t v) {
+    return __hip_atomic_fetch_sub(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // LDS is in order within a wavefront; this only stops the compiler from moving
 // LDS accesses across the point (the workgroup is a single wave).
@@ -102,24 +110,24 @@ __device__ __forceinline__ int prio_old(int k) { return -k - 2; }
 // node/arc arrays in this slot's HBM scratch.
 struct DD {
     // LDS
-    uint32_t *noff, *nn, *nalive, *aoff, *acnt;
-    int32_t *rslot;
-    double *buf0, *buf1;
-    double *coef;     // [kMaxU] per-rank coefficients of the layer being swept
-    int16_t *walk;    // [Tcap] decisions collected by a path walk
-    double *sm1;      // [Tcap] width-1 layers: state2 of the single node (last single sweep)
-    double *xm1;      // [Tcap] width-1 layers: min over its in-arcs of parent.state2 + weight
-    uint8_t *v1;      // [Tcap] summary valid (layer had one alive node during that sweep)
+    LDS uint32_t *noff, *nn, *nalive, *aoff, *acnt;
+    LDS int32_t *rslot;
+    LDS double *buf0, *buf1;
+    LDS double *coef;     // [kMaxU] per-rank coefficients of the layer being swept
+    LDS int16_t *walk;    // [Tcap] decisions collected by a path walk
+    LDS double *sm1;      // [Tcap] width-1 layers: state2 of the single node (last single sweep)
+    LDS double *xm1;      // [Tcap] width-1 layers: min over its in-arcs of parent.state2 + weight
+    LDS uint8_t *v1;      // [Tcap] summary valid (layer had one alive node during that sweep)
     // HBM (slot base applied)
-    uint32_t *ntopo;
-    uint8_t *nflag;
-    uint32_t *nmask;
-    uint32_t *outcnt;
-    double *s2;
-    double *tw;
-    uint32_t *atopo;
-    uint8_t *aflag;
-    uint16_t *mir;    // LDS mirror of the narrow layers' topology (see build_mirror)
+    GBL uint32_t *ntopo;
+    GBL uint8_t *nflag;
+    GBL uint32_t *nmask;
+    GBL uint32_t *outcnt;
+    GBL double *s2;
+    GBL double *tw;
+    GBL uint32_t *atopo;
+    GBL uint8_t *aflag;
+    LDS uint16_t *mir;    // LDS mirror of the narrow layers' topology (see build_mirror)
     // scalars
     int g, len, T, exact, aligned;
     int kg;           // first layer wider than kLdsBatchWidth (or the last layer)
@@ -129,21 +137,23 @@ struct DD {
 };
 
 constexpr int kLdsBatchWidth = 128;
+constexpr int kStageEntries = 512;   // coefficient staging ring: entries per slot (8 per lane)
+constexpr int kStageLayers = 16;     // at most this many layers per staging group
 constexpr uint16_t kMirParent = 127, kMirRankShift = 7, kMirAlive = 1u << 12, kMirIn = 1u << 13;
 
 // LDS mirror of the narrow layers: node word = parent:7 | rank:5 | alive | in-arc alive,
 // merged-arc word = parent:7 | rank:5 | alive.  HBM stays the master copy; every edit of
 // a narrow node / arc flag is applied to both.
-__device__ inline void mir_node_clear(DD &d, uint32_t node, uint16_t bits) {
+__device__ __forceinline__ void mir_node_clear(DD &d, uint32_t node, uint16_t bits) {
     if (d.mirror && node < d.Nn) d.mir[node] &= (uint16_t)~bits;
 }
-__device__ inline void mir_arc_clear(DD &d, uint32_t a) {
+__device__ __forceinline__ void mir_arc_clear(DD &d, uint32_t a) {
     if (d.mirror) d.mir[d.Nn + a] &= (uint16_t)~kMirAlive;
 }
 
 struct LdsCarve {
     size_t bytes;
-    size_t o_lay, o_rslot, o_buf, o_coef, o_walk, o_bcoef, o_w1, o_ids, o_sm1, o_xm1, o_v1, o_mir;
+    size_t o_lay, o_rslot, o_buf, o_coef, o_walk, o_bcoef, o_w1, o_ids, o_sm1, o_xm1, o_v1, o_mir, o_ring;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -164,26 +174,27 @@ __host__ __device__ inline LdsCarve lds_carve(int Tcap, int Lcap, int cb, int mc
     c.o_sm1 = o; o = align16(o + (size_t)Tcap * 8);
     c.o_xm1 = o; o = align16(o + (size_t)Tcap * 8);
     c.o_v1 = o; o = align16(o + (size_t)Tcap);
+    c.o_ring = o; o = align16(o + (cb > 1 ? (size_t)2 * 512 * 8 : 0));
     c.o_mir = o; o = align16(o + (cb > 1 ? (size_t)mcap * 2 : 0));
     c.bytes = o;
     return c;
 }
 
-__device__ inline void dd_bind(DD &d, uint8_t *smem, const Scratch &sc, int slot, int cb = 1) {
+__device__ __forceinline__ void dd_bind(DD &d, LDS uint8_t *smem, const Scratch &sc, int slot, int cb = 1) {
     LdsCarve c = lds_carve(sc.Tcap, sc.Lcap, cb);
-    uint32_t *lay = (uint32_t *)(smem + c.o_lay);
+    LDS uint32_t *lay = (LDS uint32_t *)(smem + c.o_lay);
     d.noff = lay;
     d.nn = lay + sc.Tcap;
     d.nalive = lay + 2 * sc.Tcap;
     d.aoff = lay + 3 * sc.Tcap;
     d.acnt = lay + 4 * sc.Tcap;
-    d.rslot = (int32_t *)(smem + c.o_rslot);
-    d.buf0 = (double *)(smem + c.o_buf);
+    d.rslot = (LDS int32_t *)(smem + c.o_rslot);
+    d.buf0 = (LDS double *)(smem + c.o_buf);
     d.buf1 = d.buf0 + kLdsWidth;
-    d.coef = (double *)(smem + c.o_coef);
-    d.walk = (int16_t *)(smem + c.o_walk);
-    d.sm1 = (double *)(smem + c.o_sm1);
-    d.xm1 = (double *)(smem + c.o_xm1);
+    d.coef = (LDS double *)(smem + c.o_coef);
+    d.walk = (LDS int16_t *)(smem + c.o_walk);
+    d.sm1 = (LDS double *)(smem + c.o_sm1);
+    d.xm1 = (LDS double *)(smem + c.o_xm1);
     d.v1 = smem + c.o_v1;
     size_t N = (size_t)slot * sc.Ncap, A = (size_t)slot * sc.Acap;
     d.ntopo = sc.ntopo + N;
@@ -201,7 +212,7 @@ __device__ inline void dd_bind(DD &d, uint8_t *smem, const Scratch &sc, int slot
 // (decides the key's (q, i)) = sol_len+k-1, exactly the reference's running index
 // `i` (DD.cpp:3940,3952) -- the two differ only for records whose solution vector
 // is shorter than their global layer.
-__device__ inline int rank_slot(const NetDev &net, const DD &d, int k, int r) {
+__device__ __forceinline__ int rank_slot(const NetDev &net, const DD &d, int k, int r) {
     int ls = d.g + k - 1;
     if (d.aligned) return net.slot_tab[ls * kMaxU + r];
     int u = net.layer_universe[ls];
@@ -215,21 +226,21 @@ __device__ inline int rank_slot(const NetDev &net, const DD &d, int k, int r) {
     return net.n_slots;
 }
 
-__device__ inline int16_t rank_value(const NetDev &net, int layer, int r) {
+__device__ __forceinline__ int16_t rank_value(const NetDev &net, int layer, int r) {
     int u = net.layer_universe[layer];
     return net.set_val[net.set_off[u] + r];
 }
 
 // Arc weight as the reference stores it: the coefficient of the last swept cut,
 // 0 before any cut and always 0 for a -1 decision (DD.cpp:3559-3560, 3866-3868).
-__device__ inline double arc_weight(const NetDev &net, const DD &d, int k, int r, const double *row) {
+__device__ __forceinline__ double arc_weight(const NetDev &net, const DD &d, int k, int r, const GBL double *row) {
     if (!row || r == 0) return 0.0;
     int s = rank_slot(net, d, k, r);
     return s >= 0 ? row[s] : 0.0;
 }
 
 // per-layer coefficient table in LDS: coef[r] for every rank
-__device__ inline void load_layer_coef(const NetDev &net, const DD &d, int k, const double *row) {
+__device__ __forceinline__ void load_layer_coef(const NetDev &net, const DD &d, int k, const GBL double *row) {
     if (lane() < kMaxU) {
         int s = (lane() == 0) ? -1 : rank_slot(net, d, k, lane());
         d.coef[lane()] = s >= 0 ? row[s] : 0.0;
@@ -238,7 +249,7 @@ __device__ inline void load_layer_coef(const NetDev &net, const DD &d, int k, co
 
 // ------------------------------------------------------------------------------------
 // Build (buildTree + buildNextLayer).  Returns false on capacity overflow.
-__device__ bool dd_build(const NetDev &net, DD &d, const Scratch &sc, uint32_t root_mask, uint32_t &n_nodes,
+__device__ __forceinline__ bool dd_build(const NetDev &net, DD &d, const Scratch &sc, uint32_t root_mask, uint32_t &n_nodes,
                          uint32_t &n_arcs, uint32_t &n_merged) {
     const int L = net.L;
     if (lane() == 0) {
@@ -363,7 +374,7 @@ __device__ bool dd_build(const NetDev &net, DD &d, const Scratch &sc, uint32_t r
 
 // ------------------------------------------------------------------------------------
 // One cut sweep over layers 1..T-1 (the shared body of both apply functions).
-__device__ void dd_sweep(const NetDev &net, DD &d, const double *row, double root_value) {
+__device__ __forceinline__ void dd_sweep(const NetDev &net, DD &d, const GBL double *row, double root_value) {
     if (lane() == 0) {
         d.s2[0] = root_value;
         d.buf0[0] = root_value;
@@ -376,8 +387,8 @@ __device__ void dd_sweep(const NetDev &net, DD &d, const double *row, double roo
         const bool prev_lds = pn <= (uint32_t)kLdsWidth;
         const bool cur_lds = n <= (uint32_t)kLdsWidth;
         const bool w1 = d.nalive[k] == 1;
-        double *pbuf = (k & 1) ? d.buf0 : d.buf1;
-        double *cbuf = (k & 1) ? d.buf1 : d.buf0;
+        LDS double *pbuf = (k & 1) ? d.buf0 : d.buf1;
+        LDS double *cbuf = (k & 1) ? d.buf1 : d.buf0;
         load_layer_coef(net, d, k, row);
         wave_lds_sync();
         const uint32_t acnt = d.acnt[k];
@@ -438,7 +449,7 @@ __device__ void dd_sweep(const NetDev &net, DD &d, const double *row, double roo
 
 // arg-max with first-wins ties over alive nodes of layer k; value getter by functor
 template <typename F>
-__device__ inline VP layer_max_first(const DD &d, int k, F val) {
+__device__ __forceinline__ VP layer_max_first(const DD &d, int k, F val) {
     const uint32_t noff = d.noff[k], n = d.nn[k];
     VP best{0.0, INT_MIN};
     for (uint32_t base = 0; base < n; base += kWave) {
@@ -449,7 +460,7 @@ __device__ inline VP layer_max_first(const DD &d, int k, F val) {
 }
 
 // the single alive node of a width-1 layer
-__device__ inline uint32_t layer_single(const DD &d, int k) {
+__device__ __forceinline__ uint32_t layer_single(const DD &d, int k) {
     const uint32_t noff = d.noff[k], n = d.nn[k];
     uint32_t found = 0xFFFFFFFFu;
     for (uint32_t base = 0; base < n; base += kWave) {
@@ -463,7 +474,7 @@ __device__ inline uint32_t layer_single(const DD &d, int k) {
 // Exact pruning of one width-1 layer (the body of the loops at DD.cpp:3899-3924 /
 // 3991-4016): every alive in-arc with parent.state2 + weight + gain <= thresh goes.
 // Returns false when all of them would go (the caller returns false / DOUBLE_MIN).
-__device__ bool dd_prune_layer(const NetDev &net, DD &d, const double *row, int k, double maxState, double thresh) {
+__device__ __forceinline__ bool dd_prune_layer(const NetDev &net, DD &d, const GBL double *row, int k, double maxState, double thresh) {
     const uint32_t M = layer_single(d, k);
     const double gain = maxState - d.s2[M];
     const uint32_t pnoff = d.noff[k - 1];
@@ -485,7 +496,7 @@ __device__ bool dd_prune_layer(const NetDev &net, DD &d, const double *row, int 
                 if (pr) {
                     d.aflag[aoff + a] = 0;
                     mir_arc_clear(d, aoff + a);
-                    atomicSub(&d.outcnt[pnoff + p], 1u);
+                    gsub(&d.outcnt[pnoff + p], 1u);
                 }
             }
             total += wave_sum(alive ? 1u : 0u);
@@ -516,8 +527,9 @@ __device__ bool dd_prune_layer(const NetDev &net, DD &d, const double *row, int 
 // rounding is monotone, so some arc satisfies fl(fl(s + w) + gain) <= thresh exactly
 // when fl(xmin + gain) <= thresh.  Layers without a summary count as firing.
 // Returns a 64-bit mask of firing layers for the 64-layer window starting at `base`.
-__device__ inline uint64_t prune_fire(const DD &d, int base, int end, double maxState, double thresh,
-                                      const double *sm, const double *xm, int stride, const uint8_t *valid) {
+template <typename PV, typename PF>
+__device__ __forceinline__ uint64_t prune_fire(const DD &d, int base, int end, double maxState, double thresh,
+                                      PV sm, PV xm, int stride, PF valid) {
     int k = base + lane();
     bool fire = false;
     if (k < end && d.nalive[k] == 1) {
@@ -530,7 +542,7 @@ __device__ inline uint64_t prune_fire(const DD &d, int base, int end, double max
 // Width-1 arc pruning over layers [first, end) (DD.cpp:3895-3928, 3987-4021), after a
 // single-cut sweep (s2 and the sm1/xm1 summaries hold this cut).  Returns false when a
 // width-1 layer would lose all of its incoming arcs.
-__device__ bool dd_prune(const NetDev &net, DD &d, const double *row, int first, int end, double thresh,
+__device__ __forceinline__ bool dd_prune(const NetDev &net, DD &d, const GBL double *row, int first, int end, double thresh,
                          double maxState) {
     for (int base = first; base < end; base += kWave) {
         uint64_t b = prune_fire(d, base, end, maxState, thresh, d.sm1, d.xm1, 1, d.v1);
@@ -545,9 +557,9 @@ __device__ bool dd_prune(const NetDev &net, DD &d, const double *row, int first,
 
 // Values of the last layer for the cut being post-processed: v(i) = p[i * stride].
 struct LastVals {
-    const double *p;
+    const GBL double *p;
     int stride;
-    __device__ double operator()(uint32_t i) const { return p[(size_t)i * stride]; }
+    __device__ __forceinline__ double operator()(uint32_t i) const { return p[(size_t)i * stride]; }
 };
 
 // Last-layer removal (state2 < -0.01, DD.cpp:3880-3893) and the bottom-up deletion
@@ -556,7 +568,7 @@ struct LastVals {
 // maxState = max state2 over the surviving last layer (the value the pruning uses).
 constexpr int kUnroll = 4;
 
-__device__ bool dd_remove_last(DD &d, const LastVals &lv, double &maxState) {
+__device__ __forceinline__ bool dd_remove_last(DD &d, const LastVals &lv, double &maxState) {
     const int last = d.T - 1;
     const uint32_t lo = d.noff[last], ln = d.nn[last];
     uint32_t rm = 0;
@@ -606,7 +618,7 @@ __device__ bool dd_remove_last(DD &d, const LastVals &lv, double &maxState) {
                             uint32_t p = d.atopo[aoff + a] & kParentMask;
                             d.aflag[aoff + a] = 0;
                             mir_arc_clear(d, aoff + a);
-                            if (atomicSub(&d.outcnt[pnoff + p], 1u) == 1u) {
+                            if (gsub(&d.outcnt[pnoff + p], 1u) == 1u) {
                                 d.nflag[pnoff + p] |= kKill;
                                 pk = true;
                             }
@@ -630,7 +642,7 @@ __device__ bool dd_remove_last(DD &d, const LastVals &lv, double &maxState) {
                             if (f & kInAlive) {
                                 uint32_t p = d.ntopo[noff + i] & kParentMask;
                                 // exactly one decrement sees 1: that lane marks the parent
-                                if (atomicSub(&d.outcnt[pnoff + p], 1u) == 1u) {
+                                if (gsub(&d.outcnt[pnoff + p], 1u) == 1u) {
                                     d.nflag[pnoff + p] |= kKill;
                                     pk = true;
                                 }
@@ -653,7 +665,7 @@ __device__ bool dd_remove_last(DD &d, const LastVals &lv, double &maxState) {
 
 // Terminal arcs of an optimality cut: weight = min(weight, parent.state2), terminal
 // state = max over them (DD.cpp:3975-3984); also maxState over the last layer.
-__device__ double dd_terminal(DD &d, const LastVals &lv, double &maxState) {
+__device__ __forceinline__ double dd_terminal(DD &d, const LastVals &lv, double &maxState) {
     const int last = d.T - 1;
     const uint32_t lo = d.noff[last], ln = d.nn[last];
     VP best{0.0, INT_MIN}, mx{0.0, INT_MIN};
@@ -686,7 +698,7 @@ __device__ double dd_terminal(DD &d, const LastVals &lv, double &maxState) {
 }
 
 // applyFeasibilityCut after a single-cut sweep.
-__device__ bool dd_post_feasibility(const NetDev &net, DD &d, const double *row) {
+__device__ __forceinline__ bool dd_post_feasibility(const NetDev &net, DD &d, const GBL double *row) {
     double maxState;
     if (!dd_remove_last(d, LastVals{d.s2 + d.noff[d.T - 1], 1}, maxState)) return false;
     if (!d.exact) return dd_prune(net, d, row, 1, d.T - 1, -0.01, maxState);
@@ -694,7 +706,7 @@ __device__ bool dd_post_feasibility(const NetDev &net, DD &d, const double *row)
 }
 
 // applyOptimalityCut after a single-cut sweep.  Returns the terminal state (or DOUBLE_MIN).
-__device__ double dd_post_optimality(const NetDev &net, DD &d, const double *row, double optimal) {
+__device__ __forceinline__ double dd_post_optimality(const NetDev &net, DD &d, const GBL double *row, double optimal) {
     const int last = d.T - 1;
     double maxState;
     const double term = dd_terminal(d, LastVals{d.s2 + d.noff[last], 1}, maxState);
@@ -723,17 +735,21 @@ __device__ double dd_post_optimality(const NetDev &net, DD &d, const double *row
 // layer is never materialised: two fused passes compute the leaf values on the fly.
 
 struct BatchView {
-    double *vb;        // LDS [2][kLdsBatchWidth][CB]
-    double *coef;      // LDS [CB][ustride]
-    uint8_t *w1;       // LDS [Tcap]: layer had one alive node when the batch started
-    int32_t *ids;      // LDS [CB]: pool row of each batch cut
-    double *s2b;       // HBM [tail_cap][CB]: layers >= kg
-    double *sm, *xm;   // HBM [Tcap][CB]
+    LDS double *vb;        // [2][kLdsBatchWidth][CB]
+    LDS double *cring;     // [2][kStageEntries] staged coefficients of the narrow layers
+    LDS double *coef;      // [CB][ustride]
+    LDS uint8_t *w1;       // [Tcap]: layer had one alive node when the batch started
+    LDS int32_t *ids;      // [CB]: pool row of each batch cut
+    GBL double *s2b;       // HBM [tail_cap][CB]: layers >= kg
+    GBL double *sm, *xm;   // HBM [Tcap][CB]
     uint32_t gbase;    // noff[kg]
+#ifdef SGUFP_PROF
+    uint64_t prof[2];  // ticks: coefficient staging, merged layers
+#endif
 };
 
 
-__device__ inline void build_mirror(DD &d, uint32_t n_merged_arcs, int mcap) {
+__device__ __forceinline__ void build_mirror(DD &d, uint32_t n_merged_arcs, int mcap) {
     int kg = d.T - 1;
     for (int base = 0; base < d.T - 1; base += kWave) {
         int k = base + lane();
@@ -760,7 +776,7 @@ __device__ inline void build_mirror(DD &d, uint32_t n_merged_arcs, int mcap) {
 }
 
 // coefficients of DD layer k for the batch cuts: bv.coef[c][r] (one load per entry)
-__device__ inline void batch_coef_direct(const NetDev &net, const DD &d, BatchView &bv, const Pool &pool, int k,
+__device__ __forceinline__ void batch_coef_direct(const NetDev &net, const DD &d, BatchView &bv, const Pool &pool, int k,
                                          int nb) {
     const int us = pool.ustride, ls = d.g + k - 1;
     const size_t ltab = (size_t)net.L * us;
@@ -776,68 +792,105 @@ __device__ inline void batch_coef_direct(const NetDev &net, const DD &d, BatchVi
 // layers < kS only: the cutset layer can only move up, and exact-layer steps of a walk
 // read no state2.
 template <int CB, bool MIR>
-__device__ void sweep_narrow(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int nb, double rv, int kS) {
+__device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int nb, double rv, int kS) {
     constexpr int G = kWave / CB;
-    constexpr int PF = (CB * kMaxU + kWave - 1) / kWave;
     const int c = lane() % CB, grp = lane() / CB;
     const bool cv = c < nb;
     const int us = pool.ustride;
+    const int per_layer = nb * us;
     const size_t ltab = (size_t)net.L * us;
     if (lane() < CB && cv) {
         bv.vb[c] = rv;
         if (c == nb - 1) d.s2[0] = rv;
     }
-    // coefficient prefetch one layer ahead (registers)
-    double pf[PF];
-    auto issue = [&](int k) {
-        const int ls = d.g + k - 1;
+    // Coefficients are staged D layers at a time through a 2-slot LDS ring; the loads of
+    // group g+1 are issued when group g starts, so their latency hides behind D layers.
+    const int D = max(1, min(kStageLayers, kStageEntries / per_layer));
+    double pf[kStageEntries / kWave];
+    auto issue = [&](int k0) {
 #pragma unroll
-        for (int j = 0; j < PF; j++) {
-            int idx = lane() + j * kWave;
+        for (int j = 0; j < kStageEntries / kWave; j++) {
+            int e = lane() + j * kWave;
+            int lo = e / per_layer, rem = e - lo * per_layer;
+            int k = k0 + lo;
             pf[j] = 0.0;
-            if (k < d.kg && idx < nb * us) {
-                int cc = idx / us, r = idx - cc * us;
-                pf[j] = pool.coefT[(size_t)bv.ids[cc] * ltab + (size_t)ls * us + r];
+            if (lo < D && k < d.kg) {
+                int cc = rem / us, r = rem - cc * us;
+                pf[j] = pool.coefT[(size_t)bv.ids[cc] * ltab + (size_t)(d.g + k - 1) * us + r];
             }
         }
     };
-    if (d.kg > 1) issue(1);
-    for (int k = 1; k < d.kg; k++) {
+    auto commit = [&](int slot) {
+        LDS double *ring = bv.cring + (size_t)slot * kStageEntries;
 #pragma unroll
-        for (int j = 0; j < PF; j++) {
-            int idx = lane() + j * kWave;
-            if (idx < nb * us) bv.coef[idx] = pf[j];
+        for (int j = 0; j < kStageEntries / kWave; j++) ring[lane() + j * kWave] = pf[j];
+    };
+    issue(1);
+    commit(0);
+    issue(1 + D);
+    wave_lds_sync();
+    int gslot = 0, k0 = 1;
+    for (int k = 1; k < d.kg; k++) {
+#ifdef SGUFP_PROF
+        uint64_t t0 = wall_clock64();
+#endif
+        if (k - k0 == D) {
+            // next group: its coefficients were issued D layers ago
+            gslot ^= 1;
+            commit(gslot);
+            k0 = k;
+            issue(k0 + D);
+            wave_lds_sync();
         }
-        wave_lds_sync();
-        issue(k + 1);
+#ifdef SGUFP_PROF
+        uint64_t t1 = wall_clock64();
+        bv.prof[0] += t1 - t0;
+#endif
+        const LDS double *coefk = bv.cring + (size_t)gslot * kStageEntries + (size_t)(k - k0) * per_layer;
         const uint32_t noff = d.noff[k], n = d.nn[k];
-        const uint32_t pnoff = d.noff[k - 1];
-        const double *pbuf = bv.vb + (size_t)((k - 1) & 1) * kLdsBatchWidth * CB;
-        double *cbuf = bv.vb + (size_t)(k & 1) * kLdsBatchWidth * CB;
+        const LDS double *pbuf = bv.vb + (size_t)((k - 1) & 1) * kLdsBatchWidth * CB;
+        LDS double *cbuf = bv.vb + (size_t)(k & 1) * kLdsBatchWidth * CB;
         const bool wr = k < kS;
         const bool w1 = bv.w1[k] != 0;
         const uint32_t acnt = d.acnt[k];
+        // U independent items per lane per step: all topology words first, then all
+        // parent values / coefficients, so one step costs two LDS round trips.
+        constexpr int U = 8;
         if (acnt) {
             const uint32_t aoff = d.aoff[k];
             VP best{0.0, INT_MIN};
             double xmin = DMAX;
             bool any = false;
-            for (uint32_t a = grp; a < acnt; a += G) {
-                uint32_t p, r;
-                bool alive;
-                if (MIR) {
-                    uint16_t wd = d.mir[d.Nn + aoff + a];
-                    p = wd & kMirParent; r = (wd >> kMirRankShift) & 31u; alive = (wd & kMirAlive) != 0;
-                } else {
-                    uint32_t t = d.atopo[aoff + a];
-                    p = t & kParentMask; r = t >> kRankShift; alive = (d.aflag[aoff + a] & kAlive) != 0;
+            for (uint32_t base = 0; base < acnt; base += G * U) {
+                uint32_t p[U], r[U];
+                bool al[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const uint32_t a = base + u * G + grp;
+                    const bool ok = a < acnt && cv;
+                    if (MIR) {
+                        const uint16_t wd = ok ? d.mir[d.Nn + aoff + a] : (uint16_t)0;
+                        p[u] = wd & kMirParent; r[u] = (wd >> kMirRankShift) & 31u; al[u] = (wd & kMirAlive) != 0;
+                    } else {
+                        const uint32_t t = ok ? d.atopo[aoff + a] : 0u;
+                        p[u] = t & kParentMask; r[u] = t >> kRankShift;
+                        al[u] = ok && (d.aflag[aoff + a] & kAlive);
+                    }
                 }
-                if (cv && alive) {
-                    double x = pbuf[p * CB + c];
+                double px[U], cf[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    px[u] = al[u] ? pbuf[p[u] * CB + c] : 0.0;
+                    cf[u] = (al[u] && r[u] != 0) ? coefk[c * us + r[u]] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    if (!al[u]) continue;
+                    const uint32_t a = base + u * G + grp;
                     VP e;
                     double y;
-                    if (r != 0) { e.v = x + bv.coef[c * us + r]; e.p = prio_new((int)a); y = e.v; }
-                    else { e.v = x; e.p = prio_old((int)a); y = x + 0.0; }
+                    if (r[u] != 0) { e.v = px[u] + cf[u]; e.p = prio_new((int)a); y = e.v; }
+                    else { e.v = px[u]; e.p = prio_old((int)a); y = px[u] + 0.0; }
                     best = vp_pick(best, e);
                     xmin = fmin(xmin, y);
                     any = true;
@@ -850,7 +903,8 @@ __device__ void sweep_narrow(const NetDev &net, DD &d, BatchView &bv, const Pool
                 o.p = __shfl_xor(best.p, sft, kWave);
                 best = vp_pick(best, o);
                 xmin = fmin(xmin, __shfl_xor(xmin, sft, kWave));
-                any = any || (__shfl_xor((int)any, sft, kWave) != 0);
+                const int oany = __shfl_xor((int)any, sft, kWave);  // every lane must take part
+                any = any || oany != 0;
             }
             if (grp == 0 && cv) {
                 double v = (best.p == INT_MIN) ? DMIN : smax(best.v, DMIN);
@@ -861,37 +915,49 @@ __device__ void sweep_narrow(const NetDev &net, DD &d, BatchView &bv, const Pool
                     bv.xm[(size_t)k * CB + c] = any ? xmin : DMAX;
                 }
             }
+#ifdef SGUFP_PROF
+            wave_lds_sync();
+            bv.prof[1] += wall_clock64() - t1;
+#endif
         } else {
-            for (uint32_t base = 0; base < n; base += G) {
-                uint32_t i = base + grp;
-                if (i < n && cv) {
-                    uint32_t node = noff + i;
-                    uint32_t p, r;
-                    bool alive, inal;
+            for (uint32_t base = 0; base < n; base += G * U) {
+                uint32_t p[U], r[U];
+                bool al[U], in[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const uint32_t i = base + u * G + grp;
+                    const bool ok = i < n && cv;
                     if (MIR) {
-                        uint16_t wd = d.mir[node];
-                        p = wd & kMirParent; r = (wd >> kMirRankShift) & 31u;
-                        alive = (wd & kMirAlive) != 0; inal = (wd & kMirIn) != 0;
+                        const uint16_t wd = ok ? d.mir[noff + i] : (uint16_t)0;
+                        p[u] = wd & kMirParent; r[u] = (wd >> kMirRankShift) & 31u;
+                        al[u] = (wd & kMirAlive) != 0; in[u] = (wd & kMirIn) != 0;
                     } else {
-                        uint32_t t = d.ntopo[node];
-                        uint8_t f = d.nflag[node];
-                        p = t & kParentMask; r = t >> kRankShift;
-                        alive = (f & kAlive) != 0; inal = (f & kInAlive) != 0;
+                        const uint32_t t = ok ? d.ntopo[noff + i] : 0u;
+                        const uint8_t f = ok ? d.nflag[noff + i] : (uint8_t)0;
+                        p[u] = t & kParentMask; r[u] = t >> kRankShift;
+                        al[u] = (f & kAlive) != 0; in[u] = (f & kInAlive) != 0;
                     }
-                    if (alive) {
-                        double x, y = DMAX;
-                        if (!inal) x = DMIN;
-                        else {
-                            double px = pbuf[p * CB + c];
-                            if (r != 0) { x = px + bv.coef[c * us + r]; y = x; }
-                            else { x = px; y = px + 0.0; }
-                        }
-                        cbuf[i * CB + c] = x;
-                        if (wr && c == nb - 1) d.s2[node] = x;
-                        if (w1) {
-                            bv.sm[(size_t)k * CB + c] = x;
-                            bv.xm[(size_t)k * CB + c] = y;
-                        }
+                }
+                double px[U], cf[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const bool use = al[u] && in[u];
+                    px[u] = use ? pbuf[p[u] * CB + c] : 0.0;
+                    cf[u] = (use && r[u] != 0) ? coefk[c * us + r[u]] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    if (!al[u]) continue;
+                    const uint32_t i = base + u * G + grp;
+                    double x, y = DMAX;
+                    if (!in[u]) x = DMIN;
+                    else if (r[u] != 0) { x = px[u] + cf[u]; y = x; }
+                    else { x = px[u]; y = px[u] + 0.0; }
+                    cbuf[i * CB + c] = x;
+                    if (wr && c == nb - 1) d.s2[noff + i] = x;
+                    if (w1) {
+                        bv.sm[(size_t)k * CB + c] = x;
+                        bv.xm[(size_t)k * CB + c] = y;
                     }
                 }
             }
@@ -902,7 +968,7 @@ __device__ void sweep_narrow(const NetDev &net, DD &d, BatchView &bv, const Pool
 
 // value of node p of layer k for batch cut c (LDS for narrow layers, HBM for the tail)
 template <int CB>
-__device__ inline double batch_value(const DD &d, const BatchView &bv, int k, uint32_t p, int c) {
+__device__ __forceinline__ double batch_value(const DD &d, const BatchView &bv, int k, uint32_t p, int c) {
     if (k >= d.kg) return bv.s2b[(size_t)(d.noff[k] + p - bv.gbase) * CB + c];
     return bv.vb[(size_t)(k & 1) * kLdsBatchWidth * CB + p * CB + c];
 }
@@ -910,9 +976,9 @@ __device__ inline double batch_value(const DD &d, const BatchView &bv, int k, ui
 // One tail layer (k >= kg, exact expansion) into HBM: several independent nodes per
 // lane per step so that the loads overlap.
 template <int CB>
-__device__ void sweep_tail_layer(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int k, int nb, int kS) {
+__device__ __forceinline__ void sweep_tail_layer(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int k, int nb, int kS) {
     constexpr int G = kWave / CB;
-    constexpr int U = 4;
+    constexpr int U = 8;
     batch_coef_direct(net, d, bv, pool, k, nb);
     const int c = lane() % CB, grp = lane() / CB;
     const bool cv = c < nb;
@@ -957,7 +1023,7 @@ __device__ void sweep_tail_layer(const NetDev &net, DD &d, BatchView &bv, const 
 // redo this cut exactly (some arc is pruned, or a width-1 layer has no summary because
 // deletions made it width-1 inside the batch).
 template <int CB>
-__device__ bool dd_prune_check(const DD &d, const BatchView &bv, int c, int first, int end, double thresh,
+__device__ __forceinline__ bool dd_prune_check(const DD &d, const BatchView &bv, int c, int first, int end, double thresh,
                                double maxState) {
     for (int base = first; base < end; base += kWave)
         if (prune_fire(d, base, end, maxState, thresh, bv.sm + c, bv.xm + c, CB, bv.w1)) return true;
@@ -968,14 +1034,15 @@ __device__ bool dd_prune_check(const DD &d, const BatchView &bv, int c, int firs
 // the running-min update and maxState, without storing anything; pass B: commit the
 // terminal weights of cuts 0 .. capply.  Leaf value = parent value + coefficient.
 template <int CB>
-__device__ void fused_leaf_pass(const DD &d, BatchView &bv, const Pool &pool, int nb, int capply, VP *term, VP *mxs) {
+__device__ __forceinline__ void fused_leaf_pass(const DD &d, BatchView &bv, const Pool &pool, int nb, int capply, VP *term, VP *mxs) {
     const int last = d.T - 1;
     const uint32_t lo = d.noff[last], ln = d.nn[last];
     const int us = pool.ustride;
     const bool commit = capply >= 0;
 #pragma unroll
     for (int c = 0; c < CB; c++) { term[c] = VP{0.0, INT_MIN}; mxs[c] = VP{0.0, INT_MIN}; }
-    constexpr int U = 2;
+    constexpr int U = 4;
+    const int ncut = commit ? min(nb, capply + 1) : nb;
     for (uint32_t base = 0; base < ln; base += U * kWave) {
         uint32_t t[U];
         uint8_t f[U];
@@ -988,22 +1055,26 @@ __device__ void fused_leaf_pass(const DD &d, BatchView &bv, const Pool &pool, in
             f[u] = ok ? d.nflag[lo + i] : (uint8_t)0;
             w[u] = ok ? d.tw[lo + i] : 0.0;
         }
+        // parent values of all leaves and cuts of this step, issued together
+        double px[U][CB];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int c = 0; c < CB; c++)
+                px[u][c] = (c < ncut && (f[u] & kAlive)) ? batch_value<CB>(d, bv, last - 1, t[u] & kParentMask, c) : 0.0;
 #pragma unroll
         for (int u = 0; u < U; u++) {
             if (!(f[u] & kAlive)) continue;
             const uint32_t i = base + u * kWave + lane();
-            const uint32_t p = t[u] & kParentMask, r = t[u] >> kRankShift;
+            const uint32_t r = t[u] >> kRankShift;
             const bool inal = (f[u] & kInAlive) != 0;
             double ww = w[u];
 #pragma unroll
             for (int c = 0; c < CB; c++) {
-                if (c >= nb || (commit && c > capply)) break;
+                if (c >= ncut) continue;
                 double v;
                 if (!inal) v = DMIN;
-                else {
-                    double px = batch_value<CB>(d, bv, last - 1, p, c);
-                    v = (r != 0) ? px + bv.coef[c * us + r] : px;
-                }
+                else v = (r != 0) ? px[u][c] + bv.coef[c * us + r] : px[u][c];
                 ww = smin(ww, v);
                 if (!commit) {
                     term[c] = vp_pick(term[c], VP{ww, prio_old((int)i)});
@@ -1026,7 +1097,7 @@ __device__ void fused_leaf_pass(const DD &d, BatchView &bv, const Pool &pool, in
 // getPathForNode (DD.cpp:3796-3820): walk up, first in-arc whose parent.state2 + weight
 // equals this node's state2; if none matches, continue through the first in-arc
 // without recording a decision.  Decisions land in d.walk (bottom-up); returns count.
-__device__ int dd_walk(const NetDev &net, DD &d, uint32_t node, int k, const double *row) {
+__device__ __forceinline__ int dd_walk(const NetDev &net, DD &d, uint32_t node, int k, const GBL double *row) {
     int cnt = 0;
     while (k > 0) {
         const uint32_t pnoff = d.noff[k - 1];
@@ -1082,10 +1153,10 @@ __device__ int dd_walk(const NetDev &net, DD &d, uint32_t node, int k, const dou
     return cnt;
 }
 
-__device__ inline void load_meta_layers(DD &d, const Scratch &sc, int slot) {
-    const int32_t *meta = sc.meta + (size_t)slot * 8;
+__device__ __forceinline__ void load_meta_layers(DD &d, const Scratch &sc, int slot) {
+    const GBL int32_t *meta = sc.meta + (size_t)slot * 8;
     d.g = meta[0]; d.len = meta[1]; d.T = meta[2]; d.exact = meta[3]; d.aligned = meta[4];
-    const uint32_t *lay = sc.lay + (size_t)slot * sc.Tcap * 5;
+    const GBL uint32_t *lay = sc.lay + (size_t)slot * sc.Tcap * 5;
     for (int k = lane(); k < d.T; k += kWave) {
         d.noff[k] = lay[k]; d.nn[k] = lay[sc.Tcap + k]; d.nalive[k] = lay[2 * sc.Tcap + k];
         d.aoff[k] = lay[3 * sc.Tcap + k]; d.acnt[k] = lay[4 * sc.Tcap + k];
@@ -1093,15 +1164,15 @@ __device__ inline void load_meta_layers(DD &d, const Scratch &sc, int slot) {
     wave_mem_sync();
 }
 
-__device__ inline void store_meta_layers(const DD &d, const Scratch &sc, int slot, int last_cut, int status,
+__device__ __forceinline__ void store_meta_layers(const DD &d, const Scratch &sc, int slot, int last_cut, int status,
                                          int cut_layer, double ub) {
-    int32_t *meta = sc.meta + (size_t)slot * 8;
+    GBL int32_t *meta = sc.meta + (size_t)slot * 8;
     if (lane() == 0) {
         meta[0] = d.g; meta[1] = d.len; meta[2] = d.T; meta[3] = d.exact; meta[4] = d.aligned;
         meta[5] = last_cut; meta[6] = status; meta[7] = cut_layer;
         sc.ubv[slot] = ub;
     }
-    uint32_t *lay = sc.lay + (size_t)slot * sc.Tcap * 5;
+    GBL uint32_t *lay = sc.lay + (size_t)slot * sc.Tcap * 5;
     for (int k = lane(); k < d.T; k += kWave) {
         lay[k] = d.noff[k]; lay[sc.Tcap + k] = d.nn[k]; lay[2 * sc.Tcap + k] = d.nalive[k];
         lay[3 * sc.Tcap + k] = d.aoff[k]; lay[4 * sc.Tcap + k] = d.acnt[k];
@@ -1109,8 +1180,8 @@ __device__ inline void store_meta_layers(const DD &d, const Scratch &sc, int slo
 }
 
 // exact DD: argmax terminal arc (strict >, first wins) then the path of its tail
-__device__ int dd_solution_path(const NetDev &net, DD &d, const double *row, int16_t *out_path,
-                                const int16_t *rsol) {
+__device__ __forceinline__ int dd_solution_path(const NetDev &net, DD &d, const GBL double *row, GBL int16_t *out_path,
+                                const GBL int16_t *rsol) {
     const int last = d.T - 1;
     const uint32_t lo = d.noff[last], ln = d.nn[last];
     VP best{0.0, INT_MIN};
@@ -1134,15 +1205,15 @@ __device__ int dd_solution_path(const NetDev &net, DD &d, const double *row, int
 // ------------------------------------------------------------------------------------
 // Pool order: the feasibility list then the optimality list, each newest first
 // (NodeExplorer.cpp:935-944 / 975-983).
-__device__ inline int seq_id(const Pool &pool, int s) { return s < pool.nf ? pool.f_order[s] : pool.o_order[s - pool.nf]; }
+__device__ __forceinline__ int seq_id(const Pool &pool, int s) { return s < pool.nf ? pool.f_order[s] : pool.o_order[s - pool.nf]; }
 
 // root fold (DD.cpp:3938-3949) of the cuts at pool positions s0 + lane
-__device__ inline double root_fold_seq(const Pool &pool, const DD &d, int s0, int total) {
+__device__ __forceinline__ double root_fold_seq(const Pool &pool, const DD &d, int s0, int total) {
     int s = s0 + lane();
     double v = 0.0;
     if (s < total) {
         int id = seq_id(pool, s);
-        const double *row = pool.rows + (size_t)id * pool.stride;
+        const GBL double *row = pool.rows + (size_t)id * pool.stride;
         v = pool.rhs[id];
         for (int t = 0; t < d.len; t++) {
             int sl = d.rslot[t];
@@ -1158,10 +1229,17 @@ struct LoopState {
     int last_cut;
     uint32_t applied;
     uint32_t redo;
+    uint64_t ph[8];   // diagnostic ticks per phase (see BatchOut::phase)
+    uint64_t t;       // last stamp
+    __device__ __forceinline__ void stamp(int k) {
+        uint64_t now = wall_clock64();
+        ph[k] += now - t;
+        t = now;
+    }
 };
 
 // one cut at a time from pool position s onwards
-__device__ void cut_loop_single(const NetDev &net, DD &d, const Pool &pool, double incumbent, int s, LoopState &st) {
+__device__ __forceinline__ void cut_loop_single(const NetDev &net, DD &d, const Pool &pool, double incumbent, int s, LoopState &st) {
     const int total = pool.nf + pool.no;
     for (int s0 = s; s0 < total; s0 += kWave) {
         double rv = root_fold_seq(pool, d, s0, total);
@@ -1169,8 +1247,9 @@ __device__ void cut_loop_single(const NetDev &net, DD &d, const Pool &pool, doub
         for (int j = 0; j < cnt; j++) {
             const int seq = s0 + j;
             const int id = seq_id(pool, seq);
-            const double *row = pool.rows + (size_t)id * pool.stride;
+            const GBL double *row = pool.rows + (size_t)id * pool.stride;
             dd_sweep(net, d, row, __shfl(rv, j, kWave));
+            st.stamp(1);
             st.last_cut = id;
             st.applied++;
             if (seq < pool.nf) {
@@ -1180,13 +1259,42 @@ __device__ void cut_loop_single(const NetDev &net, DD &d, const Pool &pool, doub
                 st.ub = d.exact ? v : smin(v, st.ub);
                 if (st.ub <= incumbent) { st.status = kPrunedOptimality; return; }
             }
+            st.stamp(4);
         }
     }
 }
 
+// Exact redo of one cut whose width-1 pruning fires: a batched sweep with this cut
+// alone (state2 of every layer below the last one), then the pruning of layers
+// [first, end) from its summaries (DD.cpp:3895-3928 / 3987-4021).  Returns false
+// when a width-1 layer would lose all of its incoming arcs.
+template <int CB>
+__device__ __forceinline__ bool redo_cut(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int id,
+                                         double rv1, int first, int end, double thresh, double maxState) {
+    const int last = d.T - 1;
+    if (lane() == 0) bv.ids[0] = id;
+    for (int k = lane(); k < d.T; k += kWave) bv.w1[k] = (d.nalive[k] == 1) ? 1 : 0;
+    wave_lds_sync();
+    if (d.mirror) sweep_narrow<CB, true>(net, d, bv, pool, 1, rv1, d.T);
+    else sweep_narrow<CB, false>(net, d, bv, pool, 1, rv1, d.T);
+    if (d.kg == 0 && lane() == 0) bv.s2b[0] = rv1;
+    for (int k = max(d.kg, 1); k < last; k++) sweep_tail_layer<CB>(net, d, bv, pool, k, 1, d.T);
+    wave_mem_sync();
+    const GBL double *row = pool.rows + (size_t)id * pool.stride;
+    for (int base = first; base < end; base += kWave) {
+        uint64_t b = prune_fire(d, base, end, maxState, thresh, bv.sm, bv.xm, CB, bv.w1);
+        while (b) {
+            int k = base + (int)(__ffsll((unsigned long long)b) - 1);
+            b &= b - 1;
+            if (!dd_prune_layer(net, d, row, k, maxState, thresh)) return false;
+        }
+    }
+    return true;
+}
+
 // CB cuts of one type per sweep, replayed in pool order (see "Multi-cut sweeps")
 template <int CB>
-__device__ void cut_loop_batched(const NetDev &net, DD &d, const Scratch &sc, BatchView &bv, const Pool &pool,
+__device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const Scratch &sc, BatchView &bv, const Pool &pool,
                                  double incumbent, LoopState &st) {
     const int total = pool.nf + pool.no;
     const int last = d.T - 1;
@@ -1209,66 +1317,86 @@ __device__ void cut_loop_batched(const NetDev &net, DD &d, const Scratch &sc, Ba
         }
         const double rv = root_fold_seq(pool, d, s, total);
         wave_lds_sync();
+        st.stamp(4);
         if (d.mirror) sweep_narrow<CB, true>(net, d, bv, pool, nb, rv, kS);
         else sweep_narrow<CB, false>(net, d, bv, pool, nb, rv, kS);
+        st.stamp(1);
         if (d.kg == 0 && lane() < nb) bv.s2b[lane()] = rv;
         for (int k = max(d.kg, 1); k < last; k++) sweep_tail_layer<CB>(net, d, bv, pool, k, nb, kS);
+        st.stamp(2);
         int next = s + nb;
         if (feas) {
             // feasibility cuts: last layer materialised, removal + cascade replayed per cut
             sweep_tail_layer<CB>(net, d, bv, pool, last, nb, kS);
-            const double *lbase = bv.s2b + (size_t)(d.noff[last] - bv.gbase) * CB;
+            st.stamp(3);
+            const GBL double *lbase = bv.s2b + (size_t)(d.noff[last] - bv.gbase) * CB;
             for (int c = 0; c < nb; c++) {
                 const int seq = s + c;
-                const double *row = pool.rows + (size_t)bv.ids[c] * pool.stride;
-                st.last_cut = bv.ids[c];
+                const int id = bv.ids[c];
+                st.last_cut = id;
                 st.applied++;
                 double maxState;
                 if (!dd_remove_last(d, LastVals{lbase + c, CB}, maxState)) { st.status = kPrunedFeasibility; return; }
                 if (!d.exact && dd_prune_check<CB>(d, bv, c, 1, last, -0.01, maxState)) {
-                    dd_sweep(net, d, row, __shfl(rv, c, kWave));
-                    if (!dd_prune(net, d, row, 1, last, -0.01, maxState)) { st.status = kPrunedFeasibility; return; }
+                    st.stamp(4);
+                    if (!redo_cut<CB>(net, d, bv, pool, id, __shfl(rv, c, kWave), 1, last, -0.01, maxState)) {
+                        st.status = kPrunedFeasibility;
+                        return;
+                    }
+                    st.stamp(5);
                     next = seq + 1;
                     st.redo++;
                     break;
                 }
             }
+            st.stamp(4);
         } else {
             // optimality cuts: fused last layer (pass A: terminal states, pass B: commit)
             batch_coef_direct(net, d, bv, pool, last, nb);
             VP term[CB], mxs[CB];
             fused_leaf_pass<CB>(d, bv, pool, nb, -1, term, mxs);
+            st.stamp(3);
+            // replay in pool order (unrolled: term / mxs stay in registers)
             int capply = nb - 1, redo = -1;
-            for (int c = 0; c < nb; c++) {
+            bool stop = false, pruned = false;
+            double redo_v = DMIN, redo_ms = DMIN;
+#pragma unroll
+            for (int c = 0; c < CB; c++) {
+                if (stop || c >= nb) continue;
                 double v = (term[c].p == INT_MIN) ? DMIN : smax(DMIN, term[c].v);
-                if (v > incumbent && !d.exact) {
-                    double maxState = (mxs[c].p == INT_MIN) ? DMIN : smax(DMIN, mxs[c].v);
-                    if (dd_prune_check<CB>(d, bv, c, 3, last - 1, incumbent - 0.01, maxState)) {
-                        capply = c;
-                        redo = c;
-                        break;
-                    }
+                double maxState = (mxs[c].p == INT_MIN) ? DMIN : smax(DMIN, mxs[c].v);
+                if (v > incumbent && !d.exact &&
+                    dd_prune_check<CB>(d, bv, c, 3, last - 1, incumbent - 0.01, maxState)) {
+                    capply = c;
+                    redo = c;
+                    redo_v = v;
+                    redo_ms = maxState;
+                    stop = true;
+                    continue;
                 }
                 st.applied++;
                 st.last_cut = bv.ids[c];
                 st.ub = d.exact ? v : smin(v, st.ub);
-                if (st.ub <= incumbent) { st.status = kPrunedOptimality; return; }
+                if (st.ub <= incumbent) { stop = true; pruned = true; }
             }
+            if (pruned) { st.status = kPrunedOptimality; return; }
+            st.stamp(4);
             VP dummy_t[CB], dummy_m[CB];
             fused_leaf_pass<CB>(d, bv, pool, nb, capply, dummy_t, dummy_m);
+            st.stamp(3);
             if (redo >= 0) {
                 const int c = redo;
-                const double *row = pool.rows + (size_t)bv.ids[c] * pool.stride;
-                double v = (term[c].p == INT_MIN) ? DMIN : smax(DMIN, term[c].v);
-                double maxState = (mxs[c].p == INT_MIN) ? DMIN : smax(DMIN, mxs[c].v);
-                dd_sweep(net, d, row, __shfl(rv, c, kWave));
-                if (!dd_prune(net, d, row, 3, last - 1, incumbent - 0.01, maxState)) v = DMIN;
+                const int id = bv.ids[c];
+                double v = redo_v;
+                if (!redo_cut<CB>(net, d, bv, pool, id, __shfl(rv, c, kWave), 3, last - 1, incumbent - 0.01, redo_ms))
+                    v = DMIN;
                 st.applied++;
-                st.last_cut = bv.ids[c];
+                st.last_cut = id;
                 st.ub = d.exact ? v : smin(v, st.ub);
                 if (st.ub <= incumbent) { st.status = kPrunedOptimality; return; }
                 next = s + c + 1;
                 st.redo++;
+                st.stamp(5);
             }
         }
         s = next;
@@ -1280,7 +1408,8 @@ __device__ void cut_loop_batched(const NetDev &net, DD &d, const Scratch &sc, Ba
 template <int CB>
 __global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn in, Pool pool, BatchOut out,
                                                 double incumbent) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
     const int slot = blockIdx.x;
     if (slot >= in.n) return;
     const uint64_t t_start = wall_clock64();
@@ -1292,10 +1421,10 @@ __global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn
     d.Amir = 0;
     d.g = in.gl[slot];
     d.len = in.sol_len[slot];
-    const int16_t *rsol = in.sol + in.sol_off[slot];
+    const GBL int16_t *rsol = in.sol + in.sol_off[slot];
     d.aligned = (d.len == d.g) ? 1 : 0;
     int cut_layer = 0;
-    LoopState st{kSuccess, in.ub[slot], -1, 0, 0};
+    LoopState st{kSuccess, in.ub[slot], -1, 0, 0, {0, 0, 0, 0, 0, 0, 0, 0}, t_start};
     double lb = DMIN;
     uint32_t nchild = 0, n_nodes = 0, n_arcs = 0, n_merged = 0;
     d.T = 1; d.exact = 1;
@@ -1322,24 +1451,34 @@ __global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn
         st.status = kErrCapacity;
         goto done;
     }
+    st.stamp(0);
     if (CB > 1 && d.aligned) {
         LdsCarve cv = lds_carve(sc.Tcap, sc.Lcap, CB, sc.mir_cap);
-        d.mir = (uint16_t *)(smem + cv.o_mir);
+        d.mir = (LDS uint16_t *)(smem + cv.o_mir);
         build_mirror(d, n_merged, sc.mir_cap);
         BatchView bv;
-        bv.vb = (double *)(smem + cv.o_buf);
-        bv.coef = (double *)(smem + cv.o_bcoef);
+#ifdef SGUFP_PROF
+        bv.prof[0] = bv.prof[1] = 0;
+#endif
+        bv.vb = (LDS double *)(smem + cv.o_buf);
+        bv.cring = (LDS double *)(smem + cv.o_ring);
+        bv.coef = (LDS double *)(smem + cv.o_bcoef);
         bv.w1 = smem + cv.o_w1;
-        bv.ids = (int32_t *)(smem + cv.o_ids);
+        bv.ids = (LDS int32_t *)(smem + cv.o_ids);
         bv.s2b = sc.s2b + (size_t)slot * sc.tail_cap * CB;
         bv.sm = sc.sm + (size_t)slot * sc.Tcap * CB;
         bv.xm = sc.xm + (size_t)slot * sc.Tcap * CB;
         cut_loop_batched<CB>(net, d, sc, bv, pool, incumbent, st);
+#ifdef SGUFP_PROF
+        st.ph[6] += bv.prof[0];
+        st.ph[7] += bv.prof[1];
+#endif
     } else {
         cut_loop_single(net, d, pool, incumbent, 0, st);
     }
+    st.stamp(6);
     if (st.status == kSuccess) {
-        const double *lrow = st.last_cut >= 0 ? pool.rows + (size_t)st.last_cut * pool.stride : nullptr;
+        const GBL double *lrow = st.last_cut >= 0 ? pool.rows + (size_t)st.last_cut * pool.stride : nullptr;
         if (d.exact) {
             st.status = kNeedsSubproblem;
             int plen = dd_solution_path(net, d, lrow, out.path + (size_t)slot * sc.Lcap, rsol);
@@ -1383,26 +1522,31 @@ done:
         out.redo[slot] = st.redo | (d.mirror ? 0x80000000u : 0u) | ((d.Nn + d.Amir) << 8);
     }
     store_meta_layers(d, sc, slot, st.last_cut, st.status, cut_layer, st.ub);
-    if (lane() == 0) out.ticks[slot] = wall_clock64() - t_start;
+    st.stamp(7);
+    if (lane() == 0) {
+        out.ticks[slot] = wall_clock64() - t_start;
+        for (int k = 0; k < 8; k++) out.phase[(size_t)slot * 8 + k] = st.ph[k];
+    }
 }
 
 // ------------------------------------------------------------------------------------
 // Kernel 2: write cutset children (getCutset, DD.cpp:4179-4218) as frontier records.
 __global__ void __launch_bounds__(kWave) k_emit_children(NetDev net, Scratch sc, BatchIn in, Pool pool,
                                                          BatchOut out, ChildOut co) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
     const int slot = blockIdx.x;
     if (slot >= in.n) return;
     if (out.status[slot] != kSuccess || out.nchild[slot] == 0) return;
     DD d;
     dd_bind(d, smem, sc, slot);
     load_meta_layers(d, sc, slot);
-    const int32_t *meta = sc.meta + (size_t)slot * 8;
+    const GBL int32_t *meta = sc.meta + (size_t)slot * 8;
     const int last_cut = meta[5];
     const int k = meta[7];
     const double ub = sc.ubv[slot];
-    const double *row = last_cut >= 0 ? pool.rows + (size_t)last_cut * pool.stride : nullptr;
-    const int16_t *rsol = in.sol + in.sol_off[slot];
+    const GBL double *row = last_cut >= 0 ? pool.rows + (size_t)last_cut * pool.stride : nullptr;
+    const GBL int16_t *rsol = in.sol + in.sol_off[slot];
     const int gl = d.g + k;
     const int stride = d.len + k;
     const bool changed = net.changed[gl] != 0;
@@ -1464,7 +1608,8 @@ __global__ void __launch_bounds__(kWave) k_emit_children(NetDev net, Scratch sc,
 __global__ void __launch_bounds__(kWave) k_refine(NetDev net, Scratch sc, BatchIn in, Pool pool, BatchOut out,
                                                   const int32_t *slots, const int32_t *cut_ids,
                                                   const uint8_t *cut_is_feas, int n, double incumbent) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
     const int w = blockIdx.x;
     if (w >= n) return;
     const int slot = slots[w];
@@ -1472,7 +1617,7 @@ __global__ void __launch_bounds__(kWave) k_refine(NetDev net, Scratch sc, BatchI
     DD d;
     dd_bind(d, smem, sc, slot);
     load_meta_layers(d, sc, slot);
-    const int16_t *rsol = in.sol + in.sol_off[slot];
+    const GBL int16_t *rsol = in.sol + in.sol_off[slot];
     for (int t = lane(); t < d.len; t += kWave) {
         int dec = rsol[t];
         int s = -1;
@@ -1488,7 +1633,7 @@ __global__ void __launch_bounds__(kWave) k_refine(NetDev net, Scratch sc, BatchI
     }
     wave_lds_sync();
     const int id = cut_ids[w];
-    const double *row = pool.rows + (size_t)id * pool.stride;
+    const GBL double *row = pool.rows + (size_t)id * pool.stride;
     double rv = 0.0;
     if (lane() == 0) {
         rv = pool.rhs[id];

@@ -15,7 +15,7 @@ import numpy as np
 from .pools import NodeRecord, PoolCut, RelaxResult
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libsgufp_hip.so")
+LIB_PATH = os.environ.get("SGUFP_LIB_PATH") or os.path.join(HERE, "lib", "libsgufp_hip.so")
 
 SUCCESS, PRUNED_F, PRUNED_O, NEEDS_SUBPROBLEM = 0, 1, 2, 3
 ERR_RECORD, ERR_CAPACITY, ERR_CUTSET = 16, 17, 18
@@ -27,6 +27,7 @@ EXPORTS = [
     "sgufp_batch_sync", "sgufp_batch_results", "sgufp_batch_children_size", "sgufp_batch_children",
     "sgufp_batch_paths", "sgufp_batch_stats", "sgufp_batch_refine", "sgufp_set_timing",
     "sgufp_last_timing", "sgufp_probe_network", "sgufp_batch_debug",
+    "sgufp_batch_phases",
 ]
 
 
@@ -74,6 +75,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.sgufp_last_timing.argtypes = [P, P, P]
     lib.sgufp_probe_network.argtypes = [C.c_char_p, P, P, C.c_int32, P, P]
     lib.sgufp_batch_debug.argtypes = [P, P, P]
+    lib.sgufp_batch_phases.argtypes = [P, P]
     _lib = lib
     return lib
 
@@ -302,6 +304,11 @@ class Engine:
         r = np.zeros(self.n, dtype=np.int32)
         self._check(self.lib.sgufp_batch_debug(self.ctx, _ptr(t), _ptr(r)))
         return t, r
+
+    def phases(self):
+        t = np.zeros((self.n, 8), dtype=np.int64)
+        self._check(self.lib.sgufp_batch_phases(self.ctx, _ptr(t)))
+        return t
 
     def children_batch(self) -> BatchArrays:
         """All cutset children of the last relaxed batch as a new batch (node order kept)."""

@@ -71,6 +71,9 @@ def main():
         m = st == s
         print(f"  status {s}: n={m.sum()} us/node {us[m].mean():.1f} sweeps {sw[m].mean():.1f} "
               f"us/sweep {np.mean(us[m] / np.maximum(sw[m], 1)):.2f} redo {redo[m].mean():.2f}")
+    ph = eng.phases() / 100.0
+    names = ["build", "narrow", "tail", "last", "post", "redo", "finish", "epilog"]
+    print("phase us/node: " + ", ".join(f"{nm} {ph[:, k].mean():.0f}" for k, nm in enumerate(names)))
     big = np.argsort(-us)[:5]
     for k in big:
         print(f"  slow node {k}: {us[k]:.0f} us, dd {dn[k]} nodes, {dl[k]} layers, sweeps {sw[k]}, status {st[k]}, "
