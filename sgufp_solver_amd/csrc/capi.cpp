@@ -18,7 +18,7 @@
 
 namespace sgufp {
 // dd_kernels.hip
-size_t relax_lds_bytes(int Tcap, int Lcap, int cb, int mcap);
+size_t relax_lds_bytes(int Tcap, int Lcap, int cb);
 hipError_t launch_relax(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &, double, int,
                         hipStream_t);
 hipError_t launch_scan(const uint32_t *, const uint32_t *, int, uint64_t *, uint64_t *, hipStream_t);
@@ -260,15 +260,9 @@ bool sgufp_ctx::init() {
     if (ncap > (int64_t)kParentMask || acap > (int64_t)0x7FFFFFFF) { err = "DD capacity beyond 22-bit indices"; return false; }
     sc.Ncap = (int)ncap;
     sc.Acap = (int)acap;
-    // LDS per relax workgroup: SGUFP_LDS_KB (default 40: four single-wave workgroups per
-    // CU, one per SIMD); what the fixed carve leaves is the narrow-layer topology mirror.
-    // A budget below the fixed carve only turns the mirror off.
-    size_t lds_budget = 40 * 1024;
-    if (const char *e = getenv("SGUFP_LDS_KB")) lds_budget = (size_t)atoi(e) * 1024;
-    size_t base_lds = relax_lds_bytes(sc.Tcap, sc.Lcap, cb, 0);
-    if (base_lds > 160 * 1024) { err = "too many layers for the LDS layer table"; return false; }
-    lds_budget = std::max(lds_budget, base_lds);
-    sc.mir_cap = cb > 1 ? (int)((lds_budget - base_lds) / 2) : 0;
+    // LDS per relax workgroup (one wave): layer table, value buffers and staging rings
+    if (relax_lds_bytes(sc.Tcap, sc.Lcap, cb) > 160 * 1024) { err = "too many layers for the LDS layer table"; return false; }
+    sc.tmir_cap = cb > 1 ? (int)(sc.Ncap + sc.Acap) : 0;
     sc.tail_cap = (int)tail;
     sc.cb_max = cb;
     const size_t B = (size_t)max_batch;
@@ -280,7 +274,7 @@ bool sgufp_ctx::init() {
         !alloc(sc.meta, B * 8, "scratch") || !alloc(sc.ubv, B, "scratch"))
         return false;
     if (cb > 1 && (!alloc(sc.s2b, B * sc.tail_cap * cb, "scratch") || !alloc(sc.sm, B * sc.Tcap * cb, "scratch") ||
-                   !alloc(sc.xm, B * sc.Tcap * cb, "scratch")))
+                   !alloc(sc.xm, B * sc.Tcap * cb, "scratch") || !alloc(sc.tmir, B * (size_t)sc.tmir_cap, "scratch")))
         return false;
     // outputs
     if (!alloc(out.status, B, "out") || !alloc(out.exact, B, "out") || !alloc(out.lb, B, "out") ||

@@ -77,10 +77,11 @@ struct Scratch {
     // multi-cut sweeps (k_relax with CB > 1)
     int tail_cap;      // nodes of the HBM-resident tail layers (wide layers + last layer)
     int cb_max;        // cuts per batched sweep the buffers are sized for
-    int mir_cap;       // LDS mirror entries (16-bit) of the narrow-layer topology
     double SGUFP_GBL *s2b;       // [tail_cap * cb_max]
     double SGUFP_GBL *sm;        // [Tcap * cb_max]
     double SGUFP_GBL *xm;        // [Tcap * cb_max]
+    int tmir_cap;                // packed narrow-layer topology words per slot (Ncap + Acap)
+    uint16_t SGUFP_GBL *tmir;    // [tmir_cap]
 };
 
 // Staged batch of open nodes (Inavap::Node records, DD.h:456-478), SoA.

@@ -25,6 +25,7 @@
 
 #include <climits>
 #include <cstdint>
+#include <type_traits>
 
 #include "dd_device.hpp"
 
@@ -41,6 +42,11 @@ namespace sgufp {
 constexpr uint32_t kCollapseWidth = 120;  // RELAXED_MAX_WIDTH (DD.h:732)
 
 __device__ __forceinline__ int lane() { return (int)threadIdx.x; }
+// a wave-uniform value read from LDS / memory, moved to an SGPR (scalar branches and
+// address arithmetic instead of per-lane ones)
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint32_t uni(uint8_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 __device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }  // std::max
 __device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b : a; }  // std::min
 __device__ __forceinline__ uint32_t gsub(GBL uint32_t *p, uint32_t v) {
@@ -65,15 +71,53 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
     }
     return x;
 }
+// Butterfly partner exchange without the LDS path: DPP row rotations inside 16-lane
+// rows (a rotation by S pairs the same orbits as xor S for an all-reduce), and the
+// gfx950 permlane swaps across rows (16) and half-waves (32).  Every lane of the wave
+// must be active.
+template <int S>
+__device__ __forceinline__ uint32_t lane_x(uint32_t x) {
+    if constexpr (S == 32) {
+        auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return lane() < 32 ? r[1] : r[0];
+    } else if constexpr (S == 16) {
+        auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return (lane() & 16) ? r[0] : r[1];
+    } else {
+        static_assert(S == 1 || S == 2 || S == 4 || S == 8, "row rotation");
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x120 + S, 0xF, 0xF, false);
+    }
+}
+template <int S>
+__device__ __forceinline__ int lane_x(int x) { return (int)lane_x<S>((uint32_t)x); }
+template <int S>
+__device__ __forceinline__ double lane_x(double x) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const uint32_t lo = lane_x<S>((uint32_t)b), hi = lane_x<S>((uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// all-reduce over the lanes that differ in bits log2(S0) .. 5 of the lane id
+template <int S0, typename T, typename Op>
+__device__ __forceinline__ T lane_reduce(T x, Op op) {
+    if constexpr (S0 < kWave) {
+        x = op(x, lane_x<S0>(x));
+        return lane_reduce<S0 * 2>(x, op);
+    } else {
+        return x;
+    }
+}
+// value of lane l (wave-uniform l) in every lane
+__device__ __forceinline__ double lane_get(double x, int l) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
-#pragma unroll
-    for (int d = kWave / 2; d; d >>= 1) x += __shfl_xor(x, d, kWave);
-    return x;
+    return lane_reduce<1>(x, [](uint32_t a, uint32_t b) { return a + b; });
 }
 __device__ __forceinline__ uint32_t wave_or(uint32_t x) {
-#pragma unroll
-    for (int d = kWave / 2; d; d >>= 1) x |= __shfl_xor(x, d, kWave);
-    return x;
+    return lane_reduce<1>(x, [](uint32_t a, uint32_t b) { return a | b; });
 }
 
 // (value, priority) arg-max.  A sequential std::max fold keeps either the newer or the
@@ -84,21 +128,26 @@ struct VP {
     int p;  // INT_MIN = empty
 };
 __device__ __forceinline__ VP vp_pick(VP a, VP b) {
-    if (b.p == INT_MIN) return a;
-    if (a.p == INT_MIN) return b;
-    if (a.v > b.v) return a;
-    if (b.v > a.v) return b;
-    return (a.p > b.p) ? a : b;
+    // branch-free: selects only (this sits in the innermost sweep loops)
+    const bool take_b = (a.p == INT_MIN) | ((b.p != INT_MIN) & ((b.v > a.v) | (!(a.v > b.v) & (b.p > a.p))));
+    VP r;
+    r.v = take_b ? b.v : a.v;
+    r.p = take_b ? b.p : a.p;
+    return r;
 }
+template <int S0 = 1>
 __device__ __forceinline__ VP wave_vp(VP x) {
-#pragma unroll
-    for (int d = kWave / 2; d; d >>= 1) {
+    if constexpr (S0 < kWave) {
         VP y;
-        y.v = __shfl_xor(x.v, d, kWave);
-        y.p = __shfl_xor(x.p, d, kWave);
-        x = vp_pick(x, y);
+        y.v = lane_x<S0>(x.v);
+        y.p = lane_x<S0>(x.p);
+        return wave_vp<S0 * 2>(vp_pick(x, y));
+    } else {
+        return x;
     }
-    return x;
+}
+__device__ __forceinline__ double wave_fmin(double x) {
+    return lane_reduce<1>(x, [](double a, double b) { return fmin(a, b); });
 }
 // fold "acc = max(x_k, acc)" (new element wins ties) -> priority k;
 // fold "acc = max(acc, x_k)" (old element wins ties) -> priority -k-2.
@@ -127,39 +176,45 @@ struct DD {
     GBL double *tw;
     GBL uint32_t *atopo;
     GBL uint8_t *aflag;
-    LDS uint16_t *mir;    // LDS mirror of the narrow layers' topology (see build_mirror)
+    GBL uint16_t *tmir;   // packed topology of the narrow layers (see build_stream)
+    LDS uint16_t *gstart; // [Tcap] first layer of each staging group of the narrow sweep
     // scalars
     int g, len, T, exact, aligned;
     int kg;           // first layer wider than kLdsBatchWidth (or the last layer)
-    uint32_t Nn;      // nodes in layers < kg (mirrored node words)
+    uint32_t Nn;      // nodes in layers < kg (packed node words)
     uint32_t Amir;    // merged-layer arcs (all in layers < kg)
-    int mirror;       // mirror valid
+    int stream;       // packed topology valid
+    int ng;           // staging groups of layers 1 .. kg-1
 };
 
 constexpr int kLdsBatchWidth = 128;
-constexpr int kStageEntries = 512;   // coefficient staging ring: entries per slot (8 per lane)
+constexpr int kStageEntries = 512;   // coefficient staging ring: f64 entries per slot (8 per lane)
+constexpr int kTopoEntries = 1024;   // topology staging ring: u16 entries per slot (16 per lane)
 constexpr int kStageLayers = 16;     // at most this many layers per staging group
 constexpr uint16_t kMirParent = 127, kMirRankShift = 7, kMirAlive = 1u << 12, kMirIn = 1u << 13;
 
-// LDS mirror of the narrow layers: node word = parent:7 | rank:5 | alive | in-arc alive,
-// merged-arc word = parent:7 | rank:5 | alive.  HBM stays the master copy; every edit of
-// a narrow node / arc flag is applied to both.
+// Packed topology of the narrow layers (HBM, per DD slot): node word = parent:7 | rank:5 |
+// alive | in-arc alive for nodes [0, Nn), merged-arc word = parent:7 | rank:5 | alive for
+// arcs at Nn + [0, Amir).  Layers are contiguous in both ranges, so the words of a run of
+// layers are two contiguous segments that the narrow sweep stages into LDS ahead of use.
+// ntopo / nflag / atopo / aflag stay the master copy; every edit of a narrow node / arc
+// flag is applied to both.
 __device__ __forceinline__ void mir_node_clear(DD &d, uint32_t node, uint16_t bits) {
-    if (d.mirror && node < d.Nn) d.mir[node] &= (uint16_t)~bits;
+    if (d.stream && node < d.Nn) d.tmir[node] &= (uint16_t)~bits;
 }
 __device__ __forceinline__ void mir_arc_clear(DD &d, uint32_t a) {
-    if (d.mirror) d.mir[d.Nn + a] &= (uint16_t)~kMirAlive;
+    if (d.stream) d.tmir[d.Nn + a] &= (uint16_t)~kMirAlive;
 }
 
 struct LdsCarve {
     size_t bytes;
-    size_t o_lay, o_rslot, o_buf, o_coef, o_walk, o_bcoef, o_w1, o_ids, o_sm1, o_xm1, o_v1, o_mir, o_ring;
+    size_t o_lay, o_rslot, o_buf, o_coef, o_walk, o_bcoef, o_w1, o_ids, o_sm1, o_xm1, o_v1, o_gs, o_ring, o_tring;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // cb = cuts per batched sweep (1 = single-cut kernels only)
-__host__ __device__ inline LdsCarve lds_carve(int Tcap, int Lcap, int cb, int mcap = 0) {
+__host__ __device__ inline LdsCarve lds_carve(int Tcap, int Lcap, int cb) {
     LdsCarve c;
     size_t o = 0;
     size_t single = (size_t)2 * kLdsWidth * 8, batch = (size_t)2 * 128 * (cb > 1 ? cb : 0) * 8;
@@ -174,8 +229,9 @@ __host__ __device__ inline LdsCarve lds_carve(int Tcap, int Lcap, int cb, int mc
     c.o_sm1 = o; o = align16(o + (size_t)Tcap * 8);
     c.o_xm1 = o; o = align16(o + (size_t)Tcap * 8);
     c.o_v1 = o; o = align16(o + (size_t)Tcap);
-    c.o_ring = o; o = align16(o + (cb > 1 ? (size_t)2 * 512 * 8 : 0));
-    c.o_mir = o; o = align16(o + (cb > 1 ? (size_t)mcap * 2 : 0));
+    c.o_gs = o; o = align16(o + (cb > 1 ? (size_t)(Tcap + 1) * 2 : 0));
+    c.o_ring = o; o = align16(o + (cb > 1 ? (size_t)2 * kStageEntries * 8 : 0));
+    c.o_tring = o; o = align16(o + (cb > 1 ? (size_t)2 * kTopoEntries * 2 : 0));
     c.bytes = o;
     return c;
 }
@@ -267,7 +323,7 @@ __device__ __forceinline__ bool dd_build(const NetDev &net, DD &d, const Scratch
     bool ok = true;
     for (int a = d.g; a < L; a++, idx++) {
         if (idx + 2 > sc.Tcap) { ok = false; break; }
-        const uint32_t cnoff = d.noff[idx], cn = d.nn[idx];
+        const uint32_t cnoff = uni(d.noff[idx]), cn = uni(d.nn[idx]);
         const int upd = net.layer_update[a];
         if (upd >= 0) {  // stateUpdateMap.contains(a): every current-layer node takes the full set
             const int sl = net.set_len[upd];
@@ -300,7 +356,7 @@ __device__ __forceinline__ bool dd_build(const NetDev &net, DD &d, const Scratch
                     d.outcnt[cnoff + i] = c;
                 }
                 uni |= m;
-                carry += __shfl(incl, kWave - 1, kWave);
+                carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
             }
             uni = wave_or(uni);
             if (base_arc + carry > (uint32_t)sc.Acap || mnode + 1 > (uint32_t)sc.Ncap) { ok = false; break; }
@@ -344,12 +400,12 @@ __device__ __forceinline__ bool dd_build(const NetDev &net, DD &d, const Scratch
                     d.outcnt[cnoff + i] = c;
                 }
                 ns += wave_sum(valid ? cs : 0u);
-                carry += __shfl(incl, kWave - 1, kWave);
+                carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
             }
             if (first + carry > (uint32_t)sc.Ncap) { ok = false; break; }
             if (lane() == 0) {
                 d.noff[idx + 1] = first; d.nn[idx + 1] = carry; d.nalive[idx + 1] = carry;
-                d.aoff[idx + 1] = 0; d.acnt[idx + 1] = 0;
+                d.aoff[idx + 1] = total_arcs; d.acnt[idx + 1] = 0;  // aoff: merged arcs before the layer
             }
             total_nodes += carry;
             next_size = ns;
@@ -360,7 +416,7 @@ __device__ __forceinline__ bool dd_build(const NetDev &net, DD &d, const Scratch
     d.T = idx + 1;
     d.exact = exact;
     // terminal arcs: weight DOUBLE_MAX (DD.cpp:3587-3597); one out-arc per last-layer node
-    const uint32_t lo = d.noff[d.T - 1], ln = d.nn[d.T - 1];
+    const uint32_t lo = uni(d.noff[d.T - 1]), ln = uni(d.nn[d.T - 1]);
     for (uint32_t i = lane(); i < ln; i += kWave) {
         d.tw[lo + i] = DMAX;
         d.outcnt[lo + i] = 1;
@@ -382,19 +438,19 @@ __device__ __forceinline__ void dd_sweep(const NetDev &net, DD &d, const GBL dou
     for (int k = lane(); k < d.T; k += kWave) d.v1[k] = 0;
     wave_lds_sync();
     for (int k = 1; k < d.T; k++) {
-        const uint32_t noff = d.noff[k], n = d.nn[k];
-        const uint32_t pnoff = d.noff[k - 1], pn = d.nn[k - 1];
+        const uint32_t noff = uni(d.noff[k]), n = uni(d.nn[k]);
+        const uint32_t pnoff = uni(d.noff[k - 1]), pn = uni(d.nn[k - 1]);
         const bool prev_lds = pn <= (uint32_t)kLdsWidth;
         const bool cur_lds = n <= (uint32_t)kLdsWidth;
-        const bool w1 = d.nalive[k] == 1;
+        const bool w1 = uni(d.nalive[k]) == 1;
         LDS double *pbuf = (k & 1) ? d.buf0 : d.buf1;
         LDS double *cbuf = (k & 1) ? d.buf1 : d.buf0;
         load_layer_coef(net, d, k, row);
         wave_lds_sync();
-        const uint32_t acnt = d.acnt[k];
+        const uint32_t acnt = uni(d.acnt[k]);
         if (acnt) {
             // merged node: max over its alive incoming arcs, in creation order
-            const uint32_t aoff = d.aoff[k];
+            const uint32_t aoff = uni(d.aoff[k]);
             VP best{0.0, INT_MIN};
             double xmin = DMAX;
             for (uint32_t base = 0; base < acnt; base += kWave) {
@@ -410,8 +466,7 @@ __device__ __forceinline__ void dd_sweep(const NetDev &net, DD &d, const GBL dou
                 }
             }
             best = wave_vp(best);
-#pragma unroll
-            for (int sft = kWave / 2; sft; sft >>= 1) xmin = fmin(xmin, __shfl_xor(xmin, sft, kWave));
+            xmin = wave_fmin(xmin);
             double v = (best.p == INT_MIN) ? DMIN : smax(best.v, DMIN);
             if (lane() == 0) {
                 d.s2[noff] = v;
@@ -450,7 +505,7 @@ __device__ __forceinline__ void dd_sweep(const NetDev &net, DD &d, const GBL dou
 // arg-max with first-wins ties over alive nodes of layer k; value getter by functor
 template <typename F>
 __device__ __forceinline__ VP layer_max_first(const DD &d, int k, F val) {
-    const uint32_t noff = d.noff[k], n = d.nn[k];
+    const uint32_t noff = uni(d.noff[k]), n = uni(d.nn[k]);
     VP best{0.0, INT_MIN};
     for (uint32_t base = 0; base < n; base += kWave) {
         uint32_t i = base + lane();
@@ -461,7 +516,7 @@ __device__ __forceinline__ VP layer_max_first(const DD &d, int k, F val) {
 
 // the single alive node of a width-1 layer
 __device__ __forceinline__ uint32_t layer_single(const DD &d, int k) {
-    const uint32_t noff = d.noff[k], n = d.nn[k];
+    const uint32_t noff = uni(d.noff[k]), n = uni(d.nn[k]);
     uint32_t found = 0xFFFFFFFFu;
     for (uint32_t base = 0; base < n; base += kWave) {
         uint32_t i = base + lane();
@@ -477,13 +532,13 @@ __device__ __forceinline__ uint32_t layer_single(const DD &d, int k) {
 __device__ __forceinline__ bool dd_prune_layer(const NetDev &net, DD &d, const GBL double *row, int k, double maxState, double thresh) {
     const uint32_t M = layer_single(d, k);
     const double gain = maxState - d.s2[M];
-    const uint32_t pnoff = d.noff[k - 1];
+    const uint32_t pnoff = uni(d.noff[k - 1]);
     load_layer_coef(net, d, k, row);
     wave_lds_sync();
-    const uint32_t acnt = d.acnt[k];
+    const uint32_t acnt = uni(d.acnt[k]);
     uint32_t total = 0, pruned = 0;
     if (acnt) {
-        const uint32_t aoff = d.aoff[k];
+        const uint32_t aoff = uni(d.aoff[k]);
         for (uint32_t base = 0; base < acnt; base += kWave) {
             uint32_t a = base + lane();
             bool alive = a < acnt && (d.aflag[aoff + a] & kAlive);
@@ -532,7 +587,7 @@ __device__ __forceinline__ uint64_t prune_fire(const DD &d, int base, int end, d
                                       PV sm, PV xm, int stride, PF valid) {
     int k = base + lane();
     bool fire = false;
-    if (k < end && d.nalive[k] == 1) {
+    if (k < end && (d.nalive[k]) == 1) {
         if (!valid[k]) fire = true;
         else fire = (xm[(size_t)k * stride] + (maxState - sm[(size_t)k * stride])) <= thresh;
     }
@@ -570,7 +625,7 @@ constexpr int kUnroll = 4;
 
 __device__ __forceinline__ bool dd_remove_last(DD &d, const LastVals &lv, double &maxState) {
     const int last = d.T - 1;
-    const uint32_t lo = d.noff[last], ln = d.nn[last];
+    const uint32_t lo = uni(d.noff[last]), ln = uni(d.nn[last]);
     uint32_t rm = 0;
     VP mx{0.0, INT_MIN};
     for (uint32_t base = 0; base < ln; base += kUnroll * kWave) {
@@ -598,19 +653,19 @@ __device__ __forceinline__ bool dd_remove_last(DD &d, const LastVals &lv, double
     rm = wave_sum(rm);
     mx = wave_vp(mx);
     maxState = (mx.p == INT_MIN) ? DMIN : smax(DMIN, mx.v);
-    if (rm == d.nalive[last]) return false;
+    if (rm == uni(d.nalive[last])) return false;
     if (rm) {
         wave_mem_sync();
         // a parent dies when its last alive out-arc dies in this batch
         for (int k = last; k >= 1; k--) {
-            const uint32_t noff = d.noff[k], n = d.nn[k], pnoff = d.noff[k - 1];
-            const uint32_t acnt = d.acnt[k];
+            const uint32_t noff = uni(d.noff[k]), n = uni(d.nn[k]), pnoff = uni(d.noff[k - 1]);
+            const uint32_t acnt = uni(d.acnt[k]);
             uint32_t killed = 0, parent_killed = 0;
             if (acnt) {
                 const uint32_t M = noff;
                 if (d.nflag[M] & kKill) {
                     killed = 1;
-                    const uint32_t aoff = d.aoff[k];
+                    const uint32_t aoff = uni(d.aoff[k]);
                     for (uint32_t base = 0; base < acnt; base += kWave) {
                         uint32_t a = base + lane();
                         bool pk = false;
@@ -667,7 +722,7 @@ __device__ __forceinline__ bool dd_remove_last(DD &d, const LastVals &lv, double
 // state = max over them (DD.cpp:3975-3984); also maxState over the last layer.
 __device__ __forceinline__ double dd_terminal(DD &d, const LastVals &lv, double &maxState) {
     const int last = d.T - 1;
-    const uint32_t lo = d.noff[last], ln = d.nn[last];
+    const uint32_t lo = uni(d.noff[last]), ln = uni(d.nn[last]);
     VP best{0.0, INT_MIN}, mx{0.0, INT_MIN};
     for (uint32_t base = 0; base < ln; base += kUnroll * kWave) {
         uint8_t f[kUnroll];
@@ -700,7 +755,7 @@ __device__ __forceinline__ double dd_terminal(DD &d, const LastVals &lv, double 
 // applyFeasibilityCut after a single-cut sweep.
 __device__ __forceinline__ bool dd_post_feasibility(const NetDev &net, DD &d, const GBL double *row) {
     double maxState;
-    if (!dd_remove_last(d, LastVals{d.s2 + d.noff[d.T - 1], 1}, maxState)) return false;
+    if (!dd_remove_last(d, LastVals{d.s2 + uni(d.noff[d.T - 1]), 1}, maxState)) return false;
     if (!d.exact) return dd_prune(net, d, row, 1, d.T - 1, -0.01, maxState);
     return true;
 }
@@ -709,7 +764,7 @@ __device__ __forceinline__ bool dd_post_feasibility(const NetDev &net, DD &d, co
 __device__ __forceinline__ double dd_post_optimality(const NetDev &net, DD &d, const GBL double *row, double optimal) {
     const int last = d.T - 1;
     double maxState;
-    const double term = dd_terminal(d, LastVals{d.s2 + d.noff[last], 1}, maxState);
+    const double term = dd_terminal(d, LastVals{d.s2 + uni(d.noff[last]), 1}, maxState);
     if (term <= optimal) return term;
     if (!d.exact) {
         if (!dd_prune(net, d, row, 3, last - 1, optimal - 0.01, maxState)) return DMIN;
@@ -729,14 +784,16 @@ __device__ __forceinline__ double dd_post_optimality(const NetDev &net, DD &d, c
 // with the exact single-cut path and the batch restarts after it.
 //
 // Layout during a batch: the narrow layers (< 128 nodes: every layer but the last
-// few) keep their CB values per node in LDS, and -- when it fits -- their topology in
-// an LDS mirror of 16-bit words, so that a layer step touches no HBM; the wide tail
-// layers stream through HBM (s2b, CB values per node); for optimality batches the last
-// layer is never materialised: two fused passes compute the leaf values on the fly.
+// few) keep their CB values per node in LDS, and their packed 16-bit topology words and
+// coefficients are staged into LDS rings a group of layers ahead, so that a layer step
+// waits on no HBM load; the wide tail layers stream through HBM (s2b, CB values per
+// node); for optimality batches the last layer is never materialised: two fused passes
+// compute the leaf values on the fly.
 
 struct BatchView {
     LDS double *vb;        // [2][kLdsBatchWidth][CB]
     LDS double *cring;     // [2][kStageEntries] staged coefficients of the narrow layers
+    LDS uint16_t *tring;   // [2][kTopoEntries] staged topology words of the narrow layers
     LDS double *coef;      // [CB][ustride]
     LDS uint8_t *w1;       // [Tcap]: layer had one alive node when the batch started
     LDS int32_t *ids;      // [CB]: pool row of each batch cut
@@ -746,33 +803,56 @@ struct BatchView {
 #ifdef SGUFP_PROF
     uint64_t prof[2];  // ticks: coefficient staging, merged layers
 #endif
+#ifdef SGUFP_TRACE
+    int trace_on;
+#endif
 };
 
 
-__device__ __forceinline__ void build_mirror(DD &d, uint32_t n_merged_arcs, int mcap) {
+// Packed topology of the narrow layers (see mir_node_clear) and the staging groups of
+// the narrow sweep: runs of at most kStageLayers layers whose words fit one topology ring
+// slot and whose coefficients (per_layer_max per layer) fit one coefficient ring slot.
+// A single layer larger than a slot (a merged layer with > kTopoEntries in-arcs) leaves
+// d.stream = 0 and the DD takes the single-cut path.
+__device__ __forceinline__ void build_stream(DD &d, uint32_t n_merged_arcs, int per_layer_max) {
     int kg = d.T - 1;
     for (int base = 0; base < d.T - 1; base += kWave) {
         int k = base + lane();
-        uint64_t b = __ballot(k < d.T - 1 && d.nn[k] > (uint32_t)kLdsBatchWidth);
+        uint64_t b = __ballot(k < d.T - 1 && (d.nn[k]) > (uint32_t)kLdsBatchWidth);
         if (b) { kg = base + (int)(__ffsll((unsigned long long)b) - 1); break; }
     }
     d.kg = kg;
-    d.Nn = d.noff[kg];
+    d.Nn = uni(d.noff[kg]);
     d.Amir = n_merged_arcs;
-    d.mirror = (mcap > 0 && d.Nn + d.Amir <= (uint32_t)mcap) ? 1 : 0;
-    if (!d.mirror) return;
+    d.stream = 0;
+    const int maxl = min(kStageLayers, max(1, kStageEntries / max(1, per_layer_max)));
+    int ng = 0;
+    for (int k = 1; k < kg;) {
+        if (lane() == 0) d.gstart[ng] = (uint16_t)k;
+        ng++;
+        const uint32_t n0 = uni(d.noff[k]), a0 = uni(d.aoff[k]);
+        if ((uni(d.noff[k + 1]) - n0) + (uni(d.aoff[k + 1]) - a0) > (uint32_t)kTopoEntries) return;
+        int k1 = k + 1;
+        while (k1 < kg && k1 - k < maxl &&
+               (uni(d.noff[k1 + 1]) - n0) + (uni(d.aoff[k1 + 1]) - a0) <= (uint32_t)kTopoEntries)
+            k1++;
+        k = k1;
+    }
+    if (lane() == 0) d.gstart[ng] = (uint16_t)kg;
+    d.ng = ng;
+    d.stream = 1;
     for (uint32_t i = lane(); i < d.Nn; i += kWave) {
         uint32_t t = d.ntopo[i];
         uint8_t f = d.nflag[i];
-        d.mir[i] = (uint16_t)((t & kMirParent) | (((t >> kRankShift) & 31u) << kMirRankShift) |
-                              ((f & kAlive) ? kMirAlive : 0) | ((f & kInAlive) ? kMirIn : 0));
+        d.tmir[i] = (uint16_t)((t & kMirParent) | (((t >> kRankShift) & 31u) << kMirRankShift) |
+                               ((f & kAlive) ? kMirAlive : 0) | ((f & kInAlive) ? kMirIn : 0));
     }
     for (uint32_t a = lane(); a < d.Amir; a += kWave) {
         uint32_t t = d.atopo[a];
-        d.mir[d.Nn + a] = (uint16_t)((t & kMirParent) | (((t >> kRankShift) & 31u) << kMirRankShift) |
-                                     ((d.aflag[a] & kAlive) ? kMirAlive : 0));
+        d.tmir[d.Nn + a] = (uint16_t)((t & kMirParent) | (((t >> kRankShift) & 31u) << kMirRankShift) |
+                                      ((d.aflag[a] & kAlive) ? kMirAlive : 0));
     }
-    wave_lds_sync();
+    wave_mem_sync();
 }
 
 // coefficients of DD layer k for the batch cuts: bv.coef[c][r] (one load per entry)
@@ -787,13 +867,17 @@ __device__ __forceinline__ void batch_coef_direct(const NetDev &net, const DD &d
     wave_lds_sync();
 }
 
-// Narrow layers 1 .. kg-1: values in LDS, topology from the mirror (MIR) or HBM.
+// Narrow layers 1 .. kg-1: values in LDS; topology words and coefficients staged into
+// LDS rings one group of layers ahead (the loads of group j+1 are issued when group j
+// starts, so their latency hides behind the group's layers).
 // s2 (single values of the batch's last cut, read later by path walks) is written for
 // layers < kS only: the cutset layer can only move up, and exact-layer steps of a walk
 // read no state2.
-template <int CB, bool MIR>
-__device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int nb, double rv, int kS) {
+template <int CB>
+__device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int nb,
+                                             double rv, int kS) {
     constexpr int G = kWave / CB;
+    constexpr int PC = kStageEntries / kWave, PT = kTopoEntries / kWave;
     const int c = lane() % CB, grp = lane() / CB;
     const bool cv = c < nb;
     const int us = pool.ustride;
@@ -803,109 +887,142 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
         bv.vb[c] = rv;
         if (c == nb - 1) d.s2[0] = rv;
     }
-    // Coefficients are staged D layers at a time through a 2-slot LDS ring; the loads of
-    // group g+1 are issued when group g starts, so their latency hides behind D layers.
-    const int D = max(1, min(kStageLayers, kStageEntries / per_layer));
-    double pf[kStageEntries / kWave];
-    auto issue = [&](int k0) {
+    if (d.ng == 0) return;
+    double pf[PC] = {};
+    uint32_t pt[PT] = {};
+    auto issue = [&](int j) {
+        if (j >= d.ng) return;
+        const int k0 = uni((int)d.gstart[j]), k1 = uni((int)d.gstart[j + 1]);
+        const uint32_t n0 = uni(d.noff[k0]), nN = uni(d.noff[k1]) - n0;
+        const uint32_t a0 = uni(d.aoff[k0]), nA = uni(d.aoff[k1]) - a0;
 #pragma unroll
-        for (int j = 0; j < kStageEntries / kWave; j++) {
-            int e = lane() + j * kWave;
-            int lo = e / per_layer, rem = e - lo * per_layer;
-            int k = k0 + lo;
-            pf[j] = 0.0;
-            if (lo < D && k < d.kg) {
-                int cc = rem / us, r = rem - cc * us;
-                pf[j] = pool.coefT[(size_t)bv.ids[cc] * ltab + (size_t)(d.g + k - 1) * us + r];
-            }
+        for (int jj = 0; jj < PC; jj++) {
+            const int e = lane() + jj * kWave;
+            const int lo = e / per_layer, rem = e - lo * per_layer;
+            const int k = k0 + lo;
+            const int cc = rem / us, r = rem - cc * us;
+            const bool ok = k < k1;
+            pf[jj] = pool.coefT[ok ? (size_t)bv.ids[cc] * ltab + (size_t)(d.g + k - 1) * us + r : 0];
+        }
+#pragma unroll
+        for (int jj = 0; jj < PT; jj++) {
+            const uint32_t e = (uint32_t)(lane() + jj * kWave);
+            const uint32_t idx = e < nN ? n0 + e : (e < nN + nA ? d.Nn + a0 + (e - nN) : 0u);
+            pt[jj] = d.tmir[idx];
         }
     };
     auto commit = [&](int slot) {
         LDS double *ring = bv.cring + (size_t)slot * kStageEntries;
+        LDS uint16_t *tr = bv.tring + (size_t)slot * kTopoEntries;
 #pragma unroll
-        for (int j = 0; j < kStageEntries / kWave; j++) ring[lane() + j * kWave] = pf[j];
+        for (int jj = 0; jj < PC; jj++) ring[lane() + jj * kWave] = pf[jj];
+#pragma unroll
+        for (int jj = 0; jj < PT; jj++) tr[lane() + jj * kWave] = (uint16_t)pt[jj];
     };
-    issue(1);
+    issue(0);
     commit(0);
-    issue(1 + D);
+    issue(1);
     wave_lds_sync();
-    int gslot = 0, k0 = 1;
+    int j = 0, slot = 0;
+    int k0 = uni((int)d.gstart[0]), k1 = uni((int)d.gstart[1]);
+    uint32_t gn0 = uni(d.noff[k0]), gnN = uni(d.noff[k1]) - gn0, ga0 = uni(d.aoff[k0]);
     for (int k = 1; k < d.kg; k++) {
 #ifdef SGUFP_PROF
         uint64_t t0 = wall_clock64();
 #endif
-        if (k - k0 == D) {
-            // next group: its coefficients were issued D layers ago
-            gslot ^= 1;
-            commit(gslot);
-            k0 = k;
-            issue(k0 + D);
+        if (k == k1) {
+            // next group: its words and coefficients were issued one group ago
+            j++;
+            slot ^= 1;
+            commit(slot);
+            issue(j + 1);
+            k0 = k1;
+            k1 = uni((int)d.gstart[j + 1]);
+            gn0 = uni(d.noff[k0]);
+            gnN = uni(d.noff[k1]) - gn0;
+            ga0 = uni(d.aoff[k0]);
             wave_lds_sync();
         }
 #ifdef SGUFP_PROF
         uint64_t t1 = wall_clock64();
         bv.prof[0] += t1 - t0;
 #endif
-        const LDS double *coefk = bv.cring + (size_t)gslot * kStageEntries + (size_t)(k - k0) * per_layer;
-        const uint32_t noff = d.noff[k], n = d.nn[k];
+#ifdef SGUFP_TRACE
+        const uint64_t tl0 = __builtin_amdgcn_s_memtime();
+#endif
+        const LDS double *coefk = bv.cring + (size_t)slot * kStageEntries + (size_t)(k - k0) * per_layer;
+        const LDS uint16_t *tr = bv.tring + (size_t)slot * kTopoEntries;
+        const uint32_t noff = uni(d.noff[k]), n = uni(d.nn[k]);
         const LDS double *pbuf = bv.vb + (size_t)((k - 1) & 1) * kLdsBatchWidth * CB;
         LDS double *cbuf = bv.vb + (size_t)(k & 1) * kLdsBatchWidth * CB;
-        const bool wr = k < kS;
-        const bool w1 = bv.w1[k] != 0;
-        const uint32_t acnt = d.acnt[k];
-        // U independent items per lane per step: all topology words first, then all
-        // parent values / coefficients, so one step costs two LDS round trips.
-        constexpr int U = 8;
+        const bool w1 = uni(bv.w1[k]) != 0;
+        const uint32_t acnt = uni(d.acnt[k]);
+        // state2 of the last batch cut: only what a path walk reads (merged nodes and their
+        // parents) unless every layer is asked for (kS = T: the exact redo of one cut)
+        const bool wr = k < kS && (kS >= d.T || acnt > 0 || uni(d.acnt[k + 1]) > 0);
+        auto word = [&](uint32_t e) -> uint32_t { return (uint32_t)tr[e]; };
+        // U independent items per lane per step (U sized to the layer): all topology words
+        // first, then all parent values / coefficients, so one step costs two LDS round
+        // trips and a narrow layer runs no idle unrolled items.
+        auto dispatch = [&](uint32_t count, auto &&step) {
+            const uint32_t per = (count + G - 1) / G;
+            if (per <= 1) step(std::integral_constant<int, 1>{}, 0u);
+            else if (per <= 2) step(std::integral_constant<int, 2>{}, 0u);
+            else if (per <= 4) step(std::integral_constant<int, 4>{}, 0u);
+            else
+                for (uint32_t base = 0; base < count; base += G * 8) step(std::integral_constant<int, 8>{}, base);
+        };
         if (acnt) {
-            const uint32_t aoff = d.aoff[k];
+            const uint32_t aoff = uni(d.aoff[k]);
+            const uint32_t ebase = gnN + (aoff - ga0);   // ring entry of the layer's first arc
             VP best{0.0, INT_MIN};
             double xmin = DMAX;
             bool any = false;
-            for (uint32_t base = 0; base < acnt; base += G * U) {
+            dispatch(acnt, [&](auto Uc, uint32_t base) {
+                constexpr int U = decltype(Uc)::value;
                 uint32_t p[U], r[U];
                 bool al[U];
+                // branch-free: out-of-range items read entry 0 and are masked afterwards,
+                // so all loads of a step issue back to back
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     const uint32_t a = base + u * G + grp;
-                    const bool ok = a < acnt && cv;
-                    if (MIR) {
-                        const uint16_t wd = ok ? d.mir[d.Nn + aoff + a] : (uint16_t)0;
-                        p[u] = wd & kMirParent; r[u] = (wd >> kMirRankShift) & 31u; al[u] = (wd & kMirAlive) != 0;
-                    } else {
-                        const uint32_t t = ok ? d.atopo[aoff + a] : 0u;
-                        p[u] = t & kParentMask; r[u] = t >> kRankShift;
-                        al[u] = ok && (d.aflag[aoff + a] & kAlive);
-                    }
+                    const bool ok = (a < acnt) & cv;
+                    const uint32_t wd = word(ebase + (ok ? a : 0u));
+                    p[u] = wd & kMirParent; r[u] = (wd >> kMirRankShift) & 31u; al[u] = ok & ((wd & kMirAlive) != 0);
                 }
                 double px[U], cf[U];
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    px[u] = al[u] ? pbuf[p[u] * CB + c] : 0.0;
-                    cf[u] = (al[u] && r[u] != 0) ? coefk[c * us + r[u]] : 0.0;
+                    px[u] = pbuf[(al[u] ? p[u] : 0u) * CB + c];
+                    cf[u] = coefk[(al[u] ? c * us + r[u] : 0u)];
                 }
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    if (!al[u]) continue;
-                    const uint32_t a = base + u * G + grp;
+                    const int a = (int)(base + u * G + grp);
+                    const bool reg = r[u] != 0;
                     VP e;
-                    double y;
-                    if (r[u] != 0) { e.v = px[u] + cf[u]; e.p = prio_new((int)a); y = e.v; }
-                    else { e.v = px[u]; e.p = prio_old((int)a); y = px[u] + 0.0; }
+                    e.v = reg ? px[u] + cf[u] : px[u];
+                    e.p = al[u] ? (reg ? prio_new(a) : prio_old(a)) : INT_MIN;
+                    const double y = reg ? e.v : px[u] + 0.0;
                     best = vp_pick(best, e);
-                    xmin = fmin(xmin, y);
-                    any = true;
+                    xmin = al[u] ? fmin(xmin, y) : xmin;
+                    any = any | al[u];
                 }
-            }
-#pragma unroll
-            for (int sft = CB; sft < kWave; sft <<= 1) {
-                VP o;
-                o.v = __shfl_xor(best.v, sft, kWave);
-                o.p = __shfl_xor(best.p, sft, kWave);
-                best = vp_pick(best, o);
-                xmin = fmin(xmin, __shfl_xor(xmin, sft, kWave));
-                const int oany = __shfl_xor((int)any, sft, kWave);  // every lane must take part
-                any = any || oany != 0;
-            }
+            });
+#ifdef SGUFP_TRACE
+            const uint64_t tla = __builtin_amdgcn_s_memtime();
+#endif
+            // across the lane groups of each cut (lanes that differ in bits >= log2(CB))
+            best = wave_vp<CB>(best);
+            xmin = lane_reduce<CB>(xmin, [](double a, double b) { return fmin(a, b); });
+            any = lane_reduce<CB>((uint32_t)any, [](uint32_t a, uint32_t b) { return a | b; }) != 0;
+#ifdef SGUFP_TRACE
+            const uint64_t tlb = __builtin_amdgcn_s_memtime();
+            if (blockIdx.x == 0 && lane() == 0 && bv.trace_on)
+                printf("M k=%d acnt=%u loop=%llu red=%llu\n", k, acnt, (unsigned long long)(tla - tl0),
+                       (unsigned long long)(tlb - tla));
+#endif
             if (grp == 0 && cv) {
                 double v = (best.p == INT_MIN) ? DMIN : smax(best.v, DMIN);
                 cbuf[c] = v;
@@ -920,56 +1037,62 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
             bv.prof[1] += wall_clock64() - t1;
 #endif
         } else {
-            for (uint32_t base = 0; base < n; base += G * U) {
+            const uint32_t ebase = noff - gn0;   // ring entry of the layer's first node
+            dispatch(n, [&](auto Uc, uint32_t base) {
+                constexpr int U = decltype(Uc)::value;
                 uint32_t p[U], r[U];
                 bool al[U], in[U];
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     const uint32_t i = base + u * G + grp;
-                    const bool ok = i < n && cv;
-                    if (MIR) {
-                        const uint16_t wd = ok ? d.mir[noff + i] : (uint16_t)0;
-                        p[u] = wd & kMirParent; r[u] = (wd >> kMirRankShift) & 31u;
-                        al[u] = (wd & kMirAlive) != 0; in[u] = (wd & kMirIn) != 0;
-                    } else {
-                        const uint32_t t = ok ? d.ntopo[noff + i] : 0u;
-                        const uint8_t f = ok ? d.nflag[noff + i] : (uint8_t)0;
-                        p[u] = t & kParentMask; r[u] = t >> kRankShift;
-                        al[u] = (f & kAlive) != 0; in[u] = (f & kInAlive) != 0;
-                    }
+                    const bool ok = (i < n) & cv;
+                    const uint32_t wd = word(ebase + (ok ? i : 0u));
+                    p[u] = wd & kMirParent; r[u] = (wd >> kMirRankShift) & 31u;
+                    al[u] = ok & ((wd & kMirAlive) != 0); in[u] = (wd & kMirIn) != 0;
                 }
                 double px[U], cf[U];
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    const bool use = al[u] && in[u];
-                    px[u] = use ? pbuf[p[u] * CB + c] : 0.0;
-                    cf[u] = (use && r[u] != 0) ? coefk[c * us + r[u]] : 0.0;
+                    const bool use = al[u] & in[u];
+                    px[u] = pbuf[(use ? p[u] : 0u) * CB + c];
+                    cf[u] = coefk[(use ? c * us + r[u] : 0u)];
                 }
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    if (!al[u]) continue;
                     const uint32_t i = base + u * G + grp;
-                    double x, y = DMAX;
-                    if (!in[u]) x = DMIN;
-                    else if (r[u] != 0) { x = px[u] + cf[u]; y = x; }
-                    else { x = px[u]; y = px[u] + 0.0; }
-                    cbuf[i * CB + c] = x;
-                    if (wr && c == nb - 1) d.s2[noff + i] = x;
-                    if (w1) {
-                        bv.sm[(size_t)k * CB + c] = x;
-                        bv.xm[(size_t)k * CB + c] = y;
+                    const bool reg = r[u] != 0;
+                    const double x = !in[u] ? DMIN : (reg ? px[u] + cf[u] : px[u]);
+                    const double y = !in[u] ? DMAX : (reg ? x : px[u] + 0.0);
+                    // a dead node's slot is never read (its children are dead too)
+                    if (i < kLdsBatchWidth) cbuf[i * CB + c] = x;
+                    if (al[u]) {
+                        if (wr && c == nb - 1) d.s2[noff + i] = x;
+                        if (w1) {
+                            bv.sm[(size_t)k * CB + c] = x;
+                            bv.xm[(size_t)k * CB + c] = y;
+                        }
                     }
                 }
-            }
+            });
         }
         wave_lds_sync();
+#ifdef SGUFP_TRACE
+        {
+            const uint64_t tl1 = __builtin_amdgcn_s_memtime();
+            if (blockIdx.x == 0 && lane() == 0 && bv.trace_on)
+                printf("L k=%d n=%u acnt=%u w1=%d cyc=%llu\n", k, n, acnt, (int)w1, (unsigned long long)(tl1 - tl0));
+        }
+#endif
     }
+#ifdef SGUFP_TRACE
+    bv.trace_on = 0;
+#endif
 }
 
 // value of node p of layer k for batch cut c (LDS for narrow layers, HBM for the tail)
 template <int CB>
 __device__ __forceinline__ double batch_value(const DD &d, const BatchView &bv, int k, uint32_t p, int c) {
-    if (k >= d.kg) return bv.s2b[(size_t)(d.noff[k] + p - bv.gbase) * CB + c];
+    if (k >= d.kg) return bv.s2b[(size_t)(uni(d.noff[k]) + p - bv.gbase) * CB + c];
     return bv.vb[(size_t)(k & 1) * kLdsBatchWidth * CB + p * CB + c];
 }
 
@@ -983,8 +1106,9 @@ __device__ __forceinline__ void sweep_tail_layer(const NetDev &net, DD &d, Batch
     const int c = lane() % CB, grp = lane() / CB;
     const bool cv = c < nb;
     const int us = pool.ustride;
-    const uint32_t noff = d.noff[k], n = d.nn[k];
-    const bool w1 = bv.w1[k] != 0, wr = k < kS;
+    const uint32_t noff = uni(d.noff[k]), n = uni(d.nn[k]);
+    // state2 of tail layers is read only by the exact redo (kS = T); see sweep_narrow
+    const bool w1 = uni(bv.w1[k]) != 0, wr = kS >= d.T;
     for (uint32_t base = 0; base < n; base += G * U) {
         uint32_t t[U];
         uint8_t f[U];
@@ -1030,61 +1154,75 @@ __device__ __forceinline__ bool dd_prune_check(const DD &d, const BatchView &bv,
     return false;
 }
 
-// Fused last layer of an optimality batch.  Pass A: per cut the terminal state after
-// the running-min update and maxState, without storing anything; pass B: commit the
-// terminal weights of cuts 0 .. capply.  Leaf value = parent value + coefficient.
-template <int CB>
-__device__ __forceinline__ void fused_leaf_pass(const DD &d, BatchView &bv, const Pool &pool, int nb, int capply, VP *term, VP *mxs) {
+// Fused last layer of an optimality batch (leaf value = parent value + coefficient).
+// Pass A: per cut the terminal state after the running-min update and maxState; it
+// commits the terminal weights of all nb cuts (the common case) and keeps the previous
+// weights in `keep`.  Pass B, only when the replay stops inside the batch: the weights of
+// cuts 0 .. capply from the kept ones.  Leaves are processed U per lane per step with the
+// next step's topology loads in flight while the current step computes.
+template <int CB, bool PASS_A>
+__device__ __forceinline__ void fused_leaf(const DD &d, BatchView &bv, const Pool &pool, int ncut, GBL double *keep,
+                                           VP *term, VP *mxs) {
+    constexpr int U = CB >= 16 ? 2 : 32 / CB;
     const int last = d.T - 1;
-    const uint32_t lo = d.noff[last], ln = d.nn[last];
+    const uint32_t lo = uni(d.noff[last]), ln = uni(d.nn[last]);
     const int us = pool.ustride;
-    const bool commit = capply >= 0;
+    if (PASS_A) {
 #pragma unroll
-    for (int c = 0; c < CB; c++) { term[c] = VP{0.0, INT_MIN}; mxs[c] = VP{0.0, INT_MIN}; }
-    constexpr int U = 4;
-    const int ncut = commit ? min(nb, capply + 1) : nb;
-    for (uint32_t base = 0; base < ln; base += U * kWave) {
-        uint32_t t[U];
-        uint8_t f[U];
-        double w[U];
+        for (int c = 0; c < CB; c++) { term[c] = VP{0.0, INT_MIN}; mxs[c] = VP{0.0, INT_MIN}; }
+    }
+    uint32_t t[U], f[U];
+    double w[U];
+    auto load_topo = [&](uint32_t base) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            uint32_t i = base + u * kWave + lane();
-            bool ok = i < ln;
-            t[u] = ok ? d.ntopo[lo + i] : 0u;
-            f[u] = ok ? d.nflag[lo + i] : (uint8_t)0;
-            w[u] = ok ? d.tw[lo + i] : 0.0;
+            const uint32_t i = base + u * kWave + lane();
+            const uint32_t ic = i < ln ? i : 0u;
+            t[u] = d.ntopo[lo + ic];
+            f[u] = i < ln ? (uint32_t)d.nflag[lo + ic] : 0u;
+            w[u] = PASS_A ? d.tw[lo + ic] : keep[(size_t)ic * CB];
         }
+    };
+    load_topo(0);
+    for (uint32_t base = 0; base < ln; base += U * kWave) {
         // parent values of all leaves and cuts of this step, issued together
         double px[U][CB];
 #pragma unroll
         for (int u = 0; u < U; u++)
 #pragma unroll
             for (int c = 0; c < CB; c++)
-                px[u][c] = (c < ncut && (f[u] & kAlive)) ? batch_value<CB>(d, bv, last - 1, t[u] & kParentMask, c) : 0.0;
+                px[u][c] = batch_value<CB>(d, bv, last - 1, (f[u] & kAlive) ? (t[u] & kParentMask) : 0u, c);
+        uint32_t tc[U], fc[U];
+        double wc[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) { tc[u] = t[u]; fc[u] = f[u]; wc[u] = w[u]; }
+        if (base + U * kWave < ln) load_topo(base + U * kWave);
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            if (!(f[u] & kAlive)) continue;
             const uint32_t i = base + u * kWave + lane();
-            const uint32_t r = t[u] >> kRankShift;
-            const bool inal = (f[u] & kInAlive) != 0;
-            double ww = w[u];
+            const bool alive = (fc[u] & kAlive) != 0;
+            const uint32_t r = tc[u] >> kRankShift;
+            const bool inal = (fc[u] & kInAlive) != 0;
+            double ww = wc[u];
 #pragma unroll
             for (int c = 0; c < CB; c++) {
-                if (c >= ncut) continue;
-                double v;
-                if (!inal) v = DMIN;
-                else v = (r != 0) ? px[u][c] + bv.coef[c * us + r] : px[u][c];
-                ww = smin(ww, v);
-                if (!commit) {
-                    term[c] = vp_pick(term[c], VP{ww, prio_old((int)i)});
-                    mxs[c] = vp_pick(mxs[c], VP{v, prio_old((int)i)});
+                const double cf = bv.coef[c * us + r];
+                const double v = !inal ? DMIN : ((r != 0) ? px[u][c] + cf : px[u][c]);
+                const double nw = smin(ww, v);
+                if (c < ncut) ww = nw;
+                if (PASS_A) {
+                    const bool use = alive & (c < ncut);
+                    term[c] = vp_pick(term[c], VP{ww, use ? prio_old((int)i) : INT_MIN});
+                    mxs[c] = vp_pick(mxs[c], VP{v, use ? prio_old((int)i) : INT_MIN});
                 }
             }
-            if (commit) d.tw[lo + i] = ww;
+            if (alive) {
+                if (PASS_A) keep[(size_t)i * CB] = wc[u];
+                d.tw[lo + i] = ww;
+            }
         }
     }
-    if (!commit) {
+    if (PASS_A) {
 #pragma unroll
         for (int c = 0; c < CB; c++) {
             term[c] = wave_vp(term[c]);
@@ -1100,14 +1238,14 @@ __device__ __forceinline__ void fused_leaf_pass(const DD &d, BatchView &bv, cons
 __device__ __forceinline__ int dd_walk(const NetDev &net, DD &d, uint32_t node, int k, const GBL double *row) {
     int cnt = 0;
     while (k > 0) {
-        const uint32_t pnoff = d.noff[k - 1];
-        const uint32_t acnt = d.acnt[k];
+        const uint32_t pnoff = uni(d.noff[k - 1]);
+        const uint32_t acnt = uni(d.acnt[k]);
         const double cur = acnt ? d.s2[node] : 0.0;
         uint32_t parent;
         int found = 0;
         int16_t dec = 0;
         if (acnt) {
-            const uint32_t aoff = d.aoff[k];
+            const uint32_t aoff = uni(d.aoff[k]);
             uint32_t first_alive = 0xFFFFFFFFu, match = 0xFFFFFFFFu;
             for (uint32_t base = 0; base < acnt && match == 0xFFFFFFFFu; base += kWave) {
                 uint32_t a = base + lane();
@@ -1124,7 +1262,7 @@ __device__ __forceinline__ int dd_walk(const NetDev &net, DD &d, uint32_t node, 
             }
             uint32_t pick = (match != 0xFFFFFFFFu) ? match : first_alive;
             if (pick == 0xFFFFFFFFu) break;  // no incoming arc left (reference: UB)
-            uint32_t t = d.atopo[d.aoff[k] + pick];
+            uint32_t t = d.atopo[uni(d.aoff[k]) + pick];
             parent = pnoff + (t & kParentMask);
             if (match != 0xFFFFFFFFu) {
                 found = 1;
@@ -1155,7 +1293,7 @@ __device__ __forceinline__ int dd_walk(const NetDev &net, DD &d, uint32_t node, 
 
 __device__ __forceinline__ void load_meta_layers(DD &d, const Scratch &sc, int slot) {
     const GBL int32_t *meta = sc.meta + (size_t)slot * 8;
-    d.g = meta[0]; d.len = meta[1]; d.T = meta[2]; d.exact = meta[3]; d.aligned = meta[4];
+    d.g = uni(meta[0]); d.len = uni(meta[1]); d.T = uni(meta[2]); d.exact = uni(meta[3]); d.aligned = uni(meta[4]);
     const GBL uint32_t *lay = sc.lay + (size_t)slot * sc.Tcap * 5;
     for (int k = lane(); k < d.T; k += kWave) {
         d.noff[k] = lay[k]; d.nn[k] = lay[sc.Tcap + k]; d.nalive[k] = lay[2 * sc.Tcap + k];
@@ -1174,8 +1312,8 @@ __device__ __forceinline__ void store_meta_layers(const DD &d, const Scratch &sc
     }
     GBL uint32_t *lay = sc.lay + (size_t)slot * sc.Tcap * 5;
     for (int k = lane(); k < d.T; k += kWave) {
-        lay[k] = d.noff[k]; lay[sc.Tcap + k] = d.nn[k]; lay[2 * sc.Tcap + k] = d.nalive[k];
-        lay[3 * sc.Tcap + k] = d.aoff[k]; lay[4 * sc.Tcap + k] = d.acnt[k];
+        lay[k] = (d.noff[k]); lay[sc.Tcap + k] = (d.nn[k]); lay[2 * sc.Tcap + k] = (d.nalive[k]);
+        lay[3 * sc.Tcap + k] = (d.aoff[k]); lay[4 * sc.Tcap + k] = (d.acnt[k]);
     }
 }
 
@@ -1183,7 +1321,7 @@ __device__ __forceinline__ void store_meta_layers(const DD &d, const Scratch &sc
 __device__ __forceinline__ int dd_solution_path(const NetDev &net, DD &d, const GBL double *row, GBL int16_t *out_path,
                                 const GBL int16_t *rsol) {
     const int last = d.T - 1;
-    const uint32_t lo = d.noff[last], ln = d.nn[last];
+    const uint32_t lo = uni(d.noff[last]), ln = uni(d.nn[last]);
     VP best{0.0, INT_MIN};
     for (uint32_t base = 0; base < ln; base += kWave) {
         uint32_t i = base + lane();
@@ -1248,7 +1386,7 @@ __device__ __forceinline__ void cut_loop_single(const NetDev &net, DD &d, const 
             const int seq = s0 + j;
             const int id = seq_id(pool, seq);
             const GBL double *row = pool.rows + (size_t)id * pool.stride;
-            dd_sweep(net, d, row, __shfl(rv, j, kWave));
+            dd_sweep(net, d, row, lane_get(rv, j));
             st.stamp(1);
             st.last_cut = id;
             st.applied++;
@@ -1273,10 +1411,9 @@ __device__ __forceinline__ bool redo_cut(const NetDev &net, DD &d, BatchView &bv
                                          double rv1, int first, int end, double thresh, double maxState) {
     const int last = d.T - 1;
     if (lane() == 0) bv.ids[0] = id;
-    for (int k = lane(); k < d.T; k += kWave) bv.w1[k] = (d.nalive[k] == 1) ? 1 : 0;
+    for (int k = lane(); k < d.T; k += kWave) bv.w1[k] = ((d.nalive[k]) == 1) ? 1 : 0;
     wave_lds_sync();
-    if (d.mirror) sweep_narrow<CB, true>(net, d, bv, pool, 1, rv1, d.T);
-    else sweep_narrow<CB, false>(net, d, bv, pool, 1, rv1, d.T);
+    sweep_narrow<CB>(net, d, bv, pool, 1, rv1, d.T);
     if (d.kg == 0 && lane() == 0) bv.s2b[0] = rv1;
     for (int k = max(d.kg, 1); k < last; k++) sweep_tail_layer<CB>(net, d, bv, pool, k, 1, d.T);
     wave_mem_sync();
@@ -1298,8 +1435,8 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
                                  double incumbent, LoopState &st) {
     const int total = pool.nf + pool.no;
     const int last = d.T - 1;
-    bv.gbase = d.noff[d.kg];
-    if (d.T < 2 || d.noff[last] + d.nn[last] - bv.gbase > (uint32_t)sc.tail_cap) {
+    bv.gbase = uni(d.noff[d.kg]);
+    if (d.T < 2 || uni(d.noff[last]) + uni(d.nn[last]) - bv.gbase > (uint32_t)sc.tail_cap) {
         cut_loop_single(net, d, pool, incumbent, 0, st);
         return;
     }
@@ -1308,18 +1445,17 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
         const bool feas = s < pool.nf;
         const int nb = min(CB, (feas ? pool.nf : total) - s);
         if (lane() < nb) bv.ids[lane()] = seq_id(pool, s + lane());
-        for (int k = lane(); k < d.T; k += kWave) bv.w1[k] = (d.nalive[k] == 1) ? 1 : 0;
+        for (int k = lane(); k < d.T; k += kWave) bv.w1[k] = ((d.nalive[k]) == 1) ? 1 : 0;
         int kS = d.T;
         for (int base = 3; base < d.T; base += kWave) {
             int k = base + lane();
-            uint64_t b = __ballot(k < d.T && d.nalive[k] == 1);
+            uint64_t b = __ballot(k < d.T && (d.nalive[k]) == 1);
             if (b) { kS = base + (int)(__ffsll((unsigned long long)b) - 1) + 1; break; }
         }
         const double rv = root_fold_seq(pool, d, s, total);
         wave_lds_sync();
         st.stamp(4);
-        if (d.mirror) sweep_narrow<CB, true>(net, d, bv, pool, nb, rv, kS);
-        else sweep_narrow<CB, false>(net, d, bv, pool, nb, rv, kS);
+        sweep_narrow<CB>(net, d, bv, pool, nb, rv, kS);
         st.stamp(1);
         if (d.kg == 0 && lane() < nb) bv.s2b[lane()] = rv;
         for (int k = max(d.kg, 1); k < last; k++) sweep_tail_layer<CB>(net, d, bv, pool, k, nb, kS);
@@ -1329,17 +1465,17 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
             // feasibility cuts: last layer materialised, removal + cascade replayed per cut
             sweep_tail_layer<CB>(net, d, bv, pool, last, nb, kS);
             st.stamp(3);
-            const GBL double *lbase = bv.s2b + (size_t)(d.noff[last] - bv.gbase) * CB;
+            const GBL double *lbase = bv.s2b + (size_t)(uni(d.noff[last]) - bv.gbase) * CB;
             for (int c = 0; c < nb; c++) {
                 const int seq = s + c;
-                const int id = bv.ids[c];
+                const int id = uni(bv.ids[c]);
                 st.last_cut = id;
                 st.applied++;
                 double maxState;
                 if (!dd_remove_last(d, LastVals{lbase + c, CB}, maxState)) { st.status = kPrunedFeasibility; return; }
                 if (!d.exact && dd_prune_check<CB>(d, bv, c, 1, last, -0.01, maxState)) {
                     st.stamp(4);
-                    if (!redo_cut<CB>(net, d, bv, pool, id, __shfl(rv, c, kWave), 1, last, -0.01, maxState)) {
+                    if (!redo_cut<CB>(net, d, bv, pool, id, lane_get(rv, c), 1, last, -0.01, maxState)) {
                         st.status = kPrunedFeasibility;
                         return;
                     }
@@ -1354,7 +1490,8 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
             // optimality cuts: fused last layer (pass A: terminal states, pass B: commit)
             batch_coef_direct(net, d, bv, pool, last, nb);
             VP term[CB], mxs[CB];
-            fused_leaf_pass<CB>(d, bv, pool, nb, -1, term, mxs);
+            GBL double *keep = bv.s2b + (size_t)(uni(d.noff[last]) - bv.gbase) * CB;  // free in O batches
+            fused_leaf<CB, true>(d, bv, pool, nb, keep, term, mxs);
             st.stamp(3);
             // replay in pool order (unrolled: term / mxs stay in registers)
             int capply = nb - 1, redo = -1;
@@ -1381,14 +1518,15 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
             }
             if (pruned) { st.status = kPrunedOptimality; return; }
             st.stamp(4);
-            VP dummy_t[CB], dummy_m[CB];
-            fused_leaf_pass<CB>(d, bv, pool, nb, capply, dummy_t, dummy_m);
-            st.stamp(3);
+            if (capply < nb - 1) {
+                fused_leaf<CB, false>(d, bv, pool, capply + 1, keep, nullptr, nullptr);
+                st.stamp(3);
+            }
             if (redo >= 0) {
                 const int c = redo;
-                const int id = bv.ids[c];
+                const int id = uni(bv.ids[c]);
                 double v = redo_v;
-                if (!redo_cut<CB>(net, d, bv, pool, id, __shfl(rv, c, kWave), 3, last - 1, incumbent - 0.01, redo_ms))
+                if (!redo_cut<CB>(net, d, bv, pool, id, lane_get(rv, c), 3, last - 1, incumbent - 0.01, redo_ms))
                     v = DMIN;
                 st.applied++;
                 st.last_cut = id;
@@ -1415,12 +1553,13 @@ __global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn
     const uint64_t t_start = wall_clock64();
     DD d;
     dd_bind(d, smem, sc, slot, CB);
-    d.mirror = 0;
+    d.stream = 0;
+    d.ng = 0;
     d.kg = 0;
     d.Nn = 0;
     d.Amir = 0;
-    d.g = in.gl[slot];
-    d.len = in.sol_len[slot];
+    d.g = uni((int)in.gl[slot]);
+    d.len = uni((int)in.sol_len[slot]);
     const GBL int16_t *rsol = in.sol + in.sol_off[slot];
     d.aligned = (d.len == d.g) ? 1 : 0;
     int cut_layer = 0;
@@ -1453,22 +1592,28 @@ __global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn
     }
     st.stamp(0);
     if (CB > 1 && d.aligned) {
-        LdsCarve cv = lds_carve(sc.Tcap, sc.Lcap, CB, sc.mir_cap);
-        d.mir = (LDS uint16_t *)(smem + cv.o_mir);
-        build_mirror(d, n_merged, sc.mir_cap);
+        LdsCarve cv = lds_carve(sc.Tcap, sc.Lcap, CB);
+        d.tmir = sc.tmir + (size_t)slot * sc.tmir_cap;
+        d.gstart = (LDS uint16_t *)(smem + cv.o_gs);
         BatchView bv;
+#ifdef SGUFP_TRACE
+        bv.trace_on = 1;
+#endif
 #ifdef SGUFP_PROF
         bv.prof[0] = bv.prof[1] = 0;
 #endif
         bv.vb = (LDS double *)(smem + cv.o_buf);
         bv.cring = (LDS double *)(smem + cv.o_ring);
+        bv.tring = (LDS uint16_t *)(smem + cv.o_tring);
         bv.coef = (LDS double *)(smem + cv.o_bcoef);
         bv.w1 = smem + cv.o_w1;
         bv.ids = (LDS int32_t *)(smem + cv.o_ids);
         bv.s2b = sc.s2b + (size_t)slot * sc.tail_cap * CB;
         bv.sm = sc.sm + (size_t)slot * sc.Tcap * CB;
         bv.xm = sc.xm + (size_t)slot * sc.Tcap * CB;
-        cut_loop_batched<CB>(net, d, sc, bv, pool, incumbent, st);
+        build_stream(d, n_merged, CB * pool.ustride);   // tmir_cap = Ncap + Acap >= Nn + Amir
+        if (d.stream) cut_loop_batched<CB>(net, d, sc, bv, pool, incumbent, st);
+        else cut_loop_single(net, d, pool, incumbent, 0, st);
 #ifdef SGUFP_PROF
         st.ph[6] += bv.prof[0];
         st.ph[7] += bv.prof[1];
@@ -1485,14 +1630,14 @@ __global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn
             if (lane() == 0) out.path_len[slot] = (uint16_t)plen;
         } else {
             int k = 3;
-            while (k < d.T && d.nalive[k] != 1) k++;
+            while (k < d.T && uni(d.nalive[k]) != 1) k++;
             if (k >= d.T) {
                 st.status = kErrCutset;
             } else {
                 cut_layer = k;
                 const uint32_t M = layer_single(d, k);
-                if (d.acnt[k]) {
-                    const uint32_t aoff = d.aoff[k], acnt = d.acnt[k];
+                if (uni(d.acnt[k])) {
+                    const uint32_t aoff = uni(d.aoff[k]), acnt = uni(d.acnt[k]);
                     for (uint32_t base = 0; base < acnt; base += kWave) {
                         uint32_t a = base + lane();
                         nchild += wave_sum((a < acnt && (d.aflag[aoff + a] & kAlive)) ? 1u : 0u);
@@ -1519,7 +1664,7 @@ done:
         out.dd_arcs[slot] = n_arcs;
         out.dd_layers[slot] = (uint32_t)d.T + 1;
         out.sweeps[slot] = st.applied;
-        out.redo[slot] = st.redo | (d.mirror ? 0x80000000u : 0u) | ((d.Nn + d.Amir) << 8);
+        out.redo[slot] = st.redo | (d.stream ? 0x80000000u : 0u) | ((d.Nn + d.Amir) << 8);
     }
     store_meta_layers(d, sc, slot, st.last_cut, st.status, cut_layer, st.ub);
     st.stamp(7);
@@ -1542,8 +1687,8 @@ __global__ void __launch_bounds__(kWave) k_emit_children(NetDev net, Scratch sc,
     dd_bind(d, smem, sc, slot);
     load_meta_layers(d, sc, slot);
     const GBL int32_t *meta = sc.meta + (size_t)slot * 8;
-    const int last_cut = meta[5];
-    const int k = meta[7];
+    const int last_cut = uni(meta[5]);
+    const int k = uni(meta[7]);
     const double ub = sc.ubv[slot];
     const GBL double *row = last_cut >= 0 ? pool.rows + (size_t)last_cut * pool.stride : nullptr;
     const GBL int16_t *rsol = in.sol + in.sol_off[slot];
@@ -1557,19 +1702,19 @@ __global__ void __launch_bounds__(kWave) k_emit_children(NetDev net, Scratch sc,
     }
     const uint64_t cbase = co.child_off[slot];
     const uint64_t sbase = co.sol_base[slot];
-    const uint32_t pnoff = d.noff[k - 1];
+    const uint32_t pnoff = uni(d.noff[k - 1]);
     const uint32_t M = layer_single(d, k);
 
     // enumerate the alive in-arcs of M in order: (parent, rank)
-    const uint32_t acnt = d.acnt[k] ? d.acnt[k] : 1u;
+    const uint32_t acnt = uni(d.acnt[k]) ? uni(d.acnt[k]) : 1u;
     uint32_t child = 0;
     uint32_t cur_parent = 0xFFFFFFFFu;
     int plen = 0;
     for (uint32_t a = 0; a < acnt; a++) {
         uint32_t p, r;
-        if (d.acnt[k]) {
-            if (!(d.aflag[d.aoff[k] + a] & kAlive)) continue;
-            uint32_t t = d.atopo[d.aoff[k] + a];
+        if (uni(d.acnt[k])) {
+            if (!(d.aflag[uni(d.aoff[k]) + a] & kAlive)) continue;
+            uint32_t t = d.atopo[uni(d.aoff[k]) + a];
             p = t & kParentMask;
             r = t >> kRankShift;
         } else {
@@ -1642,7 +1787,7 @@ __global__ void __launch_bounds__(kWave) k_refine(NetDev net, Scratch sc, BatchI
             if (s >= 0) rv = rv + row[s];
         }
     }
-    rv = __shfl(rv, 0, kWave);
+    rv = lane_get(rv, 0);
     dd_sweep(net, d, row, rv);
     int status = kNeedsSubproblem;
     double ub = sc.ubv[slot];
@@ -1695,12 +1840,12 @@ __global__ void __launch_bounds__(1024) k_scan2(const uint32_t *a, const uint32_
 
 // ------------------------------------------------------------------------------------
 // host-side launchers (called from capi.cpp)
-size_t relax_lds_bytes(int Tcap, int Lcap, int cb, int mcap) { return lds_carve(Tcap, Lcap, cb, mcap).bytes; }
+size_t relax_lds_bytes(int Tcap, int Lcap, int cb) { return lds_carve(Tcap, Lcap, cb).bytes; }
 
 hipError_t launch_relax(const NetDev &net, const Scratch &sc, const BatchIn &in, const Pool &pool,
                         const BatchOut &out, double incumbent, int cb, hipStream_t st) {
     if (in.n <= 0) return hipSuccess;
-    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, cb, sc.mir_cap);
+    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, cb);
     switch (cb) {
         case 4: hipLaunchKernelGGL(k_relax<4>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent); break;
         case 8: hipLaunchKernelGGL(k_relax<8>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent); break;
@@ -1718,7 +1863,7 @@ hipError_t launch_scan(const uint32_t *a, const uint32_t *b, int n, uint64_t *oa
 hipError_t launch_emit(const NetDev &net, const Scratch &sc, const BatchIn &in, const Pool &pool,
                        const BatchOut &out, const ChildOut &co, hipStream_t st) {
     if (in.n <= 0) return hipSuccess;
-    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, 1, 0);
+    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, 1);
     hipLaunchKernelGGL(k_emit_children, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, co);
     return hipGetLastError();
 }
@@ -1727,7 +1872,7 @@ hipError_t launch_refine(const NetDev &net, const Scratch &sc, const BatchIn &in
                          const BatchOut &out, const int32_t *slots, const int32_t *cut_ids,
                          const uint8_t *cut_is_feas, int n, double incumbent, hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, 1, 0);
+    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, 1);
     hipLaunchKernelGGL(k_refine, dim3(n), dim3(kWave), lds, st, net, sc, in, pool, out, slots, cut_ids,
                        cut_is_feas, n, incumbent);
     return hipGetLastError();

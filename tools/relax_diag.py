@@ -56,7 +56,7 @@ def main():
     ticks, rinfo = eng.debug()
     rinfo = rinfo.astype(np.int64) & 0xFFFFFFFF
     redo = rinfo & 0xFF
-    mirror = (rinfo >> 31) & 1
+    stream = (rinfo >> 31) & 1
     mirsz = (rinfo >> 8) & 0x7FFFFF
     us = ticks / 100.0
     print(f"cb={os.environ.get('SGUFP_CUT_BATCH', 'default')} inc={inc:.3f} k_relax={ms_relax:.2f} ms "
@@ -65,7 +65,7 @@ def main():
     print(f"wave us: mean {us.mean():.1f} p50 {np.median(us):.1f} p90 {np.percentile(us, 90):.1f} "
           f"max {us.max():.1f}; sum/CU(256) {us.sum() / 256 / 1e3:.2f} ms")
     print(f"dd nodes mean {dn.mean():.0f} max {dn.max()}; sweeps mean {sw.mean():.1f}; redo mean {redo.mean():.2f} "
-          f"max {redo.max()}; mirror {mirror.mean():.2f} (entries mean {mirsz.mean():.0f} max {mirsz.max()}) "
+          f"max {redo.max()}; stream {stream.mean():.2f} (entries mean {mirsz.mean():.0f} max {mirsz.max()}) "
           f"cap {eng.info.node_capacity}")
     for s in np.unique(st):
         m = st == s
