@@ -188,7 +188,7 @@ struct DD {
 };
 
 constexpr int kLdsBatchWidth = 128;
-constexpr int kStageEntries = 512;   // coefficient staging ring: f64 entries per slot (8 per lane)
+constexpr int kStageEntries = 256;   // coefficient staging ring: f64 entries per slot (4 per lane)
 constexpr int kTopoEntries = 1024;   // topology staging ring: u16 entries per slot (16 per lane)
 constexpr int kStageLayers = 16;     // at most this many layers per staging group
 constexpr uint16_t kMirParent = 127, kMirRankShift = 7, kMirAlive = 1u << 12, kMirIn = 1u << 13;
@@ -226,12 +226,19 @@ __host__ __device__ inline LdsCarve lds_carve(int Tcap, int Lcap, int cb) {
     c.o_bcoef = o; o = align16(o + (cb > 1 ? (size_t)cb * kMaxU * 8 : 0));
     c.o_w1 = o; o = align16(o + (cb > 1 ? (size_t)Tcap : 0));
     c.o_ids = o; o = align16(o + (cb > 1 ? (size_t)cb * 4 : 0));
+    c.o_gs = o; o = align16(o + (cb > 1 ? (size_t)(Tcap + 1) * 2 : 0));
+    // The single-cut summaries (sm1 / xm1 / v1) and the batched-sweep staging rings are
+    // never live together in one DD (a DD takes either the batched or the single-cut
+    // loop; redo uses the batched sweep), so they share one region.
+    const size_t r0 = o;
     c.o_sm1 = o; o = align16(o + (size_t)Tcap * 8);
     c.o_xm1 = o; o = align16(o + (size_t)Tcap * 8);
     c.o_v1 = o; o = align16(o + (size_t)Tcap);
-    c.o_gs = o; o = align16(o + (cb > 1 ? (size_t)(Tcap + 1) * 2 : 0));
+    const size_t single_end = o;
+    o = r0;
     c.o_ring = o; o = align16(o + (cb > 1 ? (size_t)2 * kStageEntries * 8 : 0));
     c.o_tring = o; o = align16(o + (cb > 1 ? (size_t)2 * kTopoEntries * 2 : 0));
+    if (o < single_end) o = single_end;
     c.bytes = o;
     return c;
 }
