@@ -127,6 +127,25 @@ int sgufp_batch_debug(sgufp_ctx *ctx, int64_t *ticks, int32_t *redo);
 /* ticks per phase [n * 8]: build, narrow sweep, tail layers, last layer, replay/post, redo, finish, tail */
 int sgufp_batch_phases(sgufp_ctx *ctx, int64_t *phase);
 
+/* -- scenario subproblem (replaces GuroSolver::solveSubProblem, grb.h:75 / grb.cpp:139-360) --
+ * For n paths (concatenated int16 decisions, one per DD layer, path_off has n+1 entries)
+ * solve every scenario's flow LP on the device and build the cut the reference would add:
+ * type[k] = 0 optimality cut (sum over scenarios / S, grb.cpp:236-281), 1 feasibility cut
+ * (ray of the first infeasible scenario, grb.cpp:288-350), -1 invalid path / numerical
+ * failure.  rhs[k], rows[k * (n_slots + 1) ...] (dense coefficient row, slot keys from
+ * sgufp_slot_keys, last entry 0) and obj_mean[k] = sum_s objective_s / S; any output
+ * pointer may be NULL.  Paths longer than totalLayers are an argument error. */
+int sgufp_subproblem(sgufp_ctx *ctx, int n, const int64_t *path_off, const int16_t *paths, int32_t *type,
+                     double *rhs, double *rows, double *obj_mean);
+/* Per (path, scenario) detail of the last sgufp_subproblem call, [n * S] each: status (0
+ * optimal, 1 infeasible, 2 error), primal objective, objective of the dual built. */
+int sgufp_subproblem_detail(sgufp_ctx *ctx, int32_t *status, double *objective, double *dual_objective);
+/* Inavap::getKey(q, i, j) (Cut.h:342-344) of every coefficient slot (n_slots entries). */
+int sgufp_slot_keys(const sgufp_ctx *ctx, uint64_t *keys);
+/* Append cuts given as dense rows (n_slots + 1 doubles each, as sgufp_subproblem returns
+ * them) -- the device-side counterpart of Container::add (Cut.h:461-465). */
+int sgufp_cuts_append_rows(sgufp_ctx *ctx, int is_feasibility, int n_cuts, const double *rhs, const double *rows);
+
 /* -- timing (hipEvents on the ctx stream around each kernel of the last relax) -- */
 int sgufp_set_timing(sgufp_ctx *ctx, int enabled);
 int sgufp_last_timing(const sgufp_ctx *ctx, float *ms_relax, float *ms_emit);

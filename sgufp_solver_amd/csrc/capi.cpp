@@ -15,10 +15,13 @@
 #define SGUFP_HOST_ONLY 1  // no device code here: plain pointers in the device pass too
 #include "dd_device.hpp"
 #include "network.hpp"
+#include "sub_device.hpp"
 
 namespace sgufp {
 // dd_kernels.hip
 size_t relax_lds_bytes(int Tcap, int Lcap, int cb);
+size_t sub_lds_bytes(int n, int m, int n_slots);
+hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st);
 hipError_t launch_relax(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &, double, int,
                         hipStream_t);
 hipError_t launch_scan(const uint32_t *, const uint32_t *, int, uint64_t *, uint64_t *, hipStream_t);
@@ -90,6 +93,19 @@ struct sgufp_ctx {
     // refine staging
     int32_t *d_rslots = nullptr, *d_rcuts = nullptr;
     uint8_t *d_rfeas = nullptr;
+
+    // scenario subproblem (built on first use)
+    bool sub_ready = false;
+    SubNet sn{};
+    SubIO sio{};
+    int sub_cap = 0;                          // paths the per-path buffers hold
+    size_t sub_path_cap = 0;                  // int16 decisions
+    int64_t *d_spoff = nullptr;
+    int16_t *d_spaths = nullptr;
+    int sub_last_n = 0;
+    bool sub_init();
+    bool sub_grow(int n, size_t total);
+    bool append_rows(int is_feasibility, int n_cuts, const double *rhs, const std::vector<double> &rows);
 
     bool timing = false;
     hipEvent_t ev[4] = {};
@@ -465,9 +481,13 @@ int sgufp_cuts_append(sgufp_ctx *ctx, int is_feasibility, int n_cuts, const doub
             }
         }
     }
+    return ctx->append_rows(is_feasibility, n_cuts, rhs, rows) ? SGUFP_OK : SGUFP_ERR_HIP;
+}
+
+bool sgufp_ctx::append_rows(int is_feasibility, int n_cuts, const double *rhs_in, const std::vector<double> &rows) {
     // per (layer, state rank) coefficients for the batched sweeps: coefT[l][r] = row[slot_tab[l][r]]
-    const Network &net = ctx->net;
-    const int us = ctx->ustride;
+    const size_t stride = (size_t)net.n_slots + 1;
+    const int us = ustride;
     const size_t tstride = (size_t)std::max(net.L, 1) * us;
     std::vector<double> coefT((size_t)n_cuts * tstride, 0.0);
     for (int c = 0; c < n_cuts; c++)
@@ -476,15 +496,156 @@ int sgufp_cuts_append(sgufp_ctx *ctx, int is_feasibility, int n_cuts, const doub
                 int sl = net.slot_tab[(size_t)l * kMaxStates + r];
                 if (sl >= 0) coefT[(size_t)c * tstride + (size_t)l * us + r] = rows[(size_t)c * stride + sl];
             }
-    int first = ctx->n_rows;
-    if (!ctx->grow_rows(first + n_cuts)) return SGUFP_ERR_HIP;
-    if (!ctx->upload(ctx->d_coefT + (size_t)first * tstride, coefT.data(), coefT.size()) ||
-        !ctx->upload(ctx->d_rows + (size_t)first * stride, rows.data(), rows.size()) ||
-        !ctx->upload(ctx->d_rhs + first, rhs, (size_t)n_cuts) || !ctx->sync())
+    int first = n_rows;
+    if (!grow_rows(first + n_cuts)) return false;
+    if (!upload(d_coefT + (size_t)first * tstride, coefT.data(), coefT.size()) ||
+        !upload(d_rows + (size_t)first * stride, rows.data(), rows.size()) ||
+        !upload(d_rhs + first, rhs_in, (size_t)n_cuts) || !sync())
+        return false;
+    for (int c = 0; c < n_cuts; c++) (is_feasibility ? f_rows : o_rows).push_back(first + c);
+    n_rows += n_cuts;
+    order_dirty = true;
+    return true;
+}
+
+int sgufp_cuts_append_rows(sgufp_ctx *ctx, int is_feasibility, int n_cuts, const double *rhs, const double *rows) {
+    if (!ctx || n_cuts < 0 || (n_cuts && (!rhs || !rows))) return SGUFP_ERR_ARG;
+    if (n_cuts == 0) return SGUFP_OK;
+    const size_t stride = (size_t)ctx->net.n_slots + 1;
+    std::vector<double> r(rows, rows + (size_t)n_cuts * stride);
+    for (int c = 0; c < n_cuts; c++) r[(size_t)c * stride + stride - 1] = 0.0;   // the absent-key slot
+    return ctx->append_rows(is_feasibility, n_cuts, rhs, r) ? SGUFP_OK : SGUFP_ERR_HIP;
+}
+
+int sgufp_slot_keys(const sgufp_ctx *ctx, uint64_t *keys) {
+    if (!ctx || !keys) return SGUFP_ERR_ARG;
+    for (int s = 0; s < ctx->net.n_slots; s++) keys[s] = ctx->net.slot_key(s);
+    return SGUFP_OK;
+}
+
+// ---- scenario subproblem ------------------------------------------------------------
+bool sgufp_ctx::sub_init() {
+    if (sub_ready) return true;
+    const Network &N = net;
+    const int n = N.n, m = N.m, S = N.S;
+    if (sub_lds_bytes(n, m, N.n_slots) > 160 * 1024) { err = "network too large for the LDS subproblem"; return false; }
+    std::vector<int32_t> inner(n), arc_layer(m, -1), lb((size_t)S * m), ub((size_t)S * m), rew(m);
+    std::vector<uint8_t> vb(n), in8(n);
+    std::vector<int32_t> in_off(n + 1, 0), out_off(n + 1, 0), in_list, out_list;
+    for (int v = 0; v < n; v++) {
+        vb[v] = N.is_vbar[v];
+        in8[v] = (!N.in_arcs[v].empty() && !N.out_arcs[v].empty()) ? 1 : 0;
+        in_off[v] = (int32_t)in_list.size();
+        for (int a : N.in_arcs[v]) in_list.push_back(a);
+        out_off[v] = (int32_t)out_list.size();
+        for (int a : N.out_arcs[v]) out_list.push_back(a);
+    }
+    in_off[n] = (int32_t)in_list.size();
+    out_off[n] = (int32_t)out_list.size();
+    for (int l = 0; l < N.L; l++) arc_layer[N.layer_arc[l]] = l;
+    for (int a = 0; a < m; a++) {
+        rew[a] = N.reward[(size_t)a * S];
+        for (int s = 0; s < S; s++) {
+            lb[(size_t)s * m + a] = N.lb[(size_t)a * S + s];
+            ub[(size_t)s * m + a] = N.ub[(size_t)a * S + s];
+        }
+    }
+    int32_t *d_tail, *d_head, *d_layer, *d_lb, *d_ub, *d_rew, *d_ioff, *d_il, *d_ooff, *d_ol, *d_soff, *d_shead;
+    uint8_t *d_vb, *d_inner;
+    if (!alloc(d_tail, m, "sub") || !alloc(d_head, m, "sub") || !alloc(d_layer, m, "sub") ||
+        !alloc(d_lb, (size_t)S * m, "sub") || !alloc(d_ub, (size_t)S * m, "sub") || !alloc(d_rew, m, "sub") ||
+        !alloc(d_ioff, n + 1, "sub") || !alloc(d_il, m, "sub") || !alloc(d_ooff, n + 1, "sub") ||
+        !alloc(d_ol, m, "sub") || !alloc(d_soff, N.L + 1, "sub") || !alloc(d_shead, N.n_slots, "sub") ||
+        !alloc(d_vb, n, "sub") || !alloc(d_inner, n, "sub"))
+        return false;
+    if (!upload(d_tail, N.tail.data(), m) || !upload(d_head, N.head.data(), m) || !upload(d_layer, arc_layer.data(), m) ||
+        !upload(d_lb, lb.data(), lb.size()) || !upload(d_ub, ub.data(), ub.size()) || !upload(d_rew, rew.data(), m) ||
+        !upload(d_ioff, in_off.data(), in_off.size()) || !upload(d_il, in_list.data(), in_list.size()) ||
+        !upload(d_ooff, out_off.data(), out_off.size()) || !upload(d_ol, out_list.data(), out_list.size()) ||
+        !upload(d_soff, N.slot_off.data(), N.slot_off.size()) || !upload(d_shead, N.slot_head.data(), N.slot_head.size()) ||
+        !upload(d_vb, vb.data(), n) || !upload(d_inner, in8.data(), n) || !sync())
+        return false;
+    sn.n = n; sn.m = m; sn.S = S; sn.L = N.L; sn.n_slots = N.n_slots;
+    sn.tail = d_tail; sn.head = d_head; sn.vbar = d_vb; sn.inner = d_inner; sn.arc_layer = d_layer;
+    sn.lb = d_lb; sn.ub = d_ub; sn.reward = d_rew;
+    sn.in_off = d_ioff; sn.in_list = d_il; sn.out_off = d_ooff; sn.out_list = d_ol;
+    sn.slot_off = d_soff; sn.slot_head = d_shead;
+    sub_ready = true;
+    return true;
+}
+
+bool sgufp_ctx::sub_grow(int n, size_t total) {
+    const int S = net.S, ns = net.n_slots;
+    if (n > sub_cap) {
+        int cap = std::max(n, 2 * sub_cap);
+        int32_t *st, *ct;
+        double *ob, *du, *rh, *cf, *crh, *crow, *om;
+        if (!alloc(st, (size_t)cap * S, "sub io") || !alloc(ob, (size_t)cap * S, "sub io") ||
+            !alloc(du, (size_t)cap * S, "sub io") || !alloc(rh, (size_t)cap * S, "sub io") ||
+            !alloc(cf, (size_t)cap * S * std::max(ns, 1), "sub io") || !alloc(ct, cap, "sub io") ||
+            !alloc(crh, cap, "sub io") || !alloc(crow, (size_t)cap * (ns + 1), "sub io") || !alloc(om, cap, "sub io"))
+            return false;
+        if (sub_cap) {
+            int32_t *ost = sio.status, *oct = sio.cut_type;
+            double *oob = sio.obj, *odu = sio.dual, *orh = sio.rhs, *ocf = sio.coef, *ocrh = sio.cut_rhs,
+                   *ocrow = sio.cut_row, *oom = sio.obj_mean;
+            release(ost); release(oct); release(oob); release(odu); release(orh); release(ocf);
+            release(ocrh); release(ocrow); release(oom);
+        }
+        sio.status = st; sio.obj = ob; sio.dual = du; sio.rhs = rh; sio.coef = cf;
+        sio.cut_type = ct; sio.cut_rhs = crh; sio.cut_row = crow; sio.obj_mean = om;
+        int64_t *po;
+        if (!alloc(po, (size_t)cap + 1, "sub io")) return false;
+        if (d_spoff) release(d_spoff);
+        d_spoff = po;
+        sub_cap = cap;
+    }
+    if (total > sub_path_cap) {
+        size_t cap = std::max(total, 2 * sub_path_cap);
+        int16_t *pp;
+        if (!alloc(pp, cap, "sub paths")) return false;
+        if (d_spaths) release(d_spaths);
+        d_spaths = pp;
+        sub_path_cap = cap;
+    }
+    return true;
+}
+
+int sgufp_subproblem(sgufp_ctx *ctx, int n, const int64_t *path_off, const int16_t *paths, int32_t *type,
+                     double *rhs, double *rows, double *obj_mean) {
+    if (!ctx || n < 0 || (n && (!path_off || !paths))) return SGUFP_ERR_ARG;
+    if (n == 0) return SGUFP_OK;
+    for (int k = 0; k < n; k++)
+        if (path_off[k + 1] < path_off[k] || path_off[k + 1] - path_off[k] > ctx->net.L) {
+            ctx->err = "path longer than totalLayers";
+            return SGUFP_ERR_ARG;
+        }
+    const size_t total = (size_t)(path_off[n] - path_off[0]);
+    if (!ctx->sub_init() || !ctx->sub_grow(n, std::max<size_t>(total, 1))) return SGUFP_ERR_HIP;
+    std::vector<int64_t> off(path_off, path_off + n + 1);
+    for (auto &o : off) o -= path_off[0];
+    if (!ctx->upload(ctx->d_spoff, off.data(), off.size()) || !ctx->upload(ctx->d_spaths, paths + path_off[0], total))
         return SGUFP_ERR_HIP;
-    for (int c = 0; c < n_cuts; c++) (is_feasibility ? ctx->f_rows : ctx->o_rows).push_back(first + c);
-    ctx->n_rows += n_cuts;
-    ctx->order_dirty = true;
+    SubIO io = ctx->sio;
+    io.n_paths = n;
+    io.path_off = ctx->d_spoff;
+    io.paths = ctx->d_spaths;
+    if (!ctx->hip_ok(launch_subproblem(ctx->sn, io, ctx->stream), "subproblem launch")) return SGUFP_ERR_HIP;
+    ctx->sub_last_n = n;
+    const size_t stride = (size_t)ctx->net.n_slots + 1;
+    if ((type && !ctx->download(type, io.cut_type, n)) || (rhs && !ctx->download(rhs, io.cut_rhs, n)) ||
+        (rows && !ctx->download(rows, io.cut_row, (size_t)n * stride)) ||
+        (obj_mean && !ctx->download(obj_mean, io.obj_mean, n)) || !ctx->sync())
+        return SGUFP_ERR_HIP;
+    return SGUFP_OK;
+}
+
+int sgufp_subproblem_detail(sgufp_ctx *ctx, int32_t *status, double *objective, double *dual_objective) {
+    if (!ctx) return SGUFP_ERR_ARG;
+    const size_t cnt = (size_t)ctx->sub_last_n * ctx->net.S;
+    if ((status && !ctx->download(status, ctx->sio.status, cnt)) || (objective && !ctx->download(objective, ctx->sio.obj, cnt)) ||
+        (dual_objective && !ctx->download(dual_objective, ctx->sio.dual, cnt)) || !ctx->sync())
+        return SGUFP_ERR_HIP;
     return SGUFP_OK;
 }
 

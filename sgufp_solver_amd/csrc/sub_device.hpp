@@ -1,0 +1,53 @@
+// Device-side data of the scenario subproblem (GuroSolver::solveSubProblem,
+// /root/reference/grb.cpp:139-360), shared by sub_kernels.hip and capi.cpp.
+#pragma once
+
+#include <cstdint>
+
+#include "dd_device.hpp"
+
+namespace sgufp {
+
+// per (path, scenario) outcome
+enum SubStatus : int32_t {
+    kSubOptimal = 0,      // optimality-cut contribution written
+    kSubInfeasible = 1,   // feasibility ray written (grb.cpp:288-350)
+    kSubError = 2,        // invalid path (two in-arcs choosing one out-arc) or certificate failure
+};
+
+struct SubNet {
+    int n, m, S, L, n_slots;
+    const int32_t SGUFP_GBL *tail;       // [m]
+    const int32_t SGUFP_GBL *head;       // [m]
+    const uint8_t SGUFP_GBL *vbar;       // [n]
+    const uint8_t SGUFP_GBL *inner;      // [n] node has in- and out-arcs (conservation row, alpha)
+    const int32_t SGUFP_GBL *arc_layer;  // [m] DD layer of an arc into a V-bar node, else -1
+    const int32_t SGUFP_GBL *lb;         // [S][m]
+    const int32_t SGUFP_GBL *ub;         // [S][m]
+    const int32_t SGUFP_GBL *reward;     // [m] scenario-0 rewards (grb.cpp:53,71,89)
+    const int32_t SGUFP_GBL *in_off;     // [n+1]
+    const int32_t SGUFP_GBL *in_list;    // [m]
+    const int32_t SGUFP_GBL *out_off;    // [n+1]
+    const int32_t SGUFP_GBL *out_list;   // [m]
+    const int32_t SGUFP_GBL *slot_off;   // [L+1]
+    const int32_t SGUFP_GBL *slot_head;  // [n_slots]
+};
+
+struct SubIO {
+    int n_paths;
+    const int64_t SGUFP_GBL *path_off;   // [n_paths+1]
+    const int16_t SGUFP_GBL *paths;
+    // per (path, scenario)
+    int32_t SGUFP_GBL *status;           // [P*S]
+    double SGUFP_GBL *obj;               // [P*S] scenario objective (optimal scenarios)
+    double SGUFP_GBL *dual;              // [P*S] objective of the dual solution built (check)
+    double SGUFP_GBL *rhs;               // [P*S] RHS contribution (before the 1/S of the reference)
+    double SGUFP_GBL *coef;              // [P*S][n_slots] coefficient contributions
+    // per path
+    int32_t SGUFP_GBL *cut_type;         // [P] 0 optimality, 1 feasibility, -1 error
+    double SGUFP_GBL *cut_rhs;           // [P]
+    double SGUFP_GBL *cut_row;           // [P][n_slots+1] dense cut row (last slot 0)
+    double SGUFP_GBL *obj_mean;          // [P] sum_s obj_s / S (optimality)
+};
+
+}  // namespace sgufp

@@ -1,0 +1,608 @@
+// MI355X (gfx950) kernels for the scenario subproblem of SGUFP_Solver's exact leaves:
+// GuroSolver::solveSubProblem(path) (/root/reference/grb.cpp:139-360), which the reference
+// solves as one Gurobi LP per scenario (the dual of a flow problem, grb.cpp:42-136).
+//
+// One 64-lane wave per (path, scenario):
+//   1. y-bar from the path (grb.cpp:139-150): at every V-bar node q each incoming arc is
+//      matched to the out-arc its DD layer decided, or to nothing (-1).
+//   2. Contraction.  The primal of the reference's dual is max sum r x over the network
+//      with conservation at nodes that have in- and out-arcs, l <= x <= u, and at a
+//      V-bar node: matched pairs carry equal flow (lambda / mu rows), unmatched arcs carry
+//      none (sigma / phi rows).  Following the matching turns every arc into one "chain"
+//      through V-bar nodes; a chain from a non-V-bar tail to a non-V-bar head is one
+//      arc with bounds [max l, min u] and reward sum r, any other chain is fixed at 0.
+//   3. Max-reward flow on the contracted DAG (free supply at sources, free demand at
+//      sinks): successive shortest paths (Bellman-Ford in LDS over the residual graph,
+//      wave-parallel relaxation, 64-bit (cost, hops) keys so the predecessor graph of
+//      equal-cost paths has no cycles).  Lower bounds ride on a big-M reward; a lower
+//      bound left unmet at the end is primal infeasibility.
+//   4. An optimal dual of the reference formulation (alpha from shortest-path potentials
+//      of the final residual, beta / gamma from reduced costs, lambda / mu as the free
+//      transfers along matched pairs, sigma / phi on unmatched arcs), or, for an
+//      infeasible scenario, an unbounded dual ray (Farkas certificate).  From it the
+//      scenario's contribution to the cut, exactly as grb.cpp:236-281 / 288-350 assemble
+//      it.  All of it is integer arithmetic (integral data), written out as f64.
+// A second kernel reduces over scenarios per path in scenario order: the first infeasible
+// scenario's ray (feasibility cut), else the 1/S-weighted sum (optimality cut).
+//
+// Duals are not unique, so the cut coefficients differ from Gurobi's; what is pinned is
+// the scenario objective (== HiGHS on the reference formulation, tests/), that the cut is
+// tight at y-bar (RHS + coef.y-bar == mean objective) and valid for other y.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "sub_device.hpp"
+#include "wave.hpp"
+
+namespace sgufp {
+
+namespace {
+
+constexpr int64_t kInf = INT64_MAX / 4;
+constexpr int kHopBits = 16;
+constexpr int kMaxChain = 64;      // arcs per chain (V-bar nodes in a row + 1)
+
+struct SubLds {
+    LDS int32_t *dec;       // [m] decision at the head (out-arc id, -1 none, -2 head not V-bar)
+    LDS int32_t *chosen;    // [m] in-arc that chose this out-arc of a V-bar node, -1 none
+    LDS int32_t *ct_first;  // [m] first arc of chain k (chains indexed by start rank)
+    LDS int32_t *ct_t;      // [m] tail node (-1: chain starts at an unchosen V-bar out-arc)
+    LDS int32_t *ct_h;      // [m] head node (-1: chain ends at an unmatched V-bar in-arc)
+    LDS int32_t *ct_L, *ct_U, *ct_R, *ct_x;
+    LDS int64_t *key;       // [n+2] Bellman-Ford keys (cost << 16 | hops)
+    LDS int32_t *pred;      // [n+2]
+    LDS int64_t *alpha;     // [n+1] dual node potentials
+    LDS double *coef;       // [n_slots]
+    LDS int32_t *misc;      // [8] flags
+};
+
+__host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+__host__ __device__ inline size_t sub_lds_layout(int n, int m, int n_slots, size_t *off) {
+    size_t o = 0;
+    for (int k = 0; k < 9; k++) { off[k] = o; o = a16(o + (size_t)m * 4); }
+    off[9] = o; o = a16(o + (size_t)(n + 2) * 8);
+    off[10] = o; o = a16(o + (size_t)(n + 2) * 4);
+    off[11] = o; o = a16(o + (size_t)(n + 1) * 8);
+    off[12] = o; o = a16(o + (size_t)n_slots * 8);
+    off[13] = o; o = a16(o + 8 * 4);
+    return o;
+}
+
+__device__ inline bool is_src(const SubNet &N, int v) { return N.in_off[v + 1] == N.in_off[v]; }
+__device__ inline bool is_snk(const SubNet &N, int v) { return N.out_off[v + 1] == N.out_off[v]; }
+
+__device__ inline int slot_of(const SubNet &N, int layer, int j) {
+    for (int s = N.slot_off[layer]; s < N.slot_off[layer + 1]; s++)
+        if (N.slot_head[s] == j) return s;
+    return -1;
+}
+
+__device__ inline void lds_add(LDS double *p, double v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// ---------------------------------------------------------------------------------------
+// Bellman-Ford over the residual graph of the contracted network.
+//   SSP mode: shortest paths from Z_out (node n) to Z_in (node n+1) under the big-M costs;
+//             arcs Z_out -> source and sink -> Z_in are free and uncapacitated.
+//   POT mode: potentials; every node starts at 0 (virtual root), Z (node n) is tied to
+//             every source and sink by free arcs in both directions (alpha = 0 there);
+//             BIGM selects the big-M costs (dual ray) or the plain ones (optimal duals).
+enum BfMode { kSsp = 0, kPotPlain = 1, kPotBigM = 2 };
+
+template <typename F>
+__device__ inline void for_residual(const SubNet &N, const SubLds &W, int nct, int mode, int64_t M, F visit) {
+    // contracted arcs: code 2k (forward), 2k+1 (backward)
+    for (int k = lane(); k < nct; k += kWave) {
+        const int t = W.ct_t[k], h = W.ct_h[k];
+        if (t < 0 || h < 0) continue;
+        const int64_t x = W.ct_x[k], L = W.ct_L[k], U = W.ct_U[k], R = W.ct_R[k];
+        if (mode == kPotPlain) {
+            if (x < U) visit(t, h, -R, 2 * k);
+            if (x > L) visit(h, t, R, 2 * k + 1);
+        } else {
+            if (x < U) visit(t, h, -(R + (x < L ? M : 0)), 2 * k);
+            if (x > 0) visit(h, t, R + (x <= L ? M : 0), 2 * k + 1);
+        }
+    }
+    // Z arcs: code 2m + 2v (+1)
+    for (int v = lane(); v < N.n; v += kWave) {
+        if (N.inner[v]) continue;
+        const bool src = is_src(N, v), snk = is_snk(N, v);
+        if (src && snk) continue;
+        if (mode == kSsp) {
+            if (src) visit(N.n, v, 0, 2 * N.m + 2 * v);
+            if (snk) visit(v, N.n + 1, 0, 2 * N.m + 2 * v + 1);
+        } else {
+            visit(N.n, v, 0, 2 * N.m + 2 * v);
+            visit(v, N.n, 0, 2 * N.m + 2 * v + 1);
+        }
+    }
+}
+
+__device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, int mode, int64_t M) {
+    const int nn = N.n + 2;
+    for (int v = lane(); v < nn; v += kWave) {
+        W.key[v] = (mode == kSsp) ? (v == N.n ? 0 : kInf) : 0;
+        W.pred[v] = INT_MAX;
+    }
+    wave_lds_sync();
+    bool converged = false;
+    for (int it = 0; it < nn + 2; it++) {
+        uint32_t changed = 0;
+        for_residual(N, W, nct, mode, M, [&](int u, int v, int64_t w, int code) {
+            const int64_t ku = W.key[u];
+            if (ku >= kInf) return;
+            const int64_t nk = ku + (w << kHopBits) + 1;
+            if (nk < W.key[v]) {
+                __hip_atomic_fetch_min(&W.key[v], nk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                changed = 1;
+            }
+        });
+        wave_lds_sync();
+        if (!wave_or(changed)) { converged = true; break; }
+    }
+    if (mode != kSsp || !converged) return converged;
+    // predecessors: the smallest arc code among the tight arcs into each node
+    for_residual(N, W, nct, mode, M, [&](int u, int v, int64_t w, int code) {
+        const int64_t ku = W.key[u];
+        if (ku >= kInf) return;
+        if (ku + (w << kHopBits) + 1 == W.key[v])
+            __hip_atomic_fetch_min(&W.pred[v], code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    });
+    wave_lds_sync();
+    return true;
+}
+
+__device__ inline int64_t key_cost(int64_t k) { return k >> kHopBits; }
+
+// ---------------------------------------------------------------------------------------
+// Dual assembly for one chain a_1..a_k.  e_a = r_a - P_a - V_a is the arc's reduced reward
+// (gamma - beta); P_a = alpha(head) - alpha(tail) with alpha = 0 at free and V-bar nodes;
+// V_a collects lambda - mu (matched pairs, transfer t), sigma (unmatched in-arc of a V-bar
+// head), phi (unchosen out-arc of a V-bar tail).  Targets: a complete chain puts all of
+// E = sum r - alpha(h) + alpha(t) on its binding arc (min u if E > 0, max l if E < 0); a
+// chain fixed at 0 keeps e = 0 and lets sigma (broken end) or phi (broken start) absorb
+// the rest (e <= 0 there).  Ray mode uses r = 0 and the given targets.
+struct ChainOut {
+    int64_t rhs;     // sum (u gamma - l beta) + sum (u_iq lambda + u_qj mu)
+    int64_t obj;     // sum (u gamma - l beta): the dual objective at y-bar
+};
+
+__device__ inline void add_coef(const SubNet &N, const SubLds &W, int layer, int j, int64_t v) {
+    if (v == 0) return;
+    const int s = slot_of(N, layer, j);
+    if (s >= 0) lds_add(&W.coef[s], (double)v);
+}
+
+// sigma on in-arc a of V-bar node q: every (i, q, j) of q gets u_iq * sigma (grb.cpp:257-266)
+__device__ inline void add_sigma(const SubNet &N, const SubLds &W, int a, int64_t sig, int s) {
+    if (sig == 0) return;
+    const int q = N.head[a], layer = N.arc_layer[a];
+    const int64_t u = N.ub[(size_t)s * N.m + a];
+    for (int k = N.out_off[q]; k < N.out_off[q + 1]; k++) add_coef(N, W, layer, N.head[N.out_list[k]], u * sig);
+}
+// phi on out-arc b of V-bar node q: every (i, q, j) of q gets u_qj * phi (grb.cpp:268-277)
+__device__ inline void add_phi(const SubNet &N, const SubLds &W, int b, int64_t ph, int s) {
+    if (ph == 0) return;
+    const int q = N.tail[b], j = N.head[b];
+    const int64_t u = N.ub[(size_t)s * N.m + b];
+    for (int k = N.in_off[q]; k < N.in_off[q + 1]; k++) add_coef(N, W, N.arc_layer[N.in_list[k]], j, u * ph);
+}
+
+__device__ inline int64_t alpha_of(const SubNet &N, const SubLds &W, int v) {
+    return (v >= 0 && N.inner[v] && !N.vbar[v]) ? W.alpha[v] : 0;
+}
+
+// ray_mode: r = 0; e_target[m] given for every arc (only used when ray_mode)
+__device__ ChainOut assemble_chain(const SubNet &N, const SubLds &W, int k, int s, bool ray_mode, int ray_p,
+                                   int ray_q, bool &ok) {
+    ChainOut o{0, 0};
+    int arcs[kMaxChain];
+    int len = 0;
+    for (int a = W.ct_first[k]; a >= 0 && len < kMaxChain;) {
+        arcs[len++] = a;
+        if (!N.vbar[N.head[a]]) break;
+        a = W.dec[a];
+    }
+    if (len >= kMaxChain) { ok = false; return o; }
+    const int t = W.ct_t[k], h = W.ct_h[k];
+    const size_t so = (size_t)s * N.m;
+    auto rew = [&](int a) -> int64_t { return ray_mode ? 0 : (int64_t)N.reward[a]; };
+    auto cost = [&](int a, int64_t e) -> int64_t { return e >= 0 ? (int64_t)N.ub[so + a] * e : (int64_t)N.lb[so + a] * e; };
+    int64_t e[kMaxChain];
+    for (int i = 0; i < len; i++) e[i] = 0;
+    const bool complete = t >= 0 && h >= 0;
+    // prescribed targets: the chain that certifies infeasibility up front ((i) / (ii))
+    const bool prescribed = ray_mode && ray_p >= 0;
+    if (prescribed) {
+        for (int i = 0; i < len; i++) {
+            if (arcs[i] == ray_p) e[i] -= 1;   // beta = 1 on the max-l arc
+            if (arcs[i] == ray_q) e[i] += 1;   // gamma = 1 on the min-u arc
+        }
+    }
+    int64_t pair_t[kMaxChain];
+    if (complete) {
+        // E on the binding arc
+        int64_t E = -alpha_of(N, W, h) + alpha_of(N, W, t);
+        for (int i = 0; i < len; i++) E += rew(arcs[i]);
+        if (!prescribed) {
+            int bind = 0;
+            for (int i = 1; i < len; i++) {
+                const int64_t ui = N.ub[so + arcs[i]], ub = N.ub[so + arcs[bind]];
+                const int64_t li = N.lb[so + arcs[i]], lb = N.lb[so + arcs[bind]];
+                if (E > 0 ? ui < ub : li > lb) bind = i;
+            }
+            if (E != 0) e[bind] = E;
+        }
+        if (len == 1) {
+            o.obj += cost(arcs[0], e[0]);
+        } else {
+            int64_t tp = rew(arcs[0]) + alpha_of(N, W, t) - e[0];   // P_1 = -alpha(t)
+            pair_t[0] = tp;
+            for (int i = 1; i < len - 1; i++) {
+                tp = rew(arcs[i]) - e[i] + tp;
+                pair_t[i] = tp;
+            }
+            for (int i = 0; i < len; i++) o.obj += cost(arcs[i], e[i]);
+        }
+    } else if (h < 0) {
+        // broken end: forward transfers, sigma at the unmatched in-arc absorbs (e <= 0)
+        int64_t tp = 0;
+        for (int i = 0; i < len; i++) {
+            const int a = arcs[i];
+            const int64_t P = (i == 0) ? -alpha_of(N, W, t) : 0;
+            if (i < len - 1) {
+                tp = rew(a) - P - e[i] + tp;
+                pair_t[i] = tp;
+            } else {
+                const int64_t prev = (len >= 2) ? pair_t[len - 2] : 0;
+                const int64_t free_e = rew(a) - P + prev;     // e with sigma = 0
+                int64_t sig;
+                if (prescribed) sig = free_e - e[i];
+                else { sig = free_e > 0 ? free_e : 0; e[i] = free_e - sig; }
+                if (sig < 0) ok = false;
+                add_sigma(N, W, a, sig, s);
+            }
+            o.obj += cost(a, e[i]);
+        }
+    } else {
+        // broken start only: backward transfers, phi at the unchosen out-arc absorbs
+        int64_t tn = 0;   // transfer after the current arc
+        for (int i = len - 1; i >= 0; i--) {
+            const int a = arcs[i];
+            const int64_t P = (i == len - 1) ? alpha_of(N, W, h) : 0;
+            if (i > 0) {
+                // e_i = r_i - P_i - (-t_{i-1} + t_i)  ->  t_{i-1} = e_i - r_i + P_i + t_i
+                const int64_t tprev = e[i] - rew(a) + P + tn;
+                pair_t[i - 1] = tprev;
+                tn = tprev;
+            } else {
+                const int64_t t1 = (len >= 2) ? pair_t[0] : 0;
+                const int64_t free_e = rew(a) - P - t1;         // e with phi = 0
+                int64_t ph;
+                if (prescribed) ph = free_e - e[0];
+                else { ph = free_e > 0 ? free_e : 0; e[0] = free_e - ph; }
+                if (ph < 0) ok = false;
+                add_phi(N, W, a, ph, s);
+            }
+        }
+        for (int i = 0; i < len; i++) o.obj += cost(arcs[i], e[i]);
+    }
+    // matched pairs (a_i, a_{i+1}) at q = head(a_i): lambda = max(t, 0), mu = max(-t, 0)
+    for (int i = 0; i + 1 < len; i++) {
+        const int a = arcs[i], b = arcs[i + 1];
+        const int64_t tt = pair_t[i];
+        const int64_t lam = tt > 0 ? tt : 0, mu = tt < 0 ? -tt : 0;
+        const int64_t ua = N.ub[so + a], ubb = N.ub[so + b];
+        o.rhs += ua * lam + ubb * mu;
+        add_coef(N, W, N.arc_layer[a], N.head[b], -(ua * lam + ubb * mu));
+    }
+    o.rhs += o.obj;
+    return o;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
+    const int S = N.S;
+    const int p = blockIdx.x / S, s = blockIdx.x - p * S;
+    if (p >= io.n_paths) return;
+    size_t off[14];
+    sub_lds_layout(N.n, N.m, N.n_slots, off);
+    SubLds W;
+    W.dec = (LDS int32_t *)(smem + off[0]);
+    W.chosen = (LDS int32_t *)(smem + off[1]);
+    W.ct_first = (LDS int32_t *)(smem + off[2]);
+    W.ct_t = (LDS int32_t *)(smem + off[3]);
+    W.ct_h = (LDS int32_t *)(smem + off[4]);
+    W.ct_L = (LDS int32_t *)(smem + off[5]);
+    W.ct_U = (LDS int32_t *)(smem + off[6]);
+    W.ct_R = (LDS int32_t *)(smem + off[7]);
+    W.ct_x = (LDS int32_t *)(smem + off[8]);
+    W.key = (LDS int64_t *)(smem + off[9]);
+    W.pred = (LDS int32_t *)(smem + off[10]);
+    W.alpha = (LDS int64_t *)(smem + off[11]);
+    W.coef = (LDS double *)(smem + off[12]);
+    W.misc = (LDS int32_t *)(smem + off[13]);
+    const int n = N.n, m = N.m;
+    const size_t so = (size_t)s * m;
+    const int64_t poff = io.path_off[p], plen = io.path_off[p + 1] - poff;
+    const size_t b = (size_t)p * S + s;
+
+    // 1. decisions and matching
+    if (lane() < 8) W.misc[lane()] = 0;
+    for (int a = lane(); a < m; a += kWave) {
+        W.chosen[a] = -1;
+        const int q = N.head[a];
+        int d = -2;
+        if (N.vbar[q]) {
+            const int l = N.arc_layer[a];
+            d = (l >= 0 && l < plen) ? (int)io.paths[poff + l] : -1;
+            if (d < -1 || d >= m || (d >= 0 && N.tail[d] != q)) d = -3;   // not an out-arc of q
+        }
+        W.dec[a] = d;
+    }
+    for (int v = lane(); v < N.n_slots; v += kWave) W.coef[v] = 0.0;
+    wave_lds_sync();
+    for (int a = lane(); a < m; a += kWave) {
+        const int d = W.dec[a];
+        if (d == -3) W.misc[0] = 1;
+        if (d >= 0 && __hip_atomic_exchange(&W.chosen[d], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != -1)
+            W.misc[0] = 1;   // two in-arcs chose one out-arc: not a path of an exact DD
+    }
+    wave_lds_sync();
+
+    // 2. chains, indexed by the rank of their first arc
+    int nct = 0;
+    for (int base = 0; base < m; base += kWave) {
+        const int a = base + lane();
+        bool st = false;
+        if (a < m) st = !N.vbar[N.tail[a]] || W.chosen[a] < 0;
+        const uint32_t incl = wave_scan_incl(st ? 1u : 0u);
+        if (st) W.ct_first[nct + (int)incl - 1] = a;
+        nct += (int)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+    }
+    wave_lds_sync();
+    int first_bad = INT_MAX;   // first chain (rank) that makes the scenario infeasible up front
+    for (int k = lane(); k < nct; k += kWave) {
+        int a = W.ct_first[k];
+        const int t0 = N.tail[a];
+        int L = N.lb[so + a], U = N.ub[so + a], R = N.reward[a];
+        int h = -1, len = 1;
+        for (;;) {
+            const int q = N.head[a];
+            if (!N.vbar[q]) { h = q; break; }
+            const int d = W.dec[a];
+            if (d < 0) break;
+            a = d;
+            if (++len > kMaxChain) { W.misc[0] = 1; break; }
+            L = max(L, (int)N.lb[so + a]);
+            U = min(U, (int)N.ub[so + a]);
+            R += N.reward[a];
+        }
+        const int t = N.vbar[t0] ? -1 : t0;
+        W.ct_t[k] = t;
+        W.ct_h[k] = h;
+        W.ct_L[k] = L;
+        W.ct_U[k] = U;
+        W.ct_R[k] = R;
+        W.ct_x[k] = 0;
+        const bool complete = t >= 0 && h >= 0;
+        if ((complete && L > U) || (!complete && L > 0)) first_bad = min(first_bad, k);
+    }
+    first_bad = lane_reduce<1>(first_bad, [](int x, int y) { return x < y ? x : y; });
+    wave_lds_sync();
+    if (W.misc[0]) {
+        if (lane() == 0) { io.status[b] = kSubError; io.obj[b] = 0; io.dual[b] = 0; io.rhs[b] = 0; }
+        for (int v = lane(); v < N.n_slots; v += kWave) io.coef[b * N.n_slots + v] = 0.0;
+        return;
+    }
+
+    int status = kSubOptimal;
+    int64_t M = 1;
+    for (int k = lane(); k < nct; k += kWave) {
+        if (W.ct_t[k] >= 0 && W.ct_h[k] >= 0) {
+            const int64_t R = W.ct_R[k];
+            M += 2 * (R < 0 ? -R : R) * ((int64_t)W.ct_U[k] + 1);
+        }
+    }
+    M = lane_reduce<1>(M, [](int64_t x, int64_t y) { return x + y; }) - (kWave - 1);
+    int ray_chain = -1, ray_p = -1, ray_q = -1;
+    int64_t primal = 0;
+
+    if (first_bad != INT_MAX) {
+        // (i) a chain fixed at 0 with a positive lower bound, or (ii) a chain with max l > min u
+        status = kSubInfeasible;
+        ray_chain = first_bad;
+        const int k = first_bad;
+        int a = W.ct_first[k];
+        const bool complete = W.ct_t[k] >= 0 && W.ct_h[k] >= 0;
+        int bp = a, bq = a;
+        int64_t bl = N.lb[so + a], bu = N.ub[so + a];
+        for (int len = 0; len < kMaxChain; len++) {
+            const int64_t l = N.lb[so + a], u = N.ub[so + a];
+            if (l > bl) { bl = l; bp = a; }
+            if (u < bu) { bu = u; bq = a; }
+            if (!N.vbar[N.head[a]] || W.dec[a] < 0) break;
+            a = W.dec[a];
+        }
+        if (complete) { ray_p = bp; ray_q = bq; }
+        else { ray_p = bp; ray_q = -1; }
+        for (int v = lane(); v <= n; v += kWave) W.alpha[v] = 0;
+        wave_lds_sync();
+    } else {
+        // 3. successive shortest paths (max reward) from the sources to the sinks
+        int iters = 0;
+        for (;; iters++) {
+            if (!bellman_ford(N, W, nct, kSsp, M)) { status = kSubError; break; }
+            const int64_t kz = W.key[n + 1];
+            if (kz >= kInf || key_cost(kz) >= 0) break;
+            if (iters > 8 * m + 64) { status = kSubError; break; }
+            // bottleneck along the predecessor chain, then augment (lane 0 walks)
+            if (lane() == 0) {
+                int64_t delta = kInf;
+                int v = n + 1, steps = 0;
+                while (v != n && steps++ < n + 4) {
+                    const int code = W.pred[v];
+                    if (code == INT_MAX) break;
+                    if (code >= 2 * m) { v = (code & 1) ? (code - 2 * m - 1) / 2 : n; continue; }
+                    const int k = code >> 1;
+                    const int64_t x = W.ct_x[k], L = W.ct_L[k], U = W.ct_U[k];
+                    const int64_t cap = (code & 1) ? (x > L ? x - L : x) : (x < L ? L - x : U - x);
+                    delta = cap < delta ? cap : delta;
+                    v = (code & 1) ? W.ct_h[k] : W.ct_t[k];
+                }
+                if (v != n || delta <= 0 || delta >= kInf) W.misc[1] = 1;
+                else {
+                    v = n + 1;
+                    while (v != n) {
+                        const int code = W.pred[v];
+                        if (code >= 2 * m) { v = (code & 1) ? (code - 2 * m - 1) / 2 : n; continue; }
+                        const int k = code >> 1;
+                        if (code & 1) { W.ct_x[k] -= (int32_t)delta; v = W.ct_h[k]; }
+                        else { W.ct_x[k] += (int32_t)delta; v = W.ct_t[k]; }
+                    }
+                }
+            }
+            wave_lds_sync();
+            if (W.misc[1]) { status = kSubError; break; }
+        }
+        // lower bounds met?
+        int unmet = 0;
+        for (int k = lane(); k < nct; k += kWave) {
+            if (W.ct_t[k] >= 0 && W.ct_h[k] >= 0) {
+                if (W.ct_x[k] < W.ct_L[k]) unmet = 1;
+                primal += (int64_t)W.ct_R[k] * W.ct_x[k];
+            }
+        }
+        primal = lane_reduce<1>(primal, [](int64_t x, int64_t y) { return x + y; });
+        unmet = (int)wave_or((uint32_t)unmet);
+        if (status == kSubOptimal) {
+            // 4. potentials of the final residual: plain costs (optimal duals) or big-M
+            //    costs (their M-multiple is a dual ray, case (iii))
+            const int mode = unmet ? kPotBigM : kPotPlain;
+            if (unmet) status = kSubInfeasible;
+            if (!bellman_ford(N, W, nct, mode, M)) status = kSubError;
+            const int64_t dz = key_cost(W.key[n]);
+            for (int v = lane(); v < n; v += kWave) {
+                int64_t d = key_cost(W.key[v]) - dz;
+                int64_t al;
+                if (mode == kPotPlain) al = -d;
+                else {
+                    const int64_t r = (d >= 0 ? d + M / 2 : d - M / 2) / M;   // round(d / M)
+                    al = -r;
+                }
+                W.alpha[v] = (N.inner[v] && !N.vbar[v]) ? al : 0;
+            }
+            wave_lds_sync();
+        }
+    }
+
+    // 5. dual solution / ray and the scenario's cut contribution
+    int64_t rhs = 0, dual = 0;
+    bool ok = true;
+    if (status != kSubError) {
+        const bool ray = status == kSubInfeasible;
+        for (int k = lane(); k < nct; k += kWave) {
+            if (ray && ray_chain >= 0 && k != ray_chain) continue;   // (i)/(ii): only the bad chain
+            ChainOut c = assemble_chain(N, W, k, s, ray, (k == ray_chain) ? ray_p : -1,
+                                        (k == ray_chain) ? ray_q : -1, ok);
+            rhs += c.rhs;
+            dual += c.obj;
+        }
+        rhs = lane_reduce<1>(rhs, [](int64_t x, int64_t y) { return x + y; });
+        dual = lane_reduce<1>(dual, [](int64_t x, int64_t y) { return x + y; });
+        ok = wave_or(ok ? 0u : 1u) == 0;
+        if (ray && ray_chain >= 0 && ray_p >= 0 && ray_p == ray_q) {
+            // single arc with l > u: beta = gamma = 1 on it
+            const int64_t d0 = (int64_t)N.ub[so + ray_p] - N.lb[so + ray_p];
+            rhs += d0;
+            dual += d0;
+        }
+        if (!ok || (ray ? dual >= 0 : dual != primal)) status = kSubError;
+    }
+    wave_lds_sync();
+    if (lane() == 0) {
+        io.status[b] = status;
+        io.obj[b] = (double)primal;
+        io.dual[b] = (double)dual;
+        io.rhs[b] = (double)rhs;
+    }
+    for (int v = lane(); v < N.n_slots; v += kWave) io.coef[b * N.n_slots + v] = W.coef[v];
+}
+
+// Per path, in scenario order: the first infeasible scenario's ray (grb.cpp:288-350,
+// rhs and coefficients reset, no 1/S), else sum_s contribution / S (grb.cpp:236-281).
+__global__ void __launch_bounds__(256) k_sub_reduce(SubNet N, SubIO io) {
+    const int p = blockIdx.x;
+    if (p >= io.n_paths) return;
+    const int S = N.S;
+    __shared__ int first_inf, any_err;
+    if (threadIdx.x == 0) { first_inf = INT_MAX; any_err = 0; }
+    __syncthreads();
+    for (int s = threadIdx.x; s < S; s += blockDim.x) {
+        const int st = io.status[(size_t)p * S + s];
+        if (st == kSubInfeasible) atomicMin(&first_inf, s);
+        if (st == kSubError) atomicOr(&any_err, 1);
+    }
+    __syncthreads();
+    const int stride = N.n_slots + 1;
+    // a scenario before the first infeasible one that failed poisons the path
+    bool err = false;
+    if (any_err) {
+        for (int s = 0; s < S && s <= first_inf && s < S; s++)
+            if (io.status[(size_t)p * S + s] == kSubError) { err = true; break; }
+    }
+    if (err) {
+        if (threadIdx.x == 0) { io.cut_type[p] = -1; io.cut_rhs[p] = 0; io.obj_mean[p] = 0; }
+        for (int v = threadIdx.x; v < stride; v += blockDim.x) io.cut_row[(size_t)p * stride + v] = 0.0;
+        return;
+    }
+    if (first_inf != INT_MAX) {
+        const size_t b = (size_t)p * S + first_inf;
+        if (threadIdx.x == 0) { io.cut_type[p] = 1; io.cut_rhs[p] = io.rhs[b]; io.obj_mean[p] = 0; }
+        for (int v = threadIdx.x; v < stride; v += blockDim.x)
+            io.cut_row[(size_t)p * stride + v] = v < N.n_slots ? io.coef[b * N.n_slots + v] : 0.0;
+        return;
+    }
+    const double inv = (double)S;
+    for (int v = threadIdx.x; v < stride; v += blockDim.x) {
+        double acc = 0.0;
+        if (v < N.n_slots)
+            for (int s = 0; s < S; s++) acc += io.coef[((size_t)p * S + s) * N.n_slots + v] / inv;
+        io.cut_row[(size_t)p * stride + v] = acc;
+    }
+    if (threadIdx.x == 0) {
+        double r = 0.0, o = 0.0;
+        for (int s = 0; s < S; s++) {
+            r += io.rhs[(size_t)p * S + s] / inv;
+            o += io.obj[(size_t)p * S + s] / inv;
+        }
+        io.cut_type[p] = 0;
+        io.cut_rhs[p] = r;
+        io.obj_mean[p] = o;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+size_t sub_lds_bytes(int n, int m, int n_slots) {
+    size_t off[14];
+    return sub_lds_layout(n, m, n_slots, off);
+}
+
+hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st) {
+    if (io.n_paths <= 0) return hipSuccess;
+    const size_t lds = sub_lds_bytes(N.n, N.m, N.n_slots);
+    hipLaunchKernelGGL(k_sub_scenario, dim3((unsigned)io.n_paths * N.S), dim3(kWave), lds, st, N, io);
+    hipLaunchKernelGGL(k_sub_reduce, dim3((unsigned)io.n_paths), dim3(256), 0, st, N, io);
+    return hipGetLastError();
+}
+
+}  // namespace sgufp

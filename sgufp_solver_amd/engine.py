@@ -27,7 +27,8 @@ EXPORTS = [
     "sgufp_batch_sync", "sgufp_batch_results", "sgufp_batch_children_size", "sgufp_batch_children",
     "sgufp_batch_paths", "sgufp_batch_stats", "sgufp_batch_refine", "sgufp_set_timing",
     "sgufp_last_timing", "sgufp_probe_network", "sgufp_batch_debug",
-    "sgufp_batch_phases",
+    "sgufp_batch_phases", "sgufp_subproblem", "sgufp_subproblem_detail", "sgufp_slot_keys",
+    "sgufp_cuts_append_rows",
 ]
 
 
@@ -76,6 +77,10 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.sgufp_probe_network.argtypes = [C.c_char_p, P, P, C.c_int32, P, P]
     lib.sgufp_batch_debug.argtypes = [P, P, P]
     lib.sgufp_batch_phases.argtypes = [P, P]
+    lib.sgufp_subproblem.argtypes = [P, C.c_int, P, P, P, P, P, P]
+    lib.sgufp_subproblem_detail.argtypes = [P, P, P, P]
+    lib.sgufp_slot_keys.argtypes = [P, P]
+    lib.sgufp_cuts_append_rows.argtypes = [P, C.c_int, C.c_int, P, P]
     _lib = lib
     return lib
 
@@ -328,6 +333,46 @@ class Engine:
         fe = np.asarray(is_feas, dtype=np.uint8)
         ci = np.asarray(cut_index, dtype=np.int32)
         self._check(self.lib.sgufp_batch_refine(self.ctx, len(ni), _ptr(ni), _ptr(fe), _ptr(ci), C.c_double(incumbent)))
+
+    # -- scenario subproblem ---------------------------------------------------
+    def slot_keys(self) -> np.ndarray:
+        keys = np.zeros(max(self.info.n_slots, 1), dtype=np.uint64)
+        self._check(self.lib.sgufp_slot_keys(self.ctx, _ptr(keys)))
+        return keys[:self.info.n_slots]
+
+    def subproblem(self, paths: Sequence[Sequence[int]]):
+        """GuroSolver::solveSubProblem for each path on the device.
+
+        Returns (type[n], rhs[n], rows[n, n_slots + 1], obj_mean[n]); type 0 optimality,
+        1 feasibility, -1 error."""
+        n = len(paths)
+        off = np.zeros(n + 1, dtype=np.int64)
+        for k, p in enumerate(paths):
+            off[k + 1] = off[k] + len(p)
+        flat = np.concatenate([np.asarray(p, dtype=np.int16) for p in paths]) if n else np.zeros(1, np.int16)
+        if flat.size == 0:
+            flat = np.zeros(1, np.int16)
+        typ = np.zeros(max(n, 1), dtype=np.int32)
+        rhs = np.zeros(max(n, 1), dtype=np.float64)
+        rows = np.zeros((max(n, 1), self.info.n_slots + 1), dtype=np.float64)
+        obj = np.zeros(max(n, 1), dtype=np.float64)
+        self._check(self.lib.sgufp_subproblem(self.ctx, n, _ptr(off), _ptr(flat), _ptr(typ), _ptr(rhs), _ptr(rows),
+                                              _ptr(obj)))
+        return typ[:n], rhs[:n], rows[:n], obj[:n]
+
+    def subproblem_detail(self, n: int):
+        """Per (path, scenario) status / primal objective / dual objective of the last call."""
+        S = self.info.scenarios
+        st = np.zeros(max(n * S, 1), dtype=np.int32)
+        ob = np.zeros(max(n * S, 1), dtype=np.float64)
+        du = np.zeros(max(n * S, 1), dtype=np.float64)
+        self._check(self.lib.sgufp_subproblem_detail(self.ctx, _ptr(st), _ptr(ob), _ptr(du)))
+        return st[:n * S].reshape(n, S), ob[:n * S].reshape(n, S), du[:n * S].reshape(n, S)
+
+    def add_cut_rows(self, is_feas: int, rhs: np.ndarray, rows: np.ndarray):
+        rhs = np.ascontiguousarray(rhs, dtype=np.float64)
+        rows = np.ascontiguousarray(rows, dtype=np.float64)
+        self._check(self.lib.sgufp_cuts_append_rows(self.ctx, int(is_feas), len(rhs), _ptr(rhs), _ptr(rows)))
 
     # -- convenience: NodeExplorer::process for a list of nodes ----------------
     def relax(self, nodes: Sequence[NodeRecord], incumbent: float) -> List[RelaxResult]:
