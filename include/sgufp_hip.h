@@ -19,6 +19,12 @@
  *   sgufp_batch_refine
  *       the exact-DD refinement step of process: apply the cut the subproblem just
  *       produced and return the next argmax path        NodeExplorer.cpp:946-969
+ *   sgufp_subproblem
+ *       GuroSolver::solveSubProblem(const vector<int16_t>&) grb.h:75, grb.cpp:139-360
+ *   sgufp_frontier_* + sgufp_bnb_step
+ *       the open-node queues and the worker loop of Inavap::DDSolver
+ *       (lf_queue lock_free_queue.h:24-165, Worker::startWorker DDSolver.cpp:658-776,
+ *       Master::processNodes :556-579), as a device-resident stack and batched rounds
  *
  * Conventions: functions return SGUFP_OK (0) or a negative SGUFP_ERR_* code; the
  * caller owns every host buffer; a context is driven by one host thread at a time and
@@ -51,6 +57,7 @@ typedef struct sgufp_ctx sgufp_ctx;
 #define SGUFP_PRUNED_BY_FEASIBILITY_CUT 1
 #define SGUFP_PRUNED_BY_OPTIMALITY_CUT 2
 #define SGUFP_NEEDS_SUBPROBLEM 3
+#define SGUFP_PRUNED_BY_BOUND 4   /* B&B rounds only: ub <= zOpt before processing (DDSolver.cpp:707-711) */
 #define SGUFP_NODE_ERR_RECORD 16
 #define SGUFP_NODE_ERR_CAPACITY 17
 #define SGUFP_NODE_ERR_CUTSET 18
@@ -145,6 +152,51 @@ int sgufp_slot_keys(const sgufp_ctx *ctx, uint64_t *keys);
 /* Append cuts given as dense rows (n_slots + 1 doubles each, as sgufp_subproblem returns
  * them) -- the device-side counterpart of Container::add (Cut.h:461-465). */
 int sgufp_cuts_append_rows(sgufp_ctx *ctx, int is_feasibility, int n_cuts, const double *rhs, const double *rows);
+
+/* -- batched branch-and-bound (Inavap::DDSolver, DDSolver.cpp:556-846) ------------------
+ * The frontier is a LIFO stack of open-node records in HBM.  sgufp_bnb_step pops up to
+ * max_nodes (<= max_batch; <= 0: max_batch) records from the top and does for all of them
+ * what a worker does for one popped node: skip it if ub <= *incumbent (DDSolver.cpp:707),
+ * NodeExplorer::process it against the current pools (exact DDs run their refinement loop
+ * with the device subproblem, new cuts are appended to the pools: Container::add), raise
+ * *incumbent to the best closed exact bound (CAS-max, :723-731), and push the cutset
+ * children of parents with ub > *incumbent (:744-748).  Returns SGUFP_ERR_STATE if any
+ * record fails (node status >= 16) or a subproblem fails; sgufp_last_error says which. */
+typedef struct {
+    int64_t popped;              /* records taken from the frontier */
+    int64_t relaxed;             /* NodeExplorer::process calls (popped - pruned_bound) */
+    int64_t pruned_bound;
+    int64_t pruned_feasibility;
+    int64_t pruned_optimality;
+    int64_t exact;               /* exact DDs (refinement loop entered) */
+    int64_t exact_closed;        /* exact DDs that returned {ub, ub} (incumbent candidates) */
+    int64_t subproblems;         /* paths sent to the scenario subproblem */
+    int64_t new_feasibility_cuts;
+    int64_t new_optimality_cuts;
+    int64_t children;            /* cutset children produced */
+    int64_t pushed;              /* children pushed (parent ub > incumbent) */
+    int64_t frontier;            /* frontier size after the round */
+    int64_t dd_nodes, dd_arcs, sweeps;   /* sums over the relaxed records */
+    int32_t refine_iters;
+    int32_t improved;            /* 1 if *incumbent rose */
+    double ms_relax;             /* k_relax time of the round (sgufp_set_timing) */
+} sgufp_bnb_stats;
+
+int sgufp_frontier_clear(sgufp_ctx *ctx);
+int sgufp_frontier_size(const sgufp_ctx *ctx, int64_t *n, int64_t *sol_entries);
+/* Push n host records on top of the stack (the last record ends on top). */
+int sgufp_frontier_push(sgufp_ctx *ctx, int n, const uint16_t *gl, const double *lb, const double *ub,
+                        const int64_t *states_off, const int16_t *states, const int64_t *sol_off, const int16_t *sol);
+/* Remove n records from the top (from_bottom = 0) or the bottom (oldest, from_bottom = 1:
+ * work stealing, cf. lf_queue::m_pop) and return them as host records, in stack order.
+ * sgufp_frontier_take_size gives the states / solution entries they need. */
+int sgufp_frontier_take_size(sgufp_ctx *ctx, int n, int from_bottom, int64_t *n_states, int64_t *n_sol);
+int sgufp_frontier_take(sgufp_ctx *ctx, int n, int from_bottom, uint16_t *gl, double *lb, double *ub,
+                        int64_t *states_off, int16_t *states, int64_t *sol_off, int16_t *sol);
+int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_stats *stats);
+/* Read back pool cuts [first, first + count) of one list (insertion order) as dense rows,
+ * e.g. to all-gather the cuts a round produced to the other frontier shards. */
+int sgufp_cuts_rows(sgufp_ctx *ctx, int is_feasibility, int first, int count, double *rhs, double *rows);
 
 /* -- timing (hipEvents on the ctx stream around each kernel of the last relax) -- */
 int sgufp_set_timing(sgufp_ctx *ctx, int enabled);

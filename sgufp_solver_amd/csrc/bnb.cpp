@@ -1,0 +1,390 @@
+// Batched branch-and-bound rounds on the device: the replacement of the reference's
+// DDSolver master/worker loop (DDSolver.cpp:556-846) around NodeExplorer::process
+// (NodeExplorer.cpp:915-986), with the open-node frontier resident in HBM.
+//
+// One round (sgufp_bnb_step) = what the reference's workers do for a batch of popped nodes:
+//   1. pop the top `b` records of the frontier stack (LIFO like lf_queue::pop);
+//   2. prune records with ub <= zOpt unprocessed (DDSolver.cpp:707-711) -- inside k_relax;
+//   3. process every other record against the current pools and zOpt (k_relax + k_emit);
+//   4. exact DDs run the refinement loop of NodeExplorer.cpp:946-969: argmax path, stop when
+//      the path was seen ({ub, ub}), else the device scenario subproblem, the new cut is
+//      appended to the global pool (Container::add) and applied to that DD (k_refine);
+//   5. incumbent = max(zOpt, lb of closed exact DDs)  (the CAS at DDSolver.cpp:723-731);
+//   6. cutset children of parents with ub > zOpt are pushed (DDSolver.cpp:744-748),
+//      compacted from the emit buffers onto the stack where the popped batch was.
+// Records processed in one round all see the same zOpt and pools, as concurrent workers
+// of the reference may.  Children of a parent keep the reference's cutset order; parents
+// keep their frontier order, so the top of the stack is the last parent's first child.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "ctx.hpp"
+
+void sgufp_ctx::decode_states(const uint16_t *gl, const uint32_t *mask, size_t count, int64_t *states_off,
+                              int16_t *states) const {
+    int64_t ss = 0;
+    for (size_t c = 0; c < count; c++) {
+        if (states_off) states_off[c] = ss;
+        const int u = net.layer_universe[gl[c]];
+        for (uint32_t m = mask[c]; m; m &= m - 1) {
+            if (states) states[ss] = net.sets[u][__builtin_ctz(m)];
+            ss++;
+        }
+    }
+    if (states_off) states_off[count] = ss;
+}
+
+bool sgufp_ctx::frontier_reserve(int64_t entries, size_t sol_entries) {
+    if (entries > fr_cap) {
+        const int64_t cap = std::max<int64_t>(entries, std::max<int64_t>(2 * fr_cap, 4096));
+        FrontierDev f{};
+        if (!alloc(f.gl, cap, "frontier") || !alloc(f.lb, cap, "frontier") || !alloc(f.ub, cap, "frontier") ||
+            !alloc(f.mask, cap, "frontier") || !alloc(f.valid, cap, "frontier") ||
+            !alloc(f.sol_off, cap, "frontier") || !alloc(f.sol_len, cap, "frontier"))
+            return false;
+        const size_t k = (size_t)fr_n;
+        if (k && (!hip_ok(hipMemcpyAsync(f.gl, fr.gl, k * 2, hipMemcpyDeviceToDevice, stream), "D2D") ||
+                  !hip_ok(hipMemcpyAsync(f.lb, fr.lb, k * 8, hipMemcpyDeviceToDevice, stream), "D2D") ||
+                  !hip_ok(hipMemcpyAsync(f.ub, fr.ub, k * 8, hipMemcpyDeviceToDevice, stream), "D2D") ||
+                  !hip_ok(hipMemcpyAsync(f.mask, fr.mask, k * 4, hipMemcpyDeviceToDevice, stream), "D2D") ||
+                  !hip_ok(hipMemcpyAsync(f.valid, fr.valid, k, hipMemcpyDeviceToDevice, stream), "D2D") ||
+                  !hip_ok(hipMemcpyAsync(f.sol_off, fr.sol_off, k * 8, hipMemcpyDeviceToDevice, stream), "D2D") ||
+                  !hip_ok(hipMemcpyAsync(f.sol_len, fr.sol_len, k * 2, hipMemcpyDeviceToDevice, stream), "D2D")))
+            return false;
+        if (!sync()) return false;
+        release(fr.gl); release(fr.lb); release(fr.ub); release(fr.mask); release(fr.valid);
+        release(fr.sol_off); release(fr.sol_len);
+        f.sol = fr.sol;
+        fr = f;
+        fr_cap = cap;
+    }
+    if (sol_entries > fr_sol_cap) {
+        const size_t cap = std::max(sol_entries, std::max<size_t>(2 * fr_sol_cap, 1 << 20));
+        int16_t *s = nullptr;
+        if (!alloc(s, cap, "frontier sol")) return false;
+        if (fr_sol_top && !hip_ok(hipMemcpyAsync(s, fr.sol, (size_t)fr_sol_top * 2, hipMemcpyDeviceToDevice, stream), "D2D"))
+            return false;
+        if (!sync()) return false;
+        release(fr.sol);
+        fr.sol = s;
+        fr_sol_cap = cap;
+    }
+    return true;
+}
+
+extern "C" {
+
+int sgufp_frontier_clear(sgufp_ctx *ctx) {
+    if (!ctx) return SGUFP_ERR_ARG;
+    ctx->fr_n = 0;
+    ctx->fr_sol_top = 0;
+    return SGUFP_OK;
+}
+
+int sgufp_frontier_size(const sgufp_ctx *ctx, int64_t *n, int64_t *sol_entries) {
+    if (!ctx) return SGUFP_ERR_ARG;
+    if (n) *n = ctx->fr_n;
+    if (sol_entries) *sol_entries = ctx->fr_sol_top;
+    return SGUFP_OK;
+}
+
+int sgufp_frontier_push(sgufp_ctx *ctx, int n, const uint16_t *gl, const double *lb, const double *ub,
+                        const int64_t *states_off, const int16_t *states, const int64_t *sol_off, const int16_t *sol) {
+    if (!ctx || n < 0 || (n && (!gl || !lb || !ub || !states_off || !sol_off))) return SGUFP_ERR_ARG;
+    if (n == 0) return SGUFP_OK;
+    EncodedRecords e;
+    ctx->encode_records(n, gl, states_off, states, sol_off, sol, e);
+    const int64_t base = ctx->fr_n;
+    const int64_t sbase = ctx->fr_sol_top;
+    if (!ctx->frontier_reserve(base + n, (size_t)sbase + e.sols.size())) return SGUFP_ERR_HIP;
+    for (auto &o : e.soff) o += sbase;
+    FrontierDev &f = ctx->fr;
+    if (!ctx->upload(f.gl + base, gl, n) || !ctx->upload(f.lb + base, lb, n) || !ctx->upload(f.ub + base, ub, n) ||
+        !ctx->upload(f.mask + base, e.mask.data(), n) || !ctx->upload(f.valid + base, e.valid.data(), n) ||
+        !ctx->upload(f.sol_off + base, e.soff.data(), n) || !ctx->upload(f.sol_len + base, e.slen.data(), n) ||
+        !ctx->upload(f.sol + sbase, e.sols.data(), e.sols.size()) || !ctx->sync())
+        return SGUFP_ERR_HIP;
+    ctx->fr_n += n;
+    ctx->fr_sol_top += (int64_t)e.sols.size();
+    return SGUFP_OK;
+}
+
+int sgufp_frontier_take_size(sgufp_ctx *ctx, int n, int from_bottom, int64_t *n_states, int64_t *n_sol) {
+    if (!ctx || n < 0 || n > ctx->fr_n) return SGUFP_ERR_ARG;
+    const int64_t lo = from_bottom ? 0 : ctx->fr_n - n;
+    std::vector<uint32_t> mask(n);
+    std::vector<uint16_t> len(n);
+    if (!ctx->download(mask.data(), ctx->fr.mask + lo, n) || !ctx->download(len.data(), ctx->fr.sol_len + lo, n) ||
+        !ctx->sync())
+        return SGUFP_ERR_HIP;
+    int64_t ns = 0, nl = 0;
+    for (int k = 0; k < n; k++) {
+        ns += __builtin_popcount(mask[k]);
+        nl += len[k];
+    }
+    if (n_states) *n_states = ns;
+    if (n_sol) *n_sol = nl;
+    return SGUFP_OK;
+}
+
+int sgufp_frontier_take(sgufp_ctx *ctx, int n, int from_bottom, uint16_t *gl, double *lb, double *ub,
+                        int64_t *states_off, int16_t *states, int64_t *sol_off, int16_t *sol) {
+    if (!ctx || n < 0 || n > ctx->fr_n) return SGUFP_ERR_ARG;
+    if (n == 0) {
+        if (states_off) states_off[0] = 0;
+        if (sol_off) sol_off[0] = 0;
+        return SGUFP_OK;
+    }
+    FrontierDev &f = ctx->fr;
+    const int64_t total = ctx->fr_n;
+    const int64_t lo = from_bottom ? 0 : total - n;
+    std::vector<uint16_t> g(n), len(n);
+    std::vector<double> l(n), u(n);
+    std::vector<uint32_t> mask(n);
+    std::vector<int64_t> so(n + 1);
+    if (!ctx->download(g.data(), f.gl + lo, n) || !ctx->download(l.data(), f.lb + lo, n) ||
+        !ctx->download(u.data(), f.ub + lo, n) || !ctx->download(mask.data(), f.mask + lo, n) ||
+        !ctx->download(len.data(), f.sol_len + lo, n) || !ctx->download(so.data(), f.sol_off + lo, n) || !ctx->sync())
+        return SGUFP_ERR_HIP;
+    // arena span of the taken records (offsets increase with the entry index)
+    int64_t s_hi = ctx->fr_sol_top;
+    if (from_bottom && n < total) {
+        if (!ctx->download(&s_hi, f.sol_off + n, 1) || !ctx->sync()) return SGUFP_ERR_HIP;
+    }
+    const int64_t s_lo = so[0];
+    std::vector<int16_t> arena((size_t)(s_hi - s_lo));
+    if (!ctx->download(arena.data(), f.sol + s_lo, arena.size()) || !ctx->sync()) return SGUFP_ERR_HIP;
+    if (gl) std::copy(g.begin(), g.end(), gl);
+    if (lb) std::copy(l.begin(), l.end(), lb);
+    if (ub) std::copy(u.begin(), u.end(), ub);
+    ctx->decode_states(g.data(), mask.data(), (size_t)n, states_off, states);
+    int64_t o = 0;
+    for (int k = 0; k < n; k++) {
+        if (sol_off) sol_off[k] = o;
+        if (sol) std::memcpy(sol + o, arena.data() + (so[k] - s_lo), len[k] * sizeof(int16_t));
+        o += len[k];
+    }
+    if (sol_off) sol_off[n] = o;
+    if (!from_bottom || n == total) {
+        ctx->fr_n -= n;
+        ctx->fr_sol_top = ctx->fr_n ? s_lo : 0;
+        return SGUFP_OK;
+    }
+    // from the bottom: move the remaining entries down (through a bounce buffer, the ranges overlap)
+    const size_t rest = (size_t)(total - n);
+    const size_t srest = (size_t)(ctx->fr_sol_top - s_hi);
+    std::vector<int64_t> soff(rest);
+    if (!ctx->download(soff.data(), f.sol_off + n, rest) || !ctx->sync()) return SGUFP_ERR_HIP;
+    for (auto &x : soff) x -= s_hi;
+    void *tmp = nullptr;
+    const size_t tbytes = std::max(rest * 8, srest * 2);
+    if (!ctx->hip_ok(hipMalloc(&tmp, std::max<size_t>(tbytes, 8)), "bounce")) return SGUFP_ERR_HIP;
+    auto move = [&](void *dst, const void *src, size_t bytes) {
+        return ctx->hip_ok(hipMemcpyAsync(tmp, src, bytes, hipMemcpyDeviceToDevice, ctx->stream), "D2D") &&
+               ctx->hip_ok(hipMemcpyAsync(dst, tmp, bytes, hipMemcpyDeviceToDevice, ctx->stream), "D2D");
+    };
+    bool ok = move(f.gl, f.gl + n, rest * 2) && move(f.lb, f.lb + n, rest * 8) && move(f.ub, f.ub + n, rest * 8) &&
+              move(f.mask, f.mask + n, rest * 4) && move(f.valid, f.valid + n, rest) &&
+              move(f.sol_len, f.sol_len + n, rest * 2) && (srest == 0 || move(f.sol, f.sol + s_hi, srest * 2)) &&
+              ctx->upload(f.sol_off, soff.data(), rest) && ctx->sync();
+    (void)hipFree(tmp);
+    if (!ok) return SGUFP_ERR_HIP;
+    ctx->fr_n = (int64_t)rest;
+    ctx->fr_sol_top = (int64_t)srest;
+    return SGUFP_OK;
+}
+
+int sgufp_cuts_rows(sgufp_ctx *ctx, int is_feasibility, int first, int count, double *rhs, double *rows) {
+    if (!ctx || first < 0 || count < 0) return SGUFP_ERR_ARG;
+    const auto &v = is_feasibility ? ctx->f_rows : ctx->o_rows;
+    if (first + count > (int)v.size()) return SGUFP_ERR_ARG;
+    const size_t stride = (size_t)ctx->net.n_slots + 1;
+    for (int c = 0; c < count; c++) {
+        const int r = v[first + c];
+        if ((rhs && !ctx->download(rhs + c, ctx->d_rhs + r, 1)) ||
+            (rows && !ctx->download(rows + (size_t)c * stride, ctx->d_rows + (size_t)r * stride, stride)))
+            return SGUFP_ERR_HIP;
+    }
+    return ctx->sync() ? SGUFP_OK : SGUFP_ERR_HIP;
+}
+
+int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_stats *stats) {
+    if (!ctx || !incumbent) return SGUFP_ERR_ARG;
+    sgufp_bnb_stats S{};
+    const double z = *incumbent;
+    const int64_t T = ctx->fr_n;
+    if (T == 0) {
+        if (stats) *stats = S;
+        return SGUFP_OK;
+    }
+    int b = ctx->max_batch;
+    if (max_nodes > 0) b = std::min(b, max_nodes);
+    b = (int)std::min<int64_t>(b, T);
+    const int64_t base = T - b;
+    S.popped = b;
+
+    // 1-3: relax the top of the stack in place
+    ctx->n = b;
+    ctx->cur = ctx->frontier_slice(base, b);
+    if (!ctx->relax_current(z)) return SGUFP_ERR_HIP;
+    std::vector<int32_t> st(b);
+    std::vector<double> ub(b), lbv(b, -__DBL_MAX__);
+    std::vector<uint32_t> nch(b), need(b), dn(b), da(b), sw(b);
+    std::vector<uint64_t> coff(b + 1), soff(b + 1);
+    int64_t sol_start = 0;
+    BatchOut &o = ctx->out;
+    if (!ctx->download(st.data(), o.status, b) || !ctx->download(ub.data(), o.ub, b) ||
+        !ctx->download(nch.data(), o.nchild, b) || !ctx->download(need.data(), o.sol_need, b) ||
+        !ctx->download(coff.data(), ctx->d_coff, b + 1) || !ctx->download(soff.data(), ctx->d_soff, b + 1) ||
+        !ctx->download(dn.data(), o.dd_nodes, b) || !ctx->download(da.data(), o.dd_arcs, b) ||
+        !ctx->download(sw.data(), o.sweeps, b) || !ctx->download(&sol_start, ctx->fr.sol_off + base, 1) ||
+        !ctx->sync())
+        return SGUFP_ERR_HIP;
+    if (ctx->timing) hipEventElapsedTime(&ctx->ms_relax, ctx->ev[0], ctx->ev[1]);
+    S.ms_relax = ctx->timing ? ctx->ms_relax : 0.0;
+    std::vector<int> act;
+    for (int k = 0; k < b; k++) {
+        switch (st[k]) {
+            case SGUFP_PRUNED_BY_BOUND: S.pruned_bound++; continue;
+            case SGUFP_PRUNED_BY_FEASIBILITY_CUT: S.pruned_feasibility++; break;
+            case SGUFP_PRUNED_BY_OPTIMALITY_CUT: S.pruned_optimality++; break;
+            case SGUFP_NEEDS_SUBPROBLEM: act.push_back(k); break;
+            case SGUFP_SUCCESS: break;
+            default: {
+                char msg[128];
+                std::snprintf(msg, sizeof msg, "B&B round: frontier record %lld failed with node status %d",
+                              (long long)(base + k), st[k]);
+                ctx->err = msg;
+                return SGUFP_ERR_STATE;
+            }
+        }
+        S.relaxed++;
+        S.children += nch[k];
+        S.dd_nodes += dn[k];
+        S.dd_arcs += da[k];
+        S.sweeps += sw[k];
+    }
+    S.exact = (int64_t)act.size();
+
+    // 4: refinement loop of the exact DDs (NodeExplorer.cpp:946-969)
+    std::vector<std::vector<std::vector<int16_t>>> seen(b);
+    std::vector<uint16_t> plen(b);
+    const size_t stride = (size_t)ctx->net.n_slots + 1;
+    while (!act.empty()) {
+        S.refine_iters++;
+        if (!ctx->download(plen.data(), o.path_len, b) || !ctx->sync()) return SGUFP_ERR_HIP;
+        const int na = (int)act.size();
+        std::vector<int64_t> off(na + 1, 0);
+        for (int a = 0; a < na; a++) off[a + 1] = off[a] + plen[act[a]];
+        std::vector<int16_t> packed((size_t)off[na]);
+        if (!ctx->upload(ctx->d_bidx, act.data(), na) || !ctx->upload(ctx->d_boff, off.data(), na + 1) ||
+            !ctx->hip_ok(launch_gather_paths(o, ctx->sc.Lcap, ctx->d_bidx, ctx->d_boff, na, ctx->d_bpaths, ctx->stream),
+                         "k_gather_paths") ||
+            !ctx->download(packed.data(), ctx->d_bpaths, packed.size()) || !ctx->sync())
+            return SGUFP_ERR_HIP;
+        std::vector<int> fresh;
+        std::vector<int64_t> poff{0};
+        std::vector<int16_t> paths;
+        for (int a = 0; a < na; a++) {
+            const int k = act[a];
+            std::vector<int16_t> p(packed.begin() + off[a], packed.begin() + off[a + 1]);
+            auto &sv = seen[k];
+            if (std::find(sv.begin(), sv.end(), p) != sv.end()) {   // {ub, ub, {}, SUCCESS}
+                lbv[k] = ub[k];
+                S.exact_closed++;
+                continue;
+            }
+            paths.insert(paths.end(), p.begin(), p.end());
+            poff.push_back((int64_t)paths.size());
+            sv.push_back(std::move(p));
+            fresh.push_back(k);
+        }
+        act.clear();
+        if (fresh.empty()) break;
+        const int nf = (int)fresh.size();
+        std::vector<int32_t> type(nf);
+        std::vector<double> rhs(nf), rows((size_t)nf * stride);
+        int rc = sgufp_subproblem(ctx, nf, poff.data(), paths.data(), type.data(), rhs.data(), rows.data(), nullptr);
+        if (rc != SGUFP_OK) return rc;
+        S.subproblems += nf;
+        // Container::add in node order, feasibility list then optimality list
+        std::vector<int32_t> idx(nf), cut(nf);
+        std::vector<uint8_t> isf(nf);
+        for (int want = 1; want >= 0; want--) {
+            std::vector<double> r, h;
+            int cnt = 0, first = sgufp_cuts_count(ctx, want);
+            for (int i = 0; i < nf; i++) {
+                if (type[i] < 0) {
+                    ctx->err = "scenario subproblem failed (invalid path or numerical failure)";
+                    return SGUFP_ERR_STATE;
+                }
+                if (type[i] != want) continue;
+                r.insert(r.end(), rows.begin() + (size_t)i * stride, rows.begin() + (size_t)(i + 1) * stride);
+                h.push_back(rhs[i]);
+                idx[i] = fresh[i];
+                isf[i] = (uint8_t)want;
+                cut[i] = first + cnt++;
+            }
+            if (cnt && (rc = sgufp_cuts_append_rows(ctx, want, cnt, h.data(), r.data())) != SGUFP_OK) return rc;
+            (want ? S.new_feasibility_cuts : S.new_optimality_cuts) += cnt;
+        }
+        if ((rc = sgufp_batch_refine(ctx, nf, idx.data(), isf.data(), cut.data(), z)) != SGUFP_OK) return rc;
+        std::vector<int32_t> st2(b);
+        if (!ctx->download(st2.data(), o.status, b) || !ctx->download(ub.data(), o.ub, b) || !ctx->sync())
+            return SGUFP_ERR_HIP;
+        for (int k : fresh) {
+            if (st2[k] == SGUFP_NEEDS_SUBPROBLEM) act.push_back(k);
+            else if (st2[k] == SGUFP_PRUNED_BY_FEASIBILITY_CUT) S.pruned_feasibility++;
+            else if (st2[k] == SGUFP_PRUNED_BY_OPTIMALITY_CUT) S.pruned_optimality++;
+            st[k] = st2[k];
+        }
+    }
+
+    // 5: incumbent (DDSolver.cpp:723-731)
+    double znew = z;
+    for (int k = 0; k < b; k++)
+        if (lbv[k] > znew) znew = lbv[k];
+    S.improved = znew > z ? 1 : 0;
+    *incumbent = znew;
+
+    // 6: push the children of parents with ub > zOpt (DDSolver.cpp:744-748)
+    std::vector<int32_t> par;
+    std::vector<int64_t> dchild, dsol;
+    int64_t nc = 0, ns = 0;
+    for (int k = 0; k < b; k++) {
+        if (st[k] != SGUFP_SUCCESS || nch[k] == 0 || !(ub[k] > znew)) continue;
+        par.push_back(k);
+        dchild.push_back(base + nc);
+        dsol.push_back(sol_start + ns);
+        nc += nch[k];
+        ns += need[k];
+    }
+    ctx->relaxed = false;   // the popped slice is overwritten below
+    if (!ctx->frontier_reserve(base + nc, (size_t)(sol_start + ns))) return SGUFP_ERR_HIP;
+    const int np = (int)par.size();
+    if (np) {
+        int32_t *d_par = nullptr;
+        int64_t *d_dc = nullptr, *d_ds = nullptr;
+        if (np > ctx->max_batch) return SGUFP_ERR_STATE;
+        d_par = ctx->d_bidx;
+        d_dc = ctx->d_boff;
+        d_ds = ctx->d_bsol;
+        if (!ctx->upload(d_par, par.data(), np) || !ctx->upload(d_dc, dchild.data(), np) ||
+            !ctx->upload(d_ds, dsol.data(), np) ||
+            !ctx->hip_ok(launch_push_children(ctx->children_view(), o, d_par, d_dc, d_ds, np, ctx->fr, ctx->stream),
+                         "k_push_children") ||
+            !ctx->sync())
+            return SGUFP_ERR_HIP;
+    }
+    ctx->fr_n = base + nc;
+    ctx->fr_sol_top = ctx->fr_n ? sol_start + ns : 0;
+    S.pushed = nc;
+    S.frontier = ctx->fr_n;
+    if (stats) *stats = S;
+    return SGUFP_OK;
+}
+
+}  // extern "C"

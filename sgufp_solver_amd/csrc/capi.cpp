@@ -1,182 +1,7 @@
 // C ABI of libsgufp_hip.so (declared in include/sgufp_hip.h): context, device
 // memory, cut-pool densification, batch staging and result retrieval.
-#include "sgufp_hip.h"
+#include "ctx.hpp"
 
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <cstdlib>
-#include <cstring>
-#include <memory>
-#include <string>
-#include <unordered_map>
-#include <vector>
-
-#define SGUFP_HOST_ONLY 1  // no device code here: plain pointers in the device pass too
-#include "dd_device.hpp"
-#include "network.hpp"
-#include "sub_device.hpp"
-
-namespace sgufp {
-// dd_kernels.hip
-size_t relax_lds_bytes(int Tcap, int Lcap, int cb);
-size_t sub_lds_bytes(int n, int m, int n_slots);
-hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st);
-hipError_t launch_relax(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &, double, int,
-                        hipStream_t);
-hipError_t launch_scan(const uint32_t *, const uint32_t *, int, uint64_t *, uint64_t *, hipStream_t);
-hipError_t launch_emit(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &,
-                       const ChildOut &, hipStream_t);
-hipError_t launch_refine(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &,
-                         const int32_t *, const int32_t *, const uint8_t *, int, double, hipStream_t);
-}  // namespace sgufp
-
-using namespace sgufp;
-
-namespace {
-
-struct DevBuf {
-    void *p = nullptr;
-    size_t bytes = 0;
-};
-
-}  // namespace
-
-struct sgufp_ctx {
-    Network net;
-    int device = 0;
-    int max_batch = 0;
-    hipStream_t stream = nullptr;
-    std::string err;
-    std::vector<DevBuf> allocs;
-    size_t held = 0;
-
-    NetDev nd{};
-    Scratch sc{};
-    BatchOut out{};
-
-    // key (low 48 bits) -> slots carrying it
-    std::unordered_map<uint64_t, std::vector<int>> key_slots;
-
-    // cut pool
-    int row_cap = 0, n_rows = 0;
-    double *d_rows = nullptr, *d_rhs = nullptr, *d_coefT = nullptr;
-    int ustride = 1;
-    int cb = 4;                               // cuts per batched sweep
-    std::vector<int32_t> f_rows, o_rows;      // insertion order, row ids
-    int32_t *d_forder = nullptr, *d_oorder = nullptr;
-    int order_cap = 0;
-    bool order_dirty = true;
-
-    // staged batch
-    int n = 0;
-    uint16_t *d_gl = nullptr, *d_sollen = nullptr;
-    double *d_lb = nullptr, *d_ub = nullptr;
-    uint32_t *d_mask = nullptr;
-    uint8_t *d_valid = nullptr;
-    int64_t *d_soloff = nullptr;
-    int16_t *d_sol = nullptr;
-    size_t sol_cap = 0;
-    std::vector<std::vector<int16_t>> host_sols;  // kept for path / child assembly on host
-
-    // outputs / children
-    uint64_t *d_coff = nullptr, *d_soff = nullptr;
-    size_t child_cap = 0, csol_cap = 0;
-    uint16_t *d_cgl = nullptr, *d_csollen = nullptr;
-    double *d_clb = nullptr, *d_cub = nullptr;
-    uint32_t *d_cmask = nullptr;
-    int64_t *d_csoloff = nullptr;
-    int16_t *d_csol = nullptr;
-    int64_t total_children = 0, total_csol = 0;
-    bool relaxed = false;
-
-    // refine staging
-    int32_t *d_rslots = nullptr, *d_rcuts = nullptr;
-    uint8_t *d_rfeas = nullptr;
-
-    // scenario subproblem (built on first use)
-    bool sub_ready = false;
-    SubNet sn{};
-    SubIO sio{};
-    int sub_cap = 0;                          // paths the per-path buffers hold
-    size_t sub_path_cap = 0;                  // int16 decisions
-    int64_t *d_spoff = nullptr;
-    int16_t *d_spaths = nullptr;
-    int sub_last_n = 0;
-    bool sub_init();
-    bool sub_grow(int n, size_t total);
-    bool append_rows(int is_feasibility, int n_cuts, const double *rhs, const std::vector<double> &rows);
-
-    bool timing = false;
-    hipEvent_t ev[4] = {};
-    float ms_relax = 0, ms_emit = 0;
-
-    ~sgufp_ctx() {
-        if (device >= 0) (void)hipSetDevice(device);
-        for (auto &b : allocs) (void)hipFree(b.p);
-        for (auto &e : ev)
-            if (e) (void)hipEventDestroy(e);
-        if (stream) (void)hipStreamDestroy(stream);
-    }
-
-    bool hip_ok(hipError_t e, const char *what) {
-        if (e == hipSuccess) return true;
-        err = std::string(what) + ": " + hipGetErrorString(e);
-        return false;
-    }
-
-    template <typename T>
-    bool alloc(T *&ptr, size_t count, const char *what) {
-        void *p = nullptr;
-        size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
-        if (!hip_ok(hipMalloc(&p, bytes), what)) return false;
-        allocs.push_back({p, bytes});
-        held += bytes;
-        ptr = (T *)p;
-        return true;
-    }
-    template <typename T>
-    void release(T *&ptr) {
-        for (size_t k = 0; k < allocs.size(); k++)
-            if (allocs[k].p == (void *)ptr) {
-                (void)hipFree(ptr);
-                held -= allocs[k].bytes;
-                allocs.erase(allocs.begin() + (long)k);
-                break;
-            }
-        ptr = nullptr;
-    }
-    template <typename T>
-    bool upload(T *dst, const T *src, size_t count) {
-        if (!count) return true;
-        return hip_ok(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyHostToDevice, stream), "H2D");
-    }
-    template <typename T>
-    bool download(T *dst, const T *src, size_t count) {
-        if (!count) return true;
-        return hip_ok(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyDeviceToHost, stream), "D2H");
-    }
-    bool sync() { return hip_ok(hipStreamSynchronize(stream), "stream sync"); }
-
-    bool init();
-    bool grow_rows(int need);
-    bool push_orders();
-    bool grow_children(size_t nchild, size_t nsol);
-    Pool pool() const {
-        Pool p;
-        p.rows = d_rows; p.rhs = d_rhs; p.stride = net.n_slots + 1;
-        p.f_order = d_forder; p.nf = (int)f_rows.size();
-        p.o_order = d_oorder; p.no = (int)o_rows.size();
-        p.coefT = d_coefT; p.ustride = ustride;
-        return p;
-    }
-    BatchIn batch() const {
-        BatchIn b;
-        b.n = n; b.gl = d_gl; b.lb = d_lb; b.ub = d_ub; b.mask = d_mask; b.valid = d_valid;
-        b.sol_off = d_soloff; b.sol_len = d_sollen; b.sol = d_sol;
-        return b;
-    }
-};
 
 namespace {
 
@@ -307,7 +132,11 @@ bool sgufp_ctx::init() {
         return false;
     sol_cap = B * (size_t)std::max(1, L);
     if (!alloc(d_sol, sol_cap, "batch")) return false;
+    if (!alloc(d_bidx, B, "bnb") || !alloc(d_boff, B + 1, "bnb") || !alloc(d_bsol, B + 1, "bnb") ||
+        !alloc(d_bpaths, B * (size_t)sc.Lcap, "bnb"))
+        return false;
     if (!grow_rows(64)) return false;
+    cur = staged();
     return sync();
 }
 
@@ -381,7 +210,82 @@ static sgufp_ctx *finish_create(sgufp_ctx *ctx, int *err) {
     return ctx;
 }
 
+bool sgufp_ctx::relax_current(double optimal_lb) {
+    if (!push_orders()) return false;
+    const BatchIn &in = cur;
+    const Pool p = pool();
+    hipStream_t st = stream;
+    if (timing) hipEventRecord(ev[0], st);
+    if (!hip_ok(launch_relax(nd, sc, in, p, out, optimal_lb, cb, st), "k_relax")) return false;
+    if (timing) hipEventRecord(ev[1], st);
+    if (in.n > 0 && !hip_ok(launch_scan(out.nchild, out.sol_need, in.n, d_coff, d_soff, st), "k_scan2")) return false;
+    uint64_t tot[2] = {0, 0};
+    if (in.n > 0) {
+        if (!download(&tot[0], d_coff + in.n, 1) || !download(&tot[1], d_soff + in.n, 1)) return false;
+    }
+    if (!sync()) return false;
+    total_children = (int64_t)tot[0];
+    total_csol = (int64_t)tot[1];
+    if (!grow_children((size_t)tot[0], (size_t)tot[1])) return false;
+    ChildOut co = children_view();
+    if (timing) hipEventRecord(ev[2], st);
+    if (tot[0] > 0 && !hip_ok(launch_emit(nd, sc, in, p, out, co, st), "k_emit_children")) return false;
+    if (timing) hipEventRecord(ev[3], st);
+    relaxed = true;
+    return true;
+}
+
+// Host records (Inavap::Node, DD.h:456-478) -> device encoding: states as a mask over the
+// universe in force at the record's layer, solutions packed; invalid records are flagged
+// (the kernels answer them with SGUFP_NODE_ERR_RECORD) rather than rejected.
+void sgufp_ctx::encode_records(int n, const uint16_t *gl, const int64_t *states_off, const int16_t *states,
+                               const int64_t *sol_off, const int16_t *sol, EncodedRecords &e) const {
+    e.mask.assign(n, 0);
+    e.valid.assign(n, 1);
+    e.soff.resize(n);
+    e.slen.resize(n);
+    size_t total = 0;
+    for (int k = 0; k < n; k++) {
+        int64_t l = sol_off[k + 1] - sol_off[k];
+        if (l < 0 || l > net.L) { e.valid[k] = 0; l = 0; }
+        e.soff[k] = (int64_t)total;
+        e.slen[k] = (uint16_t)l;
+        total += (size_t)l;
+    }
+    e.sols.resize(total);
+    for (int k = 0; k < n; k++) {
+        if (e.slen[k]) std::memcpy(e.sols.data() + e.soff[k], sol + sol_off[k], e.slen[k] * sizeof(int16_t));
+        for (int t = 0; t < e.slen[k]; t++) {
+            int d = e.sols[e.soff[k] + t];
+            if (d != -1 && (d < 0 || d >= net.m)) e.valid[k] = 0;
+        }
+        int g = gl[k];
+        if (g > net.L) { e.valid[k] = 0; continue; }
+        // at a layer with a state update the build replaces the states (DD.cpp:3557-3571): they
+        // are kept when they fit the layer's universe (frontier round trips) and never invalid
+        const bool replaced = g < net.L && net.layer_update[g] >= 0;
+        int u = net.layer_universe[g];
+        int prev = -1;
+        for (int64_t t = states_off[k]; t < states_off[k + 1]; t++) {
+            int r = -1;
+            if (u >= 0) {
+                const auto &U = net.sets[u];
+                auto it = std::lower_bound(U.begin(), U.end(), states[t]);
+                if (it != U.end() && *it == states[t]) r = (int)(it - U.begin());
+            }
+            if (r < 0 || r <= prev) {   // not a sorted subset of the universe
+                if (replaced) e.mask[k] = 0;
+                else e.valid[k] = 0;
+                break;
+            }
+            e.mask[k] |= 1u << r;
+            prev = r;
+        }
+    }
+}
+
 extern "C" {
+
 
 sgufp_ctx *sgufp_create_from_file(const char *path, int device, int max_batch, int *err) {
     if (!path || max_batch <= 0) { if (err) *err = SGUFP_ERR_ARG; return nullptr; }
@@ -667,45 +571,9 @@ int sgufp_batch_upload(sgufp_ctx *ctx, int n, const uint16_t *gl, const double *
                        const int64_t *states_off, const int16_t *states, const int64_t *sol_off, const int16_t *sol) {
     if (!ctx || n < 0 || n > ctx->max_batch || (n && (!gl || !lb || !ub || !states_off || !sol_off)))
         return SGUFP_ERR_ARG;
-    const Network &net = ctx->net;
-    std::vector<uint32_t> mask(n, 0);
-    std::vector<uint8_t> valid(n, 1);
-    std::vector<int64_t> soff(n);
-    std::vector<uint16_t> slen(n);
-    size_t total = 0;
-    for (int k = 0; k < n; k++) {
-        int64_t l = sol_off[k + 1] - sol_off[k];
-        if (l < 0 || l > net.L) { valid[k] = 0; l = 0; }
-        soff[k] = (int64_t)total;
-        slen[k] = (uint16_t)l;
-        total += (size_t)l;
-    }
-    std::vector<int16_t> sols(total);
-    ctx->host_sols.assign(n, {});
-    for (int k = 0; k < n; k++) {
-        if (slen[k]) std::memcpy(sols.data() + soff[k], sol + sol_off[k], slen[k] * sizeof(int16_t));
-        ctx->host_sols[k].assign(sols.begin() + soff[k], sols.begin() + soff[k] + slen[k]);
-        for (int t = 0; t < slen[k]; t++) {
-            int d = sols[soff[k] + t];
-            if (d != -1 && (d < 0 || d >= net.m)) valid[k] = 0;
-        }
-        int g = gl[k];
-        if (g > net.L) { valid[k] = 0; continue; }
-        if (g < net.L && net.layer_update[g] >= 0) continue;  // states replaced at this layer (DD.cpp:3557-3571)
-        int u = net.layer_universe[g];
-        int prev = -1;
-        for (int64_t t = states_off[k]; t < states_off[k + 1]; t++) {
-            int r = -1;
-            if (u >= 0) {
-                const auto &U = net.sets[u];
-                auto it = std::lower_bound(U.begin(), U.end(), states[t]);
-                if (it != U.end() && *it == states[t]) r = (int)(it - U.begin());
-            }
-            if (r < 0 || r <= prev) { valid[k] = 0; break; }  // not a sorted subset of the universe
-            mask[k] |= 1u << r;
-            prev = r;
-        }
-    }
+    EncodedRecords e;
+    ctx->encode_records(n, gl, states_off, states, sol_off, sol, e);
+    const size_t total = e.sols.size();
     if (total > ctx->sol_cap) {
         ctx->release(ctx->d_sol);
         ctx->sol_cap = std::max(total, 2 * ctx->sol_cap);
@@ -713,46 +581,18 @@ int sgufp_batch_upload(sgufp_ctx *ctx, int n, const uint16_t *gl, const double *
     }
     ctx->n = n;
     if (!ctx->upload(ctx->d_gl, gl, n) || !ctx->upload(ctx->d_lb, lb, n) || !ctx->upload(ctx->d_ub, ub, n) ||
-        !ctx->upload(ctx->d_mask, mask.data(), n) || !ctx->upload(ctx->d_valid, valid.data(), n) ||
-        !ctx->upload(ctx->d_soloff, soff.data(), n) || !ctx->upload(ctx->d_sollen, slen.data(), n) ||
-        !ctx->upload(ctx->d_sol, sols.data(), total) || !ctx->sync())
+        !ctx->upload(ctx->d_mask, e.mask.data(), n) || !ctx->upload(ctx->d_valid, e.valid.data(), n) ||
+        !ctx->upload(ctx->d_soloff, e.soff.data(), n) || !ctx->upload(ctx->d_sollen, e.slen.data(), n) ||
+        !ctx->upload(ctx->d_sol, e.sols.data(), total) || !ctx->sync())
         return SGUFP_ERR_HIP;
+    ctx->cur = ctx->staged();
     ctx->relaxed = false;
     return SGUFP_OK;
 }
 
 int sgufp_batch_relax(sgufp_ctx *ctx, double optimal_lb) {
     if (!ctx) return SGUFP_ERR_ARG;
-    if (!ctx->push_orders()) return SGUFP_ERR_HIP;
-    const BatchIn in = ctx->batch();
-    const Pool pool = ctx->pool();
-    hipStream_t st = ctx->stream;
-    if (ctx->timing) hipEventRecord(ctx->ev[0], st);
-    if (!ctx->hip_ok(launch_relax(ctx->nd, ctx->sc, in, pool, ctx->out, optimal_lb, ctx->cb, st), "k_relax"))
-        return SGUFP_ERR_HIP;
-    if (ctx->timing) hipEventRecord(ctx->ev[1], st);
-    if (in.n > 0 &&
-        !ctx->hip_ok(launch_scan(ctx->out.nchild, ctx->out.sol_need, in.n, ctx->d_coff, ctx->d_soff, st), "k_scan2"))
-        return SGUFP_ERR_HIP;
-    uint64_t tot[2] = {0, 0};
-    if (in.n > 0) {
-        if (!ctx->download(&tot[0], ctx->d_coff + in.n, 1) || !ctx->download(&tot[1], ctx->d_soff + in.n, 1))
-            return SGUFP_ERR_HIP;
-    }
-    if (!ctx->sync()) return SGUFP_ERR_HIP;
-    ctx->total_children = (int64_t)tot[0];
-    ctx->total_csol = (int64_t)tot[1];
-    if (!ctx->grow_children((size_t)tot[0], (size_t)tot[1])) return SGUFP_ERR_HIP;
-    ChildOut co;
-    co.child_off = ctx->d_coff; co.sol_base = ctx->d_soff;
-    co.gl = ctx->d_cgl; co.lb = ctx->d_clb; co.ub = ctx->d_cub; co.mask = ctx->d_cmask;
-    co.sol_off = ctx->d_csoloff; co.sol_len = ctx->d_csollen; co.sol = ctx->d_csol;
-    if (ctx->timing) hipEventRecord(ctx->ev[2], st);
-    if (tot[0] > 0 && !ctx->hip_ok(launch_emit(ctx->nd, ctx->sc, in, pool, ctx->out, co, st), "k_emit_children"))
-        return SGUFP_ERR_HIP;
-    if (ctx->timing) hipEventRecord(ctx->ev[3], st);
-    ctx->relaxed = true;
-    return SGUFP_OK;
+    return ctx->relax_current(optimal_lb) ? SGUFP_OK : SGUFP_ERR_HIP;
 }
 
 int sgufp_batch_sync(sgufp_ctx *ctx) {

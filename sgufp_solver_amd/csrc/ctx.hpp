@@ -1,0 +1,229 @@
+// Context of libsgufp_hip.so shared by capi.cpp (C ABI) and bnb.cpp (B&B rounds):
+// device tables, scratch, cut pool, staged batch / device frontier and outputs.
+#pragma once
+
+#include "sgufp_hip.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#define SGUFP_HOST_ONLY 1  // no device code here: plain pointers in the device pass too
+#include "dd_device.hpp"
+#include "network.hpp"
+#include "sub_device.hpp"
+
+namespace sgufp {
+// dd_kernels.hip
+size_t relax_lds_bytes(int Tcap, int Lcap, int cb);
+size_t sub_lds_bytes(int n, int m, int n_slots);
+hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st);
+hipError_t launch_relax(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &, double, int,
+                        hipStream_t);
+hipError_t launch_scan(const uint32_t *, const uint32_t *, int, uint64_t *, uint64_t *, hipStream_t);
+hipError_t launch_emit(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &,
+                       const ChildOut &, hipStream_t);
+hipError_t launch_refine(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &,
+                         const int32_t *, const int32_t *, const uint8_t *, int, double, hipStream_t);
+hipError_t launch_gather_paths(const BatchOut &, int Lcap, const int32_t *idx, const int64_t *off, int n,
+                               int16_t *dst, hipStream_t);
+hipError_t launch_push_children(const ChildOut &, const BatchOut &, const int32_t *parents, const int64_t *dst_child,
+                                const int64_t *dst_sol, int n, const FrontierDev &, hipStream_t);
+}  // namespace sgufp
+
+using namespace sgufp;
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+struct EncodedRecords {
+    std::vector<uint32_t> mask;
+    std::vector<uint8_t> valid;
+    std::vector<int64_t> soff;
+    std::vector<uint16_t> slen;
+    std::vector<int16_t> sols;
+};
+
+struct sgufp_ctx {
+    Network net;
+    int device = 0;
+    int max_batch = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::vector<DevBuf> allocs;
+    size_t held = 0;
+
+    NetDev nd{};
+    Scratch sc{};
+    BatchOut out{};
+
+    // key (low 48 bits) -> slots carrying it
+    std::unordered_map<uint64_t, std::vector<int>> key_slots;
+
+    // cut pool
+    int row_cap = 0, n_rows = 0;
+    double *d_rows = nullptr, *d_rhs = nullptr, *d_coefT = nullptr;
+    int ustride = 1;
+    int cb = 4;                               // cuts per batched sweep
+    std::vector<int32_t> f_rows, o_rows;      // insertion order, row ids
+    int32_t *d_forder = nullptr, *d_oorder = nullptr;
+    int order_cap = 0;
+    bool order_dirty = true;
+
+    // current batch: the staged arrays below (sgufp_batch_upload) or a slice of the
+    // device frontier (sgufp_bnb_step)
+    BatchIn cur{};
+    // device frontier: the open-node work list of the B&B (lock_free_queue / lf_node lists,
+    // lock_free_queue.h:24-165, DDSolver.h:264-291), a LIFO stack in HBM
+    FrontierDev fr{};
+    int64_t fr_n = 0, fr_cap = 0;
+    size_t fr_sol_cap = 0;
+    int64_t fr_sol_top = 0;                   // arena entries in use (host mirror)
+    bool frontier_reserve(int64_t entries, size_t sol_entries);
+    // B&B step staging (host mirrors + small device index arrays)
+    int32_t *d_bidx = nullptr;                // [max_batch] node indices (paths / parents)
+    int64_t *d_boff = nullptr, *d_bsol = nullptr;  // [max_batch + 1]
+    int16_t *d_bpaths = nullptr;              // [max_batch * Lcap] gathered paths
+    bool relax_current(double optimal_lb);
+    void encode_records(int n, const uint16_t *gl, const int64_t *states_off, const int16_t *states,
+                        const int64_t *sol_off, const int16_t *sol, EncodedRecords &e) const;
+    // device records [count] (mask over the layer's universe) -> host states, as sgufp_batch_children
+    void decode_states(const uint16_t *gl, const uint32_t *mask, size_t count, int64_t *states_off,
+                       int16_t *states) const;
+
+    // staged batch
+    int n = 0;
+    uint16_t *d_gl = nullptr, *d_sollen = nullptr;
+    double *d_lb = nullptr, *d_ub = nullptr;
+    uint32_t *d_mask = nullptr;
+    uint8_t *d_valid = nullptr;
+    int64_t *d_soloff = nullptr;
+    int16_t *d_sol = nullptr;
+    size_t sol_cap = 0;
+
+    // outputs / children
+    uint64_t *d_coff = nullptr, *d_soff = nullptr;
+    size_t child_cap = 0, csol_cap = 0;
+    uint16_t *d_cgl = nullptr, *d_csollen = nullptr;
+    double *d_clb = nullptr, *d_cub = nullptr;
+    uint32_t *d_cmask = nullptr;
+    int64_t *d_csoloff = nullptr;
+    int16_t *d_csol = nullptr;
+    int64_t total_children = 0, total_csol = 0;
+    bool relaxed = false;
+
+    // refine staging
+    int32_t *d_rslots = nullptr, *d_rcuts = nullptr;
+    uint8_t *d_rfeas = nullptr;
+
+    // scenario subproblem (built on first use)
+    bool sub_ready = false;
+    SubNet sn{};
+    SubIO sio{};
+    int sub_cap = 0;                          // paths the per-path buffers hold
+    size_t sub_path_cap = 0;                  // int16 decisions
+    int64_t *d_spoff = nullptr;
+    int16_t *d_spaths = nullptr;
+    int sub_last_n = 0;
+    bool sub_init();
+    bool sub_grow(int n, size_t total);
+    bool append_rows(int is_feasibility, int n_cuts, const double *rhs, const std::vector<double> &rows);
+
+    bool timing = false;
+    hipEvent_t ev[4] = {};
+    float ms_relax = 0, ms_emit = 0;
+
+    ~sgufp_ctx() {
+        if (device >= 0) (void)hipSetDevice(device);
+        for (auto &b : allocs) (void)hipFree(b.p);
+        for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    bool hip_ok(hipError_t e, const char *what) {
+        if (e == hipSuccess) return true;
+        err = std::string(what) + ": " + hipGetErrorString(e);
+        return false;
+    }
+
+    template <typename T>
+    bool alloc(T *&ptr, size_t count, const char *what) {
+        void *p = nullptr;
+        size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+        if (!hip_ok(hipMalloc(&p, bytes), what)) return false;
+        allocs.push_back({p, bytes});
+        held += bytes;
+        ptr = (T *)p;
+        return true;
+    }
+    template <typename T>
+    void release(T *&ptr) {
+        for (size_t k = 0; k < allocs.size(); k++)
+            if (allocs[k].p == (void *)ptr) {
+                (void)hipFree(ptr);
+                held -= allocs[k].bytes;
+                allocs.erase(allocs.begin() + (long)k);
+                break;
+            }
+        ptr = nullptr;
+    }
+    template <typename T>
+    bool upload(T *dst, const T *src, size_t count) {
+        if (!count) return true;
+        return hip_ok(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyHostToDevice, stream), "H2D");
+    }
+    template <typename T>
+    bool download(T *dst, const T *src, size_t count) {
+        if (!count) return true;
+        return hip_ok(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyDeviceToHost, stream), "D2H");
+    }
+    bool sync() { return hip_ok(hipStreamSynchronize(stream), "stream sync"); }
+
+    bool init();
+    bool grow_rows(int need);
+    bool push_orders();
+    bool grow_children(size_t nchild, size_t nsol);
+    Pool pool() const {
+        Pool p;
+        p.rows = d_rows; p.rhs = d_rhs; p.stride = net.n_slots + 1;
+        p.f_order = d_forder; p.nf = (int)f_rows.size();
+        p.o_order = d_oorder; p.no = (int)o_rows.size();
+        p.coefT = d_coefT; p.ustride = ustride;
+        return p;
+    }
+    BatchIn staged() const {
+        BatchIn b;
+        b.n = n; b.gl = d_gl; b.lb = d_lb; b.ub = d_ub; b.mask = d_mask; b.valid = d_valid;
+        b.sol_off = d_soloff; b.sol_len = d_sollen; b.sol = d_sol;
+        b.bound_prune = 0;
+        return b;
+    }
+    BatchIn frontier_slice(int64_t base, int count) const {
+        BatchIn b;
+        b.n = count; b.gl = fr.gl + base; b.lb = fr.lb + base; b.ub = fr.ub + base; b.mask = fr.mask + base;
+        b.valid = fr.valid + base; b.sol_off = fr.sol_off + base; b.sol_len = fr.sol_len + base; b.sol = fr.sol;
+        b.bound_prune = 1;   // Worker::startWorker skips nodes with ub <= zOpt (DDSolver.cpp:707-711)
+        return b;
+    }
+    const BatchIn &batch() const { return cur; }
+    ChildOut children_view() const {
+        ChildOut co;
+        co.child_off = d_coff; co.sol_base = d_soff;
+        co.gl = d_cgl; co.lb = d_clb; co.ub = d_cub; co.mask = d_cmask;
+        co.sol_off = d_csoloff; co.sol_len = d_csollen; co.sol = d_csol;
+        return co;
+    }
+};

@@ -27,6 +27,7 @@ enum NodeStatus : int32_t {
     kPrunedFeasibility = 1,
     kPrunedOptimality = 2,
     kNeedsSubproblem = 3,      // exact DD: the argmax path waits for the scenario subproblem
+    kPrunedBound = 4,          // ub <= incumbent before processing (DDSolver.cpp:707-711), B&B rounds only
     kErrRecord = 16,           // record not representable (states not a sorted subset, bad decision id)
     kErrCapacity = 17,         // DD larger than the per-slot capacity
     kErrCutset = 18,           // getCutset would run into the terminal layer (reference UB)
@@ -95,6 +96,19 @@ struct BatchIn {
     const int64_t SGUFP_GBL *sol_off;
     const uint16_t SGUFP_GBL *sol_len;
     const int16_t SGUFP_GBL *sol;
+    int bound_prune;                     // 1: records with ub <= incumbent are pruned unprocessed
+};
+
+// Device frontier (B&B open nodes), SoA stack; sol_off are absolute offsets into sol.
+struct FrontierDev {
+    uint16_t SGUFP_GBL *gl;
+    double SGUFP_GBL *lb;
+    double SGUFP_GBL *ub;
+    uint32_t SGUFP_GBL *mask;
+    uint8_t SGUFP_GBL *valid;
+    int64_t SGUFP_GBL *sol_off;
+    uint16_t SGUFP_GBL *sol_len;
+    int16_t SGUFP_GBL *sol;
 };
 
 struct Pool {

@@ -1499,6 +1499,10 @@ __global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn
         st.status = kErrRecord;
         goto done;
     }
+    if (in.bound_prune && in.ub[slot] <= incumbent) {   // DDSolver.cpp:707-711
+        st.status = kPrunedBound;
+        goto done;
+    }
     // coefficient slots of the root solution (layer t, decision sol[t])
     for (int t = lane(); t < d.len; t += kWave) {
         int dec = rsol[t];

@@ -17,7 +17,7 @@ from .pools import NodeRecord, PoolCut, RelaxResult
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SGUFP_LIB_PATH") or os.path.join(HERE, "lib", "libsgufp_hip.so")
 
-SUCCESS, PRUNED_F, PRUNED_O, NEEDS_SUBPROBLEM = 0, 1, 2, 3
+SUCCESS, PRUNED_F, PRUNED_O, NEEDS_SUBPROBLEM, PRUNED_BOUND = 0, 1, 2, 3, 4
 ERR_RECORD, ERR_CAPACITY, ERR_CUTSET = 16, 17, 18
 
 EXPORTS = [
@@ -28,8 +28,21 @@ EXPORTS = [
     "sgufp_batch_paths", "sgufp_batch_stats", "sgufp_batch_refine", "sgufp_set_timing",
     "sgufp_last_timing", "sgufp_probe_network", "sgufp_batch_debug",
     "sgufp_batch_phases", "sgufp_subproblem", "sgufp_subproblem_detail", "sgufp_slot_keys",
-    "sgufp_cuts_append_rows",
+    "sgufp_cuts_append_rows", "sgufp_frontier_clear", "sgufp_frontier_size", "sgufp_frontier_push",
+    "sgufp_frontier_take_size", "sgufp_frontier_take", "sgufp_bnb_step", "sgufp_cuts_rows",
 ]
+
+
+class BnbStats(C.Structure):
+    """sgufp_bnb_stats (include/sgufp_hip.h)."""
+    _fields_ = [(f, C.c_int64) for f in (
+        "popped", "relaxed", "pruned_bound", "pruned_feasibility", "pruned_optimality", "exact", "exact_closed",
+        "subproblems", "new_feasibility_cuts", "new_optimality_cuts", "children", "pushed", "frontier",
+        "dd_nodes", "dd_arcs", "sweeps")] + [("refine_iters", C.c_int32), ("improved", C.c_int32),
+                                             ("ms_relax", C.c_double)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
 
 
 class NetworkInfo(C.Structure):
@@ -81,6 +94,13 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.sgufp_subproblem_detail.argtypes = [P, P, P, P]
     lib.sgufp_slot_keys.argtypes = [P, P]
     lib.sgufp_cuts_append_rows.argtypes = [P, C.c_int, C.c_int, P, P]
+    lib.sgufp_frontier_clear.argtypes = [P]
+    lib.sgufp_frontier_size.argtypes = [P, P, P]
+    lib.sgufp_frontier_push.argtypes = [P, C.c_int, P, P, P, P, P, P, P]
+    lib.sgufp_frontier_take_size.argtypes = [P, C.c_int, C.c_int, P, P]
+    lib.sgufp_frontier_take.argtypes = [P, C.c_int, C.c_int, P, P, P, P, P, P, P]
+    lib.sgufp_bnb_step.argtypes = [P, C.c_int, P, P]
+    lib.sgufp_cuts_rows.argtypes = [P, C.c_int, C.c_int, C.c_int, P, P]
     _lib = lib
     return lib
 
@@ -373,6 +393,54 @@ class Engine:
         rhs = np.ascontiguousarray(rhs, dtype=np.float64)
         rows = np.ascontiguousarray(rows, dtype=np.float64)
         self._check(self.lib.sgufp_cuts_append_rows(self.ctx, int(is_feas), len(rhs), _ptr(rhs), _ptr(rows)))
+
+    def cut_rows(self, is_feas: int, first: int = 0, count: Optional[int] = None):
+        """Pool cuts of one list (insertion order) as (rhs[k], rows[k, n_slots + 1])."""
+        total = self.lib.sgufp_cuts_count(self.ctx, int(is_feas))
+        count = total - first if count is None else count
+        rhs = np.zeros(max(count, 1), dtype=np.float64)
+        rows = np.zeros((max(count, 1), self.info.n_slots + 1), dtype=np.float64)
+        self._check(self.lib.sgufp_cuts_rows(self.ctx, int(is_feas), first, count, _ptr(rhs), _ptr(rows)))
+        return rhs[:count], rows[:count]
+
+    def cuts_count(self, is_feas: int) -> int:
+        return int(self.lib.sgufp_cuts_count(self.ctx, int(is_feas)))
+
+    # -- device frontier + B&B rounds (Inavap::DDSolver) -------------------------
+    def frontier_clear(self):
+        self._check(self.lib.sgufp_frontier_clear(self.ctx))
+
+    def frontier_size(self) -> int:
+        n = C.c_int64(0)
+        self._check(self.lib.sgufp_frontier_size(self.ctx, C.byref(n), None))
+        return n.value
+
+    def frontier_push(self, nodes: Sequence[NodeRecord] | BatchArrays):
+        b = nodes if isinstance(nodes, BatchArrays) else BatchArrays(nodes)
+        self._check(self.lib.sgufp_frontier_push(self.ctx, b.n, _ptr(b.gl), _ptr(b.lb), _ptr(b.ub), _ptr(b.states_off),
+                                                 _ptr(b.states), _ptr(b.sol_off), _ptr(b.sol)))
+
+    def frontier_take(self, n: int, from_bottom: bool = True) -> BatchArrays:
+        ns, nl = C.c_int64(0), C.c_int64(0)
+        fb = 1 if from_bottom else 0
+        self._check(self.lib.sgufp_frontier_take_size(self.ctx, n, fb, C.byref(ns), C.byref(nl)))
+        gl = np.zeros(max(n, 1), dtype=np.uint16)
+        lb = np.zeros(max(n, 1), dtype=np.float64)
+        ub = np.zeros(max(n, 1), dtype=np.float64)
+        soff = np.zeros(n + 1, dtype=np.int64)
+        states = np.zeros(max(ns.value, 1), dtype=np.int16)
+        poff = np.zeros(n + 1, dtype=np.int64)
+        sol = np.zeros(max(nl.value, 1), dtype=np.int16)
+        self._check(self.lib.sgufp_frontier_take(self.ctx, n, fb, _ptr(gl), _ptr(lb), _ptr(ub), _ptr(soff),
+                                                 _ptr(states), _ptr(poff), _ptr(sol)))
+        return batch_from_arrays(gl[:n], lb[:n], ub[:n], soff, states[:ns.value], poff, sol[:nl.value])
+
+    def bnb_step(self, incumbent: float, max_nodes: int = 0) -> Tuple[float, BnbStats]:
+        """One batched B&B round; returns the new incumbent and the round's counters."""
+        z = C.c_double(incumbent)
+        st = BnbStats()
+        self._check(self.lib.sgufp_bnb_step(self.ctx, int(max_nodes), C.byref(z), C.byref(st)))
+        return z.value, st
 
     # -- convenience: NodeExplorer::process for a list of nodes ----------------
     def relax(self, nodes: Sequence[NodeRecord], incumbent: float) -> List[RelaxResult]:

@@ -41,8 +41,14 @@ class InstanceConfig:
     scenarios: int     # S
 
 
-# SURVEY.md §8(d) configurations.
+# SURVEY.md §8(d) configurations, plus T1/T2: tiny networks whose whole B&B tree is
+# small enough for the end-to-end optimum check against the extensive form (main.cpp:66-76).
 CONFIGS = {
+    "T0": InstanceConfig("T0", 8, 2, 2, 2, 1.0, 1),
+    "T1": InstanceConfig("T1", 12, 2, 3, 2, 1.0, 1),
+    "T2": InstanceConfig("T2", 24, 3, 4, 2, 0.6, 1),
+    "T3": InstanceConfig("T3", 30, 3, 5, 2, 0.6, 1),
+    "T4": InstanceConfig("T4", 40, 4, 5, 2, 0.4, 1),
     "C1": InstanceConfig("C1", 40, 3, 6, 2, 1.0, 1),
     "C2": InstanceConfig("C2", 200, 6, 12, 3, 0.5, 1),
     "C3": InstanceConfig("C3", 1000, 12, 30, 3, 0.3, 64),

@@ -1,0 +1,179 @@
+"""Inavap::DDSolver on MI355X: batched B&B rounds over a device-resident frontier.
+
+Mirrors the reference's solver surface (/root/reference/DDSolver.h:431-439):
+
+    DDSolver(network, n_workers)           -> DDSolver(network_path, n_workers=..., ...)
+    std::pair<double,double> start(double) -> start(known_opt) -> (solution, seconds)
+    double startSolver(double)             -> start_solver(known_opt)
+
+and its final report line (DDSolver.cpp:863-865).  The work of one round is native
+(``sgufp_bnb_step``, sgufp_solver_amd/csrc/bnb.cpp): pop a batch from the frontier stack
+in HBM, relax it, run the exact-leaf refinement loops with the device subproblem, raise
+the incumbent, push the children.  This module only sequences rounds and, with more
+than one rank (one process per GPU, ``torch.distributed``; the "nccl" backend is RCCL
+over xGMI), does the exchanges the reference does through shared memory:
+
+* incumbent: all-reduce(MAX) of one double per round -- the CAS-max on
+  ``DDSolver::optimal`` (DDSolver.cpp:723-731);
+* cut pool: the rows each rank appended in the round are all-gathered and appended on
+  every other rank -- the global ``feasCutsGlobal`` / ``optCutsGlobal`` Containers
+  (DDSolver.h:415-416) every worker reads;
+* load balance: frontier sizes are all-gathered; when a rank runs dry the largest
+  shard gives away a share of its oldest records (the bottom of its stack) -- the
+  master's half-split and 40 % steal (DDSolver.cpp:603-621, 642-652);
+* termination: every shard empty (DDSolver.cpp:630-640).
+
+``engine`` may be any object with the Engine's frontier / bnb_step / cut-row methods;
+the product path passes ``sgufp_solver_amd.engine.Engine`` (HIP), the CPU multi-process
+tests pass a toy engine to exercise the protocol.
+"""
+from __future__ import annotations
+
+import time
+from typing import Optional
+
+import numpy as np
+
+from .pools import DOUBLE_MAX, DOUBLE_MIN, NodeRecord
+
+STEAL_SHARE = 0.4   # PROPORTION_OF_SHARE (DDSolver.h:22-38)
+
+
+class DDSolver:
+    def __init__(self, network_path: Optional[str] = None, n_workers: int = 1, device: int = 0,
+                 max_batch: int = 4096, batch_nodes: int = 0, engine=None, group=None, verbose: bool = True,
+                 progress: float = 0.0, max_rounds: int = 0):
+        """n_workers is accepted for API compatibility with the reference (threads there);
+        the parallelism here is the batch of ``batch_nodes`` (<= max_batch) records per
+        round and one rank per GPU."""
+        self.n_workers = n_workers
+        if engine is None:
+            from .engine import Engine
+            engine = Engine(network_path, device, max_batch)
+        self.eng = engine
+        self.batch_nodes = batch_nodes
+        self.group = group
+        self.verbose = verbose
+        self.progress = progress        # seconds between progress lines on stderr (0: none)
+        self.max_rounds = max_rounds    # safety cap for tests (0: none); hitting it raises
+        self.counters = {}
+        self.rounds = 0
+        self.seconds = 0.0
+
+    # -- collectives ---------------------------------------------------------------
+    def _dist(self):
+        import torch.distributed as dist
+        if not dist.is_available() or not dist.is_initialized():
+            return None
+        if dist.get_world_size(self.group) == 1:
+            return None
+        return dist
+
+    def _allreduce_max(self, dist, z: float) -> float:
+        import torch
+        dev = "cuda" if dist.get_backend(self.group) == "nccl" else "cpu"
+        t = torch.tensor([z], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return float(t.item())
+
+    def _exchange_cuts(self, dist, marks):
+        """All-gather the cut rows appended locally since the last exchange; append the
+        other ranks' rows in rank order.  marks[t] = rows of list t already shared."""
+        mine = {}
+        for t in (1, 0):
+            n = self.eng.cuts_count(t)
+            mine[t] = self.eng.cut_rows(t, marks[t], n - marks[t]) if n > marks[t] else None
+        world = dist.get_world_size(self.group)
+        me = dist.get_rank(self.group)
+        got = [None] * world
+        dist.all_gather_object(got, mine, group=self.group)
+        for r in range(world):
+            if r == me:
+                continue
+            for t in (1, 0):
+                if got[r][t] is not None and len(got[r][t][0]):
+                    self.eng.add_cut_rows(t, got[r][t][0], got[r][t][1])
+        for t in (1, 0):
+            marks[t] = self.eng.cuts_count(t)
+
+    def _rebalance(self, dist, sizes):
+        """Shards with an empty stack get records from the largest shard (its oldest
+        records, i.e. the shallowest subtrees)."""
+        world = len(sizes)
+        me = dist.get_rank(self.group)
+        empty = [r for r in range(world) if sizes[r] == 0]
+        donor = int(np.argmax(sizes))
+        if not empty or sizes[donor] < 2:
+            return
+        give = max(1, int(sizes[donor] * STEAL_SHARE))
+        payload = [None]
+        if me == donor:
+            taken = self.eng.frontier_take(give, from_bottom=True)
+            payload = [taken]
+        dist.broadcast_object_list(payload, src=donor, group=self.group)
+        taken = payload[0]
+        if me in empty:
+            k = empty.index(me)
+            idx = np.arange(k, taken.n, len(empty))
+            if len(idx):
+                from .engine import batch_slice
+                self.eng.frontier_push(batch_slice(taken, idx))
+
+    # -- the solver -------------------------------------------------------------------
+    def start_solver(self, known_optimal: float) -> float:
+        """DDSolver::startSolver (DDSolver.cpp:782-846): incumbent := known_optimal, the root
+        record Node{} on the frontier (rank 0), rounds until every shard is empty."""
+        dist = self._dist()
+        rank = dist.get_rank(self.group) if dist else 0
+        eng = self.eng
+        eng.frontier_clear()
+        if rank == 0:
+            eng.frontier_push([NodeRecord(0, DOUBLE_MIN, DOUBLE_MAX, [], [])])
+        z = float(known_optimal)
+        marks = {1: eng.cuts_count(1), 0: eng.cuts_count(0)}
+        keys = ("popped", "relaxed", "pruned_bound", "pruned_feasibility", "pruned_optimality", "exact",
+                "exact_closed", "subproblems", "new_feasibility_cuts", "new_optimality_cuts", "children", "pushed")
+        self.counters = {k: 0 for k in keys}
+        self.rounds = 0
+        t_last = time.perf_counter()
+        while True:
+            z, st = eng.bnb_step(z, self.batch_nodes)
+            self.rounds += 1
+            if self.progress and time.perf_counter() - t_last > self.progress:
+                t_last = time.perf_counter()
+                import sys
+                print(f"[DDSolver r{rank}] round {self.rounds} z={z!r} frontier={eng.frontier_size()} "
+                      f"{self.counters}", file=sys.stderr, flush=True)
+            if self.max_rounds and self.rounds >= self.max_rounds:
+                raise RuntimeError(f"DDSolver: no termination within {self.max_rounds} rounds (z={z!r})")
+            for k in keys:
+                self.counters[k] += int(getattr(st, k) if not isinstance(st, dict) else st[k])
+            if dist is None:
+                if eng.frontier_size() == 0:
+                    break
+                continue
+            z = self._allreduce_max(dist, z)
+            self._exchange_cuts(dist, marks)
+            sizes = [None] * dist.get_world_size(self.group)
+            dist.all_gather_object(sizes, eng.frontier_size(), group=self.group)
+            if sum(sizes) == 0:
+                break
+            self._rebalance(dist, sizes)
+        return z
+
+    def start(self, known_opt: float):
+        """DDSolver::start (DDSolver.cpp:848-867): solve, time, print the reference's line."""
+        t0 = time.perf_counter()
+        solution = self.start_solver(known_opt)
+        self.seconds = time.perf_counter() - t0
+        # "Explored N nodes" = sum of nQueue = children produced (DDSolver.cpp:742, 856-865)
+        explored = self.counters.get("children", 0)
+        dist = self._dist()
+        if dist is not None:
+            tot = [None] * dist.get_world_size(self.group)
+            dist.all_gather_object(tot, explored, group=self.group)
+            explored = sum(tot)
+        if self.verbose and (dist is None or dist.get_rank(self.group) == 0):
+            print(f"Optimal solution: {solution}. Explored {explored} nodes (entire search space) in "
+                  f"{self.seconds} seconds.")
+        return solution, self.seconds

@@ -1,0 +1,129 @@
+"""Batched branch-and-bound on the device (Inavap::DDSolver, /root/reference/DDSolver.cpp:556-846).
+
+End-to-end: the solver's optimum equals the extensive-form optimum (oracle/extensive_form.py,
+the restated StochasticModel.h:16-203 solved with HiGHS) within 1e-5 -- the reference's own
+acceptance check (main.cpp:43,76) -- seeded both as the reference's main does
+(known optimum - 10, main.cpp:75) and with no incumbent.  The instances have
+scenario-invariant rewards.  Frontier plumbing (push / take / bound
+pruning) is checked record by record.
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from oracle import extensive_form as ef
+from sgufp_solver_amd import engine as E
+from sgufp_solver_amd import instance, pools
+from sgufp_solver_amd.pools import DOUBLE_MAX, DOUBLE_MIN, NodeRecord
+from sgufp_solver_amd.solver import DDSolver
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+# (config, seed, scenarios): exact roots (refinement loop only) and non-exact roots
+# (cutset children, several rounds)
+E2E = [("T1", 1, 1), ("T1", 2, 3), ("T2", 1, 1), ("T2", 3, 3), ("T3", 1, 1), ("T3", 2, 3),
+       ("T4", 1, 1), ("T4", 2, 3), ("T4", 3, 3)]
+
+
+def _inst(cfg, seed, S):
+    inst = instance.generate(instance.CONFIGS[cfg], seed, scenarios=S)
+    d = tempfile.mkdtemp(prefix="sgufp_bnb_")
+    path = os.path.join(d, "net.txt")
+    inst.write(path)
+    return inst, path
+
+
+@pytest.mark.parametrize("cfg,seed,S", E2E, ids=[f"{c}-{s}-{S}" for c, s, S in E2E])
+@pytest.mark.parametrize("seeding", ["opt-10", "none"])
+def test_bnb_optimum_matches_extensive_form(cfg, seed, S, seeding):
+    inst, path = _inst(cfg, seed, S)
+    opt = ef.solve(inst)
+    known = opt - 10.0 if seeding == "opt-10" else DOUBLE_MIN
+    solver = DDSolver(path, max_batch=1024, max_rounds=20000, verbose=False)
+    sol, _ = solver.start(known)
+    solver.eng.close()
+    assert abs(sol - opt) <= TOL * max(1.0, abs(opt)), (sol, opt, solver.counters)
+    assert solver.counters["exact_closed"] >= 1
+
+
+@pytest.mark.parametrize("batch", [1, 3, 64])
+def test_bnb_batch_size_does_not_change_the_optimum(batch):
+    inst, path = _inst("T4", 3, 3)
+    opt = ef.solve(inst)
+    solver = DDSolver(path, max_batch=256, batch_nodes=batch, max_rounds=50000, verbose=False)
+    sol, _ = solver.start(DOUBLE_MIN)
+    solver.eng.close()
+    assert abs(sol - opt) <= TOL * max(1.0, abs(opt))
+    if batch == 1:
+        assert solver.rounds == solver.counters["popped"]
+
+
+def _records(eng, n):
+    """n real open-node records: root cutset children of a C2 instance."""
+    eng.upload([NodeRecord(0, DOUBLE_MIN, DOUBLE_MAX, [], [])])
+    eng.relax_async(DOUBLE_MIN)
+    eng.sync()
+    ch = eng.children_batch()
+    assert ch.n >= n
+    return E.batch_slice(ch, np.arange(n))
+
+
+def _same(a: E.BatchArrays, b: E.BatchArrays):
+    assert a.n == b.n
+    for f in ("gl", "lb", "ub", "states_off", "states", "sol_off", "sol"):
+        x, y = getattr(a, f), getattr(b, f)
+        if f in ("lb", "ub"):
+            assert np.array_equal(x.view(np.uint64), y.view(np.uint64)), f
+        else:
+            assert np.array_equal(x[:len(y)], y[:len(x)]) and len(x) == len(y), f
+
+
+def test_frontier_push_take_roundtrip():
+    inst, path = _inst("C2", 1, 1)
+    eng = E.Engine(path, 0, 256)
+    recs = _records(eng, 40)
+    eng.frontier_clear()
+    eng.frontier_push(E.batch_slice(recs, np.arange(25)))
+    eng.frontier_push(E.batch_slice(recs, np.arange(25, 40)))
+    assert eng.frontier_size() == 40
+    top = eng.frontier_take(5, from_bottom=False)
+    _same(top, E.batch_slice(recs, np.arange(35, 40)))
+    bottom = eng.frontier_take(10, from_bottom=True)
+    _same(bottom, E.batch_slice(recs, np.arange(10)))
+    assert eng.frontier_size() == 25
+    rest = eng.frontier_take(25, from_bottom=False)
+    _same(rest, E.batch_slice(recs, np.arange(10, 35)))
+    assert eng.frontier_size() == 0
+    eng.close()
+
+
+def test_bnb_step_matches_batch_relax_and_prunes_by_bound():
+    """One round over records on the frontier == the staged-batch relaxation of the same
+    records (status / children), and records with ub <= zOpt are skipped unprocessed."""
+    inst, path = _inst("C2", 1, 1)
+    eng = E.Engine(path, 0, 256)
+    pool = pools.synthetic_pool(inst, 4, 12, 1)
+    recs = _records(eng, 30)
+    eng.add_cuts(pool)
+    z = 100.0
+    ub = recs.ub.copy()
+    ub[::3] = 50.0                     # every third record: ub <= z, pruned by bound
+    recs = E.batch_from_arrays(recs.gl, recs.lb, ub, recs.states_off, recs.states, recs.sol_off, recs.sol)
+    keep = np.array([k for k in range(recs.n) if k % 3 != 0])
+    want = eng.relax(E.batch_to_records(E.batch_slice(recs, keep)), z)
+    eng.frontier_clear()
+    eng.frontier_push(recs)
+    z2, st = eng.bnb_step(z)
+    assert st.popped == 30 and st.pruned_bound == 10 and st.relaxed == 20
+    assert st.pruned_feasibility == sum(1 for w in want if w.status == E.PRUNED_F)
+    assert st.pruned_optimality == sum(1 for w in want if w.status == E.PRUNED_O)
+    assert st.exact == 0 and z2 == z
+    # pushed children: those of every successful parent (ub > z), in parent order
+    kids = [c for w in want if w.status == E.SUCCESS and w.ub > z for c in w.children]
+    assert st.pushed == len(kids) == eng.frontier_size()
+    got = eng.frontier_take(len(kids), from_bottom=True)
+    _same(got, E.BatchArrays(kids))
+    eng.close()

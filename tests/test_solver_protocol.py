@@ -1,0 +1,183 @@
+"""Multi-rank DDSolver protocol on CPU (gloo, world size 2 and 3).
+
+sgufp_solver_amd/solver.py sequences B&B rounds and does the reference's shared-memory
+exchanges with collectives: incumbent all-reduce(MAX) (DDSolver.cpp:723-731), all-gather
+of new cut rows (global Containers, DDSolver.h:415-416), frontier rebalancing (master
+half-split / 40 % steal, DDSolver.cpp:603-652) and termination (:630-640).  The engine is
+a toy knapsack B&B with the Engine's frontier / bnb_step / cut-row surface (test
+infrastructure), so the protocol is checked without a GPU: every rank ends with the
+brute-force optimum and identical cut pools, and every leaf is closed exactly once.
+"""
+import itertools
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from sgufp_solver_amd.engine import BatchArrays, batch_concat, batch_slice
+from sgufp_solver_amd.pools import NodeRecord
+from sgufp_solver_amd.solver import DDSolver
+
+D = 12
+RNG = np.random.default_rng(7)
+W = RNG.integers(1, 20, size=D).astype(float)
+A = RNG.integers(1, 10, size=D).astype(float)
+CAP = float(A.sum() * 0.45)
+
+
+def brute():
+    best = 0.0
+    for x in itertools.product([0, 1], repeat=D):
+        if np.dot(A, x) <= CAP:
+            best = max(best, float(np.dot(W, x)))
+    return best
+
+
+class ToyEngine:
+    """Knapsack B&B with the frontier / round / cut-row interface of engine.Engine."""
+
+    def __init__(self):
+        self.stack = []          # NodeRecord, top = end
+        self.cuts = {0: [], 1: []}
+        self.closed = []         # leaves closed on this rank
+
+    def _ub(self, sol):
+        d = len(sol)
+        v = float(np.dot(W[:d], sol))
+        return v + float(W[d:].sum())
+
+    def frontier_clear(self):
+        self.stack = []
+
+    def frontier_size(self):
+        return len(self.stack)
+
+    def frontier_push(self, recs):
+        if isinstance(recs, BatchArrays):
+            recs = [NodeRecord(int(recs.gl[k]), float(recs.lb[k]), float(recs.ub[k]),
+                               [int(s) for s in recs.states[recs.states_off[k]:recs.states_off[k + 1]]],
+                               [int(s) for s in recs.sol[recs.sol_off[k]:recs.sol_off[k + 1]]])
+                    for k in range(recs.n)]
+        self.stack.extend(recs)
+
+    def frontier_take(self, n, from_bottom=True):
+        if from_bottom:
+            out, self.stack = self.stack[:n], self.stack[n:]
+        else:
+            out, self.stack = self.stack[len(self.stack) - n:], self.stack[:len(self.stack) - n]
+        return BatchArrays(out)
+
+    def cuts_count(self, t):
+        return len(self.cuts[t])
+
+    def cut_rows(self, t, first=0, count=None):
+        rows = self.cuts[t][first:first + (len(self.cuts[t]) - first if count is None else count)]
+        return np.array([r[0] for r in rows]), np.array([r[1] for r in rows]).reshape(len(rows), 2)
+
+    def add_cut_rows(self, t, rhs, rows):
+        for h, r in zip(rhs, rows):
+            self.cuts[t].append((float(h), tuple(float(x) for x in r)))
+
+    def bnb_step(self, z, max_nodes=0):
+        b = min(len(self.stack), max_nodes or 4)
+        batch = self.stack[len(self.stack) - b:]
+        del self.stack[len(self.stack) - b:]
+        st = {k: 0 for k in ("popped", "relaxed", "pruned_bound", "pruned_feasibility", "pruned_optimality", "exact",
+                             "exact_closed", "subproblems", "new_feasibility_cuts", "new_optimality_cuts",
+                             "children", "pushed")}
+        st["popped"] = b
+        best = z
+        kids = []
+        for nd in batch:
+            if nd.ub <= z:
+                st["pruned_bound"] += 1
+                continue
+            st["relaxed"] += 1
+            sol = nd.sol
+            if float(np.dot(A[:len(sol)], sol)) > CAP:
+                st["pruned_feasibility"] += 1
+                self.cuts[1].append((-1.0, (float(len(sol)), float(sum(sol)))))
+                st["new_feasibility_cuts"] += 1
+                continue
+            if len(sol) == D:
+                st["exact"] += 1
+                st["exact_closed"] += 1
+                v = float(np.dot(W, sol))
+                self.closed.append(tuple(sol))
+                self.cuts[0].append((v, (float(D), float(sum(sol)))))
+                st["new_optimality_cuts"] += 1
+                best = max(best, v)
+                continue
+            for x in (0, 1):
+                s2 = list(sol) + [x]
+                kids.append((nd, NodeRecord(len(s2), -1e300, self._ub(s2), [], s2)))
+            st["children"] += 2
+        for parent, c in kids:
+            if parent.ub > best:
+                self.stack.append(c)
+                st["pushed"] += 1
+        return best, st
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = ToyEngine()
+    solver = DDSolver(engine=eng, batch_nodes=3, verbose=False)
+    z = solver.start_solver(-1.0)
+    q.put((rank, z, sorted(eng.cuts[0]), sorted(eng.cuts[1]), eng.closed, solver.counters, solver.rounds))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_multi_rank_solver_protocol(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    opt = brute()
+    res.sort()
+    for rank, z, c0, c1, closed, counters, rounds in res:
+        assert z == opt, (rank, z, opt)
+    # identical global pools on every rank (all-gathered rows)
+    assert all(r[2] == res[0][2] and r[3] == res[0][3] for r in res)
+    # every closed leaf closed by exactly one rank, and the work was shared
+    leaves = [t for r in res for t in r[4]]
+    assert len(leaves) == len(set(leaves))
+    assert sum(1 for r in res if r[5]["relaxed"] > 0) == world
+
+
+def test_single_rank_toy_matches_brute_force():
+    eng = ToyEngine()
+    z = DDSolver(engine=eng, batch_nodes=5, verbose=False).start_solver(-1.0)
+    assert z == brute()
+
+
+def test_toy_frontier_order_is_a_stack():
+    eng = ToyEngine()
+    recs = [NodeRecord(1, 0.0, float(k), [], [k % 2]) for k in range(6)]
+    eng.frontier_push(recs)
+    top = eng.frontier_take(2, from_bottom=False)
+    assert list(top.ub) == [4.0, 5.0]
+    bot = eng.frontier_take(2, from_bottom=True)
+    assert list(bot.ub) == [0.0, 1.0]
+    assert batch_concat([bot, top]).n == 4 and batch_slice(bot, np.array([1])).ub[0] == 1.0
