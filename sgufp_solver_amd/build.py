@@ -2,7 +2,8 @@
 
     libsgufp_hip.so   kernels + C ABI (include/sgufp_hip.h)
     libsgufp_host.so  C++ mirror of the reference's host API (Network / NodeExplorer /
-                      DDSolver) on top of the C ABI
+                      GuroSolver / DDSolver, include/sgufp/inavap.hpp) on top of the C ABI
+    host_api_test     C++ driver of that API (tests/host/host_api_test.cpp)
 """
 from __future__ import annotations
 
@@ -67,8 +68,15 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
             if os.path.isdir(os.path.join(ROOT, "include", "sgufp")) else []
         if force or _stale(hlib, host_srcs + hheaders + [lib]):
             cxx = shutil.which("g++") or "g++"
-            _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", f"-I{os.path.join(ROOT, 'include')}",
-                  *host_srcs, "-o", hlib, f"-L{LIBDIR}", "-lsgufp_hip", f"-Wl,-rpath,$ORIGIN"])
+            _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{os.path.join(ROOT, 'include')}",
+                  *host_srcs, "-o", hlib, f"-L{LIBDIR}", "-lsgufp_hip", "-Wl,-rpath,$ORIGIN"])
+        # C++ driver of the host API used by tests/test_host_api.py
+        tsrc = os.path.join(ROOT, "tests", "host", "host_api_test.cpp")
+        texe = os.path.join(LIBDIR, "host_api_test")
+        if os.path.exists(tsrc) and (force or _stale(texe, [tsrc, hlib] + hheaders)):
+            cxx = shutil.which("g++") or "g++"
+            _run([cxx, "-O2", "-std=c++17", "-Wall", f"-I{os.path.join(ROOT, 'include')}", tsrc, "-o", texe,
+                  f"-L{LIBDIR}", "-lsgufp_host", "-lsgufp_hip", "-Wl,-rpath,$ORIGIN"])
     return lib
 
 

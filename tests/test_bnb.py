@@ -127,3 +127,46 @@ def test_bnb_step_matches_batch_relax_and_prunes_by_bound():
     got = eng.frontier_take(len(kids), from_bottom=True)
     _same(got, E.BatchArrays(kids))
     eng.close()
+
+
+def _rank_main(rank, world, port, cfg, seed, S, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    inst = instance.generate(instance.CONFIGS[cfg], seed, scenarios=S)
+    path = os.path.join(tempfile.mkdtemp(prefix=f"sgufp_r{rank}_"), "net.txt")
+    inst.write(path)
+    solver = DDSolver(path, max_batch=256, batch_nodes=8, max_rounds=20000, verbose=False)
+    sol = solver.start_solver(DOUBLE_MIN)
+    q.put((rank, sol, solver.eng.cuts_count(1), solver.eng.cuts_count(0), solver.counters))
+    solver.eng.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg,seed,S", [("T4", 1, 1), ("T4", 3, 3)])
+def test_two_ranks_share_one_search(cfg, seed, S):
+    """Two frontier shards (two processes on the card, gloo for the exchanges): the same
+    optimum as the extensive form on both ranks, identical pool sizes after the final
+    all-gather, and both ranks relax records."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, cfg, seed, S, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    opt = ef.solve(instance.generate(instance.CONFIGS[cfg], seed, scenarios=S))
+    for rank, sol, nf, no, counters in res:
+        assert abs(sol - opt) <= TOL * max(1.0, abs(opt)), (rank, sol, opt)
+    assert res[0][2:4] == res[1][2:4]
+    assert all(r[4]["relaxed"] > 0 for r in res)

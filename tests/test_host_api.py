@@ -1,0 +1,50 @@
+"""The C++ host mirror of the reference API (include/sgufp/inavap.hpp, libsgufp_host.so).
+
+CPU: the library exports the reference's class surface (Network, Inavap::NodeExplorer::process,
+Inavap::GuroSolver::solveSubProblem, Inavap::DDSolver::start / startSolver, Container::add).
+GPU: tests/host/host_api_test.cpp solves seeded instances twice -- Inavap::DDSolver::start
+(batched device rounds) and a reference-style single-worker LIFO loop over
+NodeExplorer::process with two global Containers (DDSolver.cpp:658-776) -- and both optima
+must equal the extensive form within 1e-5 (main.cpp:43,76).
+"""
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "sgufp_solver_amd", "lib")
+
+
+def test_host_library_exports_reference_api(native_lib):
+    out = subprocess.run(["nm", "-DC", "--defined-only", os.path.join(LIB, "libsgufp_host.so")],
+                         capture_output=True, text=True, check=True).stdout
+    for sym in ["Network::Network(", "Inavap::NodeExplorer::process(", "Inavap::GuroSolver::solveSubProblem(",
+                "Inavap::DDSolver::start(", "Inavap::DDSolver::startSolver(", "Inavap::Container::add(",
+                "Inavap::Cut::get("]:
+        assert sym in out, sym
+    assert os.access(os.path.join(LIB, "host_api_test"), os.X_OK)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,seed,S,seeding", [("T1", 2, 3, "none"), ("T3", 1, 1, "opt-10"), ("T4", 1, 1, "none"),
+                                                 ("T4", 3, 3, "opt-10")])
+def test_host_api_solves_to_the_extensive_form_optimum(cfg, seed, S, seeding):
+    from oracle import extensive_form as ef
+    from sgufp_solver_amd import instance
+    inst = instance.generate(instance.CONFIGS[cfg], seed, scenarios=S)
+    path = os.path.join(tempfile.mkdtemp(prefix="sgufp_host_"), "net.txt")
+    inst.write(path)
+    opt = ef.solve(inst)
+    known = (opt - 10.0).hex() if seeding == "opt-10" else "none"
+    r = subprocess.run([os.path.join(LIB, "host_api_test"), path, known], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr
+    got = {}
+    for line in r.stdout.splitlines():
+        parts = line.split()
+        if parts and parts[0] in ("ddsolver", "explorer"):
+            got[parts[0]] = float.fromhex(parts[1])
+    assert "Optimal solution:" in r.stdout
+    for k in ("ddsolver", "explorer"):
+        assert abs(got[k] - opt) <= 1e-5 * max(1.0, abs(opt)), (k, got, opt)
