@@ -111,6 +111,7 @@ constexpr int kLdsBatchWidth = 128;
 constexpr int kStageEntries = 256;   // coefficient staging ring: f64 entries per slot (4 per lane)
 constexpr int kTopoEntries = 1024;   // topology staging ring: u16 entries per slot (16 per lane)
 constexpr int kStageLayers = 16;     // at most this many layers per staging group
+constexpr int kMaxRun = 4;           // exact layers folded in registers per narrow-sweep step
 constexpr uint16_t kMirParent = 127, kMirRankShift = 7, kMirAlive = 1u << 12, kMirIn = 1u << 13;
 
 // Packed topology of the narrow layers (HBM, per DD slot): node word = parent:7 | rank:5 |
@@ -846,6 +847,106 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
 #pragma unroll
         for (int jj = 0; jj < PT; jj++) tr[lane() + jj * kWave] = (uint16_t)pt[jj];
     };
+    // Exact run [ka, kb] (see the call site).  Items: nodes lane and lane + 64 of layer kb.
+    // Per-level layer metadata is read by lane s in one LDS access and moved to SGPRs;
+    // the walk packs the decision rank and in-arc flag (6 bits) and node index (7 bits)
+    // of every level into two u64 registers; the coefficients of all levels are loaded
+    // together before the fold, so a run costs the walk (one LDS access per level) plus
+    // two more LDS round trips.
+    auto fold_run = [&](int ka, int kb, int slot_, int k0_, uint32_t gn0_) {
+        const int dep = kb - ka + 1;
+        const LDS uint16_t *tr = bv.tring + (size_t)slot_ * kTopoEntries;
+        const LDS double *ring = bv.cring + (size_t)slot_ * kStageEntries;
+        const LDS double *pb = bv.vb + (size_t)((ka - 1) & 1) * kLdsBatchWidth * CB;
+        LDS double *ob = bv.vb + (size_t)(kb & 1) * kLdsBatchWidth * CB;
+        const int tl = min(ka + min(lane(), kMaxRun - 1), kb);
+        const uint32_t l_noff = d.noff[tl], l_w1 = bv.w1[tl], l_anx = d.acnt[tl + 1];
+        const uint32_t nlast = uni(d.nn[kb]);
+        uint32_t ebase[kMaxRun], nofs[kMaxRun];
+        bool w1s[kMaxRun], wrs[kMaxRun];
+#pragma unroll
+        for (int s = 0; s < kMaxRun; s++) {
+            nofs[s] = (uint32_t)__builtin_amdgcn_readlane((int)l_noff, s);
+            ebase[s] = nofs[s] - gn0_;
+            w1s[s] = s < dep && __builtin_amdgcn_readlane((int)l_w1, s) != 0;
+            wrs[s] = s < dep && ka + s < kS && (kS >= d.T || __builtin_amdgcn_readlane((int)l_anx, s) != 0);
+        }
+        const int nu = nlast > (uint32_t)kWave ? 2 : 1;
+        double res[2][CB];
+        // one item at a time (the second one, only for layers wider than a wave, behind a
+        // uniform branch): the per-level coefficient registers are not doubled
+        auto item = [&](const int u, double (&out)[CB]) {
+            {
+                const uint32_t i = (uint32_t)lane() + (uint32_t)u * kWave;
+                const bool ok = i < nlast;
+                uint64_t code = 0, ids = 0;
+                uint32_t cur = ok ? i : 0u;
+                bool alive = false;
+#pragma unroll
+                for (int s = kMaxRun - 1; s >= 0; s--) {
+                    if (s < dep) {
+                        const uint32_t wd = (uint32_t)tr[ebase[s] + cur];
+                        if (s == dep - 1) alive = ok && (wd & kMirAlive) != 0;
+                        code |= (uint64_t)(((wd >> kMirRankShift) & 31u) | ((wd & kMirIn) ? 32u : 0u)) << (6 * s);
+                        ids |= (uint64_t)cur << (7 * s);
+                        cur = wd & kMirParent;
+                    }
+                }
+                double x[CB], cfs[kMaxRun][CB];
+#pragma unroll
+                for (int c2 = 0; c2 < CB; c2++) x[c2] = pb[cur * CB + c2];
+#pragma unroll
+                for (int s = 0; s < kMaxRun; s++) {
+                    const uint32_t r = (uint32_t)(code >> (6 * s)) & 31u;
+                    const LDS double *cf = ring + (size_t)(ka + s - k0_) * per_layer + r;
+#pragma unroll
+                    for (int c2 = 0; c2 < CB; c2++) cfs[s][c2] = (s < dep && c2 < nb) ? cf[c2 * us] : 0.0;
+                }
+#pragma unroll
+                for (int s = 0; s < kMaxRun; s++) {
+                    if (s < dep) {
+                        const uint32_t cd = (uint32_t)(code >> (6 * s)) & 63u;
+                        const bool in = (cd & 32u) != 0;
+                        const bool reg = (cd & 31u) != 0;
+#pragma unroll
+                        for (int c2 = 0; c2 < CB; c2++) {
+                            if (c2 < nb) {
+                                const double xn = !in ? DMIN : (reg ? x[c2] + cfs[s][c2] : x[c2]);
+                                if (alive && w1s[s]) {
+                                    bv.sm[(size_t)(ka + s) * CB + c2] = xn;
+                                    bv.xm[(size_t)(ka + s) * CB + c2] = !in ? DMAX : (reg ? xn : x[c2] + 0.0);
+                                }
+                                x[c2] = xn;
+                            }
+                        }
+                        if (alive && wrs[s]) {
+                            double v = x[0];
+#pragma unroll
+                            for (int c2 = 1; c2 < CB; c2++) v = (c2 == nb - 1) ? x[c2] : v;
+                            d.s2[nofs[s] + (uint32_t)((ids >> (7 * s)) & 127u)] = v;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int c2 = 0; c2 < CB; c2++) out[c2] = x[c2];
+            }
+        };
+        item(0, res[0]);
+        if (nu == 2) item(1, res[1]);
+        // both items read their root values before either writes layer kb (the two
+        // buffers coincide when the run has an even number of layers)
+        wave_lds_sync();
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const uint32_t i = (uint32_t)lane() + (uint32_t)u * kWave;
+            if (u < nu && i < nlast) {
+#pragma unroll
+                for (int c2 = 0; c2 < CB; c2++)
+                    if (c2 < nb) ob[i * CB + c2] = res[u][c2];
+            }
+        }
+    };
+
     issue(0);
     commit(0);
     issue(1);
@@ -853,7 +954,7 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
     int j = 0, slot = 0;
     int k0 = uni((int)d.gstart[0]), k1 = uni((int)d.gstart[1]);
     uint32_t gn0 = uni(d.noff[k0]), gnN = uni(d.noff[k1]) - gn0, ga0 = uni(d.aoff[k0]);
-    for (int k = 1; k < d.kg; k++) {
+    for (int k = 1; k < d.kg;) {
 #ifdef SGUFP_PROF
         uint64_t t0 = wall_clock64();
 #endif
@@ -902,7 +1003,11 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
         if (acnt) {
             const uint32_t aoff = uni(d.aoff[k]);
             const uint32_t ebase = gnN + (aoff - ga0);   // ring entry of the layer's first arc
-            VP best{0.0, INT_MIN};
+            // Fast path: a plain max over the candidates.  The (value, priority) pick of the
+            // reference's mixed-order folds only differs from it when the maximum is a zero
+            // (equal doubles differ only in the sign of zero); that case re-runs the layer
+            // with the exact pick below.
+            double mx = -INFINITY;
             double xmin = DMAX;
             bool any = false;
             dispatch(acnt, [&](auto Uc, uint32_t base) {
@@ -926,24 +1031,44 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
                 }
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    const int a = (int)(base + u * G + grp);
                     const bool reg = r[u] != 0;
-                    VP e;
-                    e.v = reg ? px[u] + cf[u] : px[u];
-                    e.p = al[u] ? (reg ? prio_new(a) : prio_old(a)) : INT_MIN;
-                    const double y = reg ? e.v : px[u] + 0.0;
-                    best = vp_pick(best, e);
+                    const double v = reg ? px[u] + cf[u] : px[u];
+                    const double y = reg ? v : px[u] + 0.0;
+                    mx = (al[u] & (v > mx)) ? v : mx;
                     xmin = al[u] ? fmin(xmin, y) : xmin;
                     any = any | al[u];
                 }
             });
+            mx = lane_reduce<CB>(mx, [](double a, double b) { return (b > a) ? b : a; });
+            // across the lane groups of each cut (lanes that differ in bits >= log2(CB))
+            xmin = lane_reduce<CB>(xmin, [](double a, double b) { return fmin(a, b); });
+            any = lane_reduce<CB>((uint32_t)any, [](uint32_t a, uint32_t b) { return a | b; }) != 0;
+            VP best{mx, any ? 0 : INT_MIN};
+            if (__ballot(mx == 0.0) != 0) {
+                best = VP{0.0, INT_MIN};
+                dispatch(acnt, [&](auto Uc, uint32_t base) {
+                    constexpr int U = decltype(Uc)::value;
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        const uint32_t a = base + u * G + grp;
+                        const bool ok = (a < acnt) & cv;
+                        const uint32_t wd = word(ebase + (ok ? a : 0u));
+                        const uint32_t pp = wd & kMirParent, rr = (wd >> kMirRankShift) & 31u;
+                        const bool alive = ok & ((wd & kMirAlive) != 0);
+                        const double px = pbuf[(alive ? pp : 0u) * CB + c];
+                        const double cf = coefk[(alive ? c * us + rr : 0u)];
+                        const bool reg = rr != 0;
+                        VP e;
+                        e.v = reg ? px + cf : px;
+                        e.p = alive ? (reg ? prio_new((int)a) : prio_old((int)a)) : INT_MIN;
+                        best = vp_pick(best, e);
+                    }
+                });
+                best = wave_vp<CB>(best);
+            }
 #ifdef SGUFP_TRACE
             const uint64_t tla = __builtin_amdgcn_s_memtime();
 #endif
-            // across the lane groups of each cut (lanes that differ in bits >= log2(CB))
-            best = wave_vp<CB>(best);
-            xmin = lane_reduce<CB>(xmin, [](double a, double b) { return fmin(a, b); });
-            any = lane_reduce<CB>((uint32_t)any, [](uint32_t a, uint32_t b) { return a | b; }) != 0;
 #ifdef SGUFP_TRACE
             const uint64_t tlb = __builtin_amdgcn_s_memtime();
             if (blockIdx.x == 0 && lane() == 0 && bv.trace_on)
@@ -963,53 +1088,35 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
             wave_lds_sync();
             bv.prof[1] += wall_clock64() - t1;
 #endif
-        } else {
-            const uint32_t ebase = noff - gn0;   // ring entry of the layer's first node
-            dispatch(n, [&](auto Uc, uint32_t base) {
-                constexpr int U = decltype(Uc)::value;
-                uint32_t p[U], r[U];
-                bool al[U], in[U];
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const uint32_t i = base + u * G + grp;
-                    const bool ok = (i < n) & cv;
-                    const uint32_t wd = word(ebase + (ok ? i : 0u));
-                    p[u] = wd & kMirParent; r[u] = (wd >> kMirRankShift) & 31u;
-                    al[u] = ok & ((wd & kMirAlive) != 0); in[u] = (wd & kMirIn) != 0;
-                }
-                double px[U], cf[U];
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const bool use = al[u] & in[u];
-                    px[u] = pbuf[(use ? p[u] : 0u) * CB + c];
-                    cf[u] = coefk[(use ? c * us + r[u] : 0u)];
-                }
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const uint32_t i = base + u * G + grp;
-                    const bool reg = r[u] != 0;
-                    const double x = !in[u] ? DMIN : (reg ? px[u] + cf[u] : px[u]);
-                    const double y = !in[u] ? DMAX : (reg ? x : px[u] + 0.0);
-                    // a dead node's slot is never read (its children are dead too)
-                    if (i < kLdsBatchWidth) cbuf[i * CB + c] = x;
-                    if (al[u]) {
-                        if (wr && c == nb - 1) d.s2[noff + i] = x;
-                        if (w1) {
-                            bv.sm[(size_t)k * CB + c] = x;
-                            bv.xm[(size_t)k * CB + c] = y;
-                        }
-                    }
-                }
-            });
+            wave_lds_sync();
+            k++;
+            continue;
         }
+        // A run of exact (tree) layers [k, kb] inside the staging group: every node has one
+        // in-arc, so a node's value is the fold of its ancestors' steps from the layer
+        // before the run, x = !in ? DMIN : (reg ? x + coef : x) -- the same operations in the
+        // same order as layer by layer.  Each lane owns nodes of layer kb, walks up their
+        // ancestors' topology words once (shared by the CB cuts) and folds in registers;
+        // only layer kb goes through LDS.  Every alive node of the run is an ancestor of an
+        // alive node of layer kb (the deletion cascade removes childless parents), so the
+        // width-1 summaries and walk state2 of the inner layers are written on the way
+        // (lanes that share an ancestor write the same value).
+        int kb = min(min(k1, d.kg) - 1, k + kMaxRun - 1);
+        {
+            const int t = k + lane();
+            const uint64_t b = __ballot(lane() < kMaxRun && t <= kb && d.acnt[t] != 0);
+            if (b) kb = k + (int)(__ffsll((unsigned long long)b) - 1) - 1;
+        }
+        fold_run(k, kb, slot, k0, gn0);
         wave_lds_sync();
 #ifdef SGUFP_TRACE
         {
             const uint64_t tl1 = __builtin_amdgcn_s_memtime();
             if (blockIdx.x == 0 && lane() == 0 && bv.trace_on)
-                printf("L k=%d n=%u acnt=%u w1=%d cyc=%llu\n", k, n, acnt, (int)w1, (unsigned long long)(tl1 - tl0));
+                printf("L k=%d kb=%d n=%u acnt=0 w1=%d cyc=%llu\n", k, kb, n, (int)w1, (unsigned long long)(tl1 - tl0));
         }
 #endif
+        k = kb + 1;
     }
 #ifdef SGUFP_TRACE
     bv.trace_on = 0;
@@ -1090,7 +1197,7 @@ __device__ __forceinline__ bool dd_prune_check(const DD &d, const BatchView &bv,
 template <int CB, bool PASS_A>
 __device__ __forceinline__ void fused_leaf(const DD &d, BatchView &bv, const Pool &pool, int ncut, GBL double *keep,
                                            VP *term, VP *mxs) {
-    constexpr int U = CB >= 16 ? 2 : 32 / CB;
+    constexpr int U = CB >= 8 ? 1 : 16 / CB;
     const int last = d.T - 1;
     const uint32_t lo = uni(d.noff[last]), ln = uni(d.nn[last]);
     const int us = pool.ustride;
@@ -1471,7 +1578,7 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
 // ------------------------------------------------------------------------------------
 // Kernel 1: build + pool sweeps + finish, one wave per open node.
 template <int CB>
-__global__ void __launch_bounds__(kWave) k_relax(NetDev net, Scratch sc, BatchIn in, Pool pool, BatchOut out,
+__global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, BatchIn in, Pool pool, BatchOut out,
                                                 double incumbent) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
