@@ -151,6 +151,7 @@ class DDSolver {
     const uint16_t N_WORKERS;
     Device dev;
     int batch;
+    static constexpr int kDiveBatch = 64;
 
   public:
     explicit DDSolver(const std::shared_ptr<Network> &networkPtr_, uint16_t nWorkers, int batch = 4096);

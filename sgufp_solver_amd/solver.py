@@ -42,7 +42,7 @@ STEAL_SHARE = 0.4   # PROPORTION_OF_SHARE (DDSolver.h:22-38)
 class DDSolver:
     def __init__(self, network_path: Optional[str] = None, n_workers: int = 1, device: int = 0,
                  max_batch: int = 4096, batch_nodes: int = 0, engine=None, group=None, verbose: bool = True,
-                 progress: float = 0.0, max_rounds: int = 0):
+                 progress: float = 0.0, max_rounds: int = 0, dive_batch: int = 64):
         """n_workers is accepted for API compatibility with the reference (threads there);
         the parallelism here is the batch of ``batch_nodes`` (<= max_batch) records per
         round and one rank per GPU."""
@@ -56,6 +56,12 @@ class DDSolver:
         self.verbose = verbose
         self.progress = progress        # seconds between progress lines on stderr (0: none)
         self.max_rounds = max_rounds    # safety cap for tests (0: none); hitting it raises
+        # Until the first exact leaf closes there is no cut to prune with (and at most the
+        # seeded incumbent):
+        # rounds of dive_batch records from the top of the stack go depth-first to the
+        # exact leaves (like the reference's LIFO workers) instead of relaxing wide layers
+        # of siblings that nothing can prune yet.
+        self.dive_batch = dive_batch
         self.counters = {}
         self.rounds = 0
         self.seconds = 0.0
@@ -136,8 +142,14 @@ class DDSolver:
         self.counters = {k: 0 for k in keys}
         self.rounds = 0
         t_last = time.perf_counter()
+        diving = self.dive_batch > 0
         while True:
-            z, st = eng.bnb_step(z, self.batch_nodes)
+            batch = self.batch_nodes
+            if diving:
+                batch = self.dive_batch if not batch else min(batch, self.dive_batch)
+            z, st = eng.bnb_step(z, batch)
+            if diving and int(getattr(st, "exact_closed", 0) if not isinstance(st, dict) else st["exact_closed"]) > 0:
+                diving = False
             self.rounds += 1
             if self.progress and time.perf_counter() - t_last > self.progress:
                 t_last = time.perf_counter()

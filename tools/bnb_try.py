@@ -16,6 +16,8 @@ EF = json.load(open(os.path.join(ROOT, "tests", "golden", "extensive_form.json")
 cases = [a.split(":") for a in sys.argv[1:]] or [["C1", "1", "1", "0", "10"]]
 for cfg, seed, S, bn, gap in cases:
     key = f"{cfg}-{seed}-{S}"
+    if key not in EF and gap == "inf":
+        EF[key] = {"optimum": float("nan")}
     if key not in EF:
         from oracle import extensive_form as ef
         EF[key] = {"optimum": ef.solve(instance.generate(instance.CONFIGS[cfg], int(seed), scenarios=int(S)))}
