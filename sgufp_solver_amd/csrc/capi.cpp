@@ -97,6 +97,8 @@ bool sgufp_ctx::init() {
     ustride = std::max(1, net.max_states);
     if (const char *e = getenv("SGUFP_CUT_BATCH")) cb = atoi(e);
     if (cb != 1 && cb != 4 && cb != 8 && cb != 16) cb = 4;
+    nscreen = cb;
+    if (const char *e = getenv("SGUFP_SCREEN")) nscreen = std::max(0, atoi(e));
     int64_t acap = std::max<int64_t>(1, (int64_t)std::max(0, L - 4) * (kRelaxedMaxWidth - 1) * maxU);
     if (ncap > (int64_t)kParentMask || acap > (int64_t)0x7FFFFFFF) { err = "DD capacity beyond 22-bit indices"; return false; }
     sc.Ncap = (int)ncap;
@@ -172,12 +174,20 @@ bool sgufp_ctx::push_orders() {
     if (need > order_cap) {
         release(d_forder);
         release(d_oorder);
+        release(d_orank);
         order_cap = std::max(need, 2 * order_cap);
-        if (!alloc(d_forder, order_cap, "orders") || !alloc(d_oorder, order_cap, "orders")) return false;
+        if (!alloc(d_forder, order_cap, "orders") || !alloc(d_oorder, order_cap, "orders") ||
+            !alloc(d_orank, order_cap, "orders"))
+            return false;
     }
     // newest first: the Container is a LIFO list read from its head (Cut.h:456-465)
     std::vector<int32_t> f(f_rows.rbegin(), f_rows.rend()), o(o_rows.rbegin(), o_rows.rend());
-    if (!upload(d_forder, f.data(), f.size()) || !upload(d_oorder, o.data(), o.size())) return false;
+    // screening order: strongest node-independent bound first, newest first among equals
+    std::vector<int32_t> rank(o);
+    std::stable_sort(rank.begin(), rank.end(), [&](int32_t a, int32_t b) { return row_ub[a] < row_ub[b]; });
+    if (!upload(d_forder, f.data(), f.size()) || !upload(d_oorder, o.data(), o.size()) ||
+        !upload(d_orank, rank.data(), rank.size()))
+        return false;
     if (!sync()) return false;
     order_dirty = false;
     return true;
@@ -402,6 +412,16 @@ bool sgufp_ctx::append_rows(int is_feasibility, int n_cuts, const double *rhs_in
             }
     int first = n_rows;
     if (!grow_rows(first + n_cuts)) return false;
+    row_ub.resize((size_t)first + n_cuts);
+    for (int c = 0; c < n_cuts; c++) {
+        double b = rhs_in[c];
+        for (int l = 0; l < net.L; l++) {
+            double m = 0.0;
+            for (int r = 0; r < us; r++) m = std::max(m, coefT[(size_t)c * tstride + (size_t)l * us + r]);
+            b += m;
+        }
+        row_ub[(size_t)first + c] = b;
+    }
     if (!upload(d_coefT + (size_t)first * tstride, coefT.data(), coefT.size()) ||
         !upload(d_rows + (size_t)first * stride, rows.data(), rows.size()) ||
         !upload(d_rhs + first, rhs_in, (size_t)n_cuts) || !sync())

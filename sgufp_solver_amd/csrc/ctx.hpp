@@ -79,6 +79,9 @@ struct sgufp_ctx {
     int cb = 4;                               // cuts per batched sweep
     std::vector<int32_t> f_rows, o_rows;      // insertion order, row ids
     int32_t *d_forder = nullptr, *d_oorder = nullptr;
+    int32_t *d_orank = nullptr;               // optimality rows by ascending row_ub (screening order)
+    std::vector<double> row_ub;               // per row: RHS + sum_l max_r coef (node-independent bound)
+    int nscreen = 4;                          // optimality cuts screened before the exact phase
     int order_cap = 0;
     bool order_dirty = true;
 
@@ -202,6 +205,7 @@ struct sgufp_ctx {
         p.f_order = d_forder; p.nf = (int)f_rows.size();
         p.o_order = d_oorder; p.no = (int)o_rows.size();
         p.coefT = d_coefT; p.ustride = ustride;
+        p.o_rank = d_orank; p.nscreen = d_orank ? nscreen : 0;
         return p;
     }
     BatchIn staged() const {

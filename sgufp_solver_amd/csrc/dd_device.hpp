@@ -121,6 +121,11 @@ struct Pool {
     int no;
     const double SGUFP_GBL *coefT;       // [cap][L][ustride]: coefficient of state rank r at layer l
     int ustride;               // max state-set size of the network
+    // optimality-cut screening (see screen_opt in dd_kernels.hip): the first nscreen rows
+    // of o_rank (strongest first by a node-independent bound) are tried before the exact
+    // optimality phase; 0 disables it
+    const int32_t SGUFP_GBL *o_rank;
+    int nscreen;
 };
 
 struct BatchOut {

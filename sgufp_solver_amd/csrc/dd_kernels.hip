@@ -1464,6 +1464,96 @@ __device__ __forceinline__ bool redo_cut(const NetDev &net, DD &d, BatchView &bv
 }
 
 // CB cuts of one type per sweep, replayed in pool order (see "Multi-cut sweeps")
+// ------------------------------------------------------------------------------------
+// Optimality-cut screening.  After the feasibility phase the reference applies the O cuts
+// newest first and prunes as soon as ub <= optimalLB, where after cut j
+//     ub <= terminalState_j = max_leaf min_{i <= j} state2'_i(leaf)
+// (running minimum on every terminal arc, DD.cpp:3975-3984) and state2' is computed on
+// the DD the earlier O cuts edited.  Those edits only remove arcs, and rounding is
+// monotone, so state2'_i(leaf) <= v_i(leaf), the longest-path value of cut i on the
+// post-feasibility DD without any O edit.  Hence, for any set S of O cuts,
+//     max_leaf min_{i in S} v_i(leaf) <= optimalLB   ==>   the reference prunes the node
+// (status PRUNED_BY_OPTIMALITY_CUT, lb = ub = DOUBLE_MIN) at or before the last cut of S.
+// The screen sweeps the few strongest cuts first (o_rank: ascending node-independent
+// upper bound RHS + sum_l max_r coef) with a per-leaf running minimum; when it proves
+// the prune the exact optimality phase is skipped, otherwise the exact phase runs as if
+// nothing happened (the screen writes no DD state the exact phase reads).
+
+// leaf values of the nb screening cuts: run[i] = min(run[i], v_c(i)); returns the max over
+// alive leaves of run (DMIN when none is alive)
+template <int CB>
+__device__ __forceinline__ double screen_leaf(const DD &d, BatchView &bv, const Pool &pool, int nb, bool first,
+                                              GBL double *run) {
+    const int last = d.T - 1;
+    const uint32_t lo = uni(d.noff[last]), ln = uni(d.nn[last]);
+    const int us = pool.ustride;
+    double best = -INFINITY;
+    bool any = false;
+    for (uint32_t base = 0; base < ln; base += kWave) {
+        const uint32_t i = base + lane();
+        const bool ok = i < ln;
+        const uint32_t ic = ok ? i : 0u;
+        const uint32_t t = d.ntopo[lo + ic];
+        const uint32_t f = ok ? (uint32_t)d.nflag[lo + ic] : 0u;
+        const bool alive = (f & kAlive) != 0, inal = (f & kInAlive) != 0;
+        const uint32_t r = t >> kRankShift, p = alive ? (t & kParentMask) : 0u;
+        double m = first ? DMAX : run[(size_t)ic * CB];
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            if (c < nb) {
+                const double px = batch_value<CB>(d, bv, last - 1, p, c);
+                const double cf = bv.coef[c * us + r];
+                const double v = !inal ? DMIN : ((r != 0) ? px + cf : px);
+                m = fmin(m, v);
+            }
+        }
+        if (alive) {
+            run[(size_t)i * CB] = m;
+            best = (m > best) ? m : best;
+            any = true;
+        }
+    }
+    best = lane_reduce<1>(best, [](double a, double b) { return (b > a) ? b : a; });
+    any = wave_or((uint32_t)any) != 0;
+    wave_mem_sync();
+    return any ? best : DMIN;
+}
+
+// root fold (DD.cpp:3938-3949) of pool row `id` (lane-uniform or per lane)
+__device__ __forceinline__ double root_fold_row(const Pool &pool, const DD &d, int id) {
+    const GBL double *row = pool.rows + (size_t)id * pool.stride;
+    double v = pool.rhs[id];
+    for (int t = 0; t < d.len; t++) {
+        int sl = d.rslot[t];
+        if (sl >= 0) v = v + row[sl];
+    }
+    return v;
+}
+
+// true: the screen proves the optimality prune
+template <int CB>
+__device__ __forceinline__ bool screen_opt(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, double incumbent,
+                                           LoopState &st) {
+    const int last = d.T - 1;
+    GBL double *run = bv.s2b + (size_t)(uni(d.noff[last]) - bv.gbase) * CB;   // last-layer region, free here
+    const int n = min(pool.nscreen, pool.no);
+    for (int sp = 0; sp < n; sp += CB) {
+        const int nb = min(CB, n - sp);
+        if (lane() < nb) bv.ids[lane()] = pool.o_rank[sp + lane()];
+        for (int k = lane(); k < d.T; k += kWave) bv.w1[k] = ((d.nalive[k]) == 1) ? 1 : 0;
+        const double rv = (lane() < nb) ? root_fold_row(pool, d, pool.o_rank[sp + lane()]) : 0.0;
+        wave_lds_sync();
+        sweep_narrow<CB>(net, d, bv, pool, nb, rv, 0);
+        if (d.kg == 0 && lane() < nb) bv.s2b[lane()] = rv;
+        for (int k = max(d.kg, 1); k < last; k++) sweep_tail_layer<CB>(net, d, bv, pool, k, nb, 0);
+        batch_coef_direct(net, d, bv, pool, last, nb);
+        const double u = screen_leaf<CB>(d, bv, pool, nb, sp == 0, run);
+        st.applied += (uint32_t)nb;
+        if (u <= incumbent) return true;
+    }
+    return false;
+}
+
 template <int CB>
 __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const Scratch &sc, BatchView &bv, const Pool &pool,
                                  double incumbent, LoopState &st) {
@@ -1475,8 +1565,15 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
         return;
     }
     int s = 0;
+    bool screened = pool.nscreen <= 0;
     while (s < total) {
         const bool feas = s < pool.nf;
+        if (!feas && !screened) {
+            screened = true;
+            const bool pruned = screen_opt<CB>(net, d, bv, pool, incumbent, st);
+            st.stamp(6);
+            if (pruned) { st.status = kPrunedOptimality; return; }
+        }
         const int nb = min(CB, (feas ? pool.nf : total) - s);
         if (lane() < nb) bv.ids[lane()] = seq_id(pool, s + lane());
         for (int k = lane(); k < d.T; k += kWave) bv.w1[k] = ((d.nalive[k]) == 1) ? 1 : 0;
