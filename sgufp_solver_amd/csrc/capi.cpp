@@ -104,7 +104,9 @@ bool sgufp_ctx::init() {
     sc.Ncap = (int)ncap;
     sc.Acap = (int)acap;
     // LDS per relax workgroup (one wave): layer table, value buffers and staging rings
-    if (relax_lds_bytes(sc.Tcap, sc.Lcap, cb) > 160 * 1024) { err = "too many layers for the LDS layer table"; return false; }
+    sc.us = ustride;
+    if (net.n_slots >= 32767) { err = "more than 32766 coefficient slots (int16 root-solution slots)"; return false; }
+    if (relax_lds_bytes(sc.Tcap, sc.Lcap, cb, sc.us) > 160 * 1024) { err = "too many layers for the LDS layer table"; return false; }
     sc.tmir_cap = cb > 1 ? (int)(sc.Ncap + sc.Acap) : 0;
     sc.tail_cap = (int)tail;
     sc.cb_max = cb;
@@ -114,7 +116,9 @@ bool sgufp_ctx::init() {
         !alloc(sc.s2, B * sc.Ncap, "scratch") || !alloc(sc.tw, B * sc.Ncap, "scratch") ||
         !alloc(sc.atopo, B * sc.Acap, "scratch") || !alloc(sc.aflag, B * sc.Acap, "scratch") ||
         !alloc(sc.lay, B * sc.Tcap * 5, "scratch") || !alloc(sc.rslot, B * sc.Lcap, "scratch") ||
-        !alloc(sc.meta, B * 8, "scratch") || !alloc(sc.ubv, B, "scratch"))
+        !alloc(sc.meta, B * 8, "scratch") || !alloc(sc.ubv, B, "scratch") ||
+        !alloc(sc.sm1, B * sc.Tcap, "scratch") || !alloc(sc.xm1, B * sc.Tcap, "scratch") ||
+        !alloc(sc.v1, B * sc.Tcap, "scratch"))
         return false;
     if (cb > 1 && (!alloc(sc.s2b, B * sc.tail_cap * cb, "scratch") || !alloc(sc.sm, B * sc.Tcap * cb, "scratch") ||
                    !alloc(sc.xm, B * sc.Tcap * cb, "scratch") || !alloc(sc.tmir, B * (size_t)sc.tmir_cap, "scratch")))

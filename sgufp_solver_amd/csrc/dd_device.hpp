@@ -75,6 +75,12 @@ struct Scratch {
     int32_t SGUFP_GBL *rslot;    // [Lcap] coefficient slot of each root-solution decision (-1: decision -1)
     int32_t SGUFP_GBL *meta;     // [8] g, sol_len, T, exact, aligned, last_cut, status, cut_layer
     double SGUFP_GBL *ubv;       // [1] running upper bound
+    // single-cut sweep summaries (dd_sweep / dd_prune), [Tcap] per slot: HBM, so that the
+    // batched kernels' LDS fits eight waves per CU
+    double SGUFP_GBL *sm1;
+    double SGUFP_GBL *xm1;
+    uint8_t SGUFP_GBL *v1;
+    int us;                      // coefficient table entries per layer (the network's max state count)
     // multi-cut sweeps (k_relax with CB > 1)
     int tail_cap;      // nodes of the HBM-resident tail layers (wide layers + last layer)
     int cb_max;        // cuts per batched sweep the buffers are sized for

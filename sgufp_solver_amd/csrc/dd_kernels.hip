@@ -80,13 +80,14 @@ __device__ __forceinline__ int prio_old(int k) { return -k - 2; }
 struct DD {
     // LDS
     LDS uint32_t *noff, *nn, *nalive, *aoff, *acnt;
-    LDS int32_t *rslot;
+    LDS int16_t *rslot;   // [Lcap] coefficient slot of each root-solution decision (-1: decision -1)
     LDS double *buf0, *buf1;
-    LDS double *coef;     // [kMaxU] per-rank coefficients of the layer being swept
+    LDS double *coef;     // [us] per-rank coefficients of the layer being swept
     LDS int16_t *walk;    // [Tcap] decisions collected by a path walk
-    LDS double *sm1;      // [Tcap] width-1 layers: state2 of the single node (last single sweep)
-    LDS double *xm1;      // [Tcap] width-1 layers: min over its in-arcs of parent.state2 + weight
-    LDS uint8_t *v1;      // [Tcap] summary valid (layer had one alive node during that sweep)
+    GBL double *sm1;      // [Tcap] width-1 layers: state2 of the single node (last single sweep)
+    GBL double *xm1;      // [Tcap] width-1 layers: min over its in-arcs of parent.state2 + weight
+    GBL uint8_t *v1;      // [Tcap] summary valid (layer had one alive node during that sweep)
+    int us;               // entries of the per-layer coefficient tables
     // HBM (slot base applied)
     GBL uint32_t *ntopo;
     GBL uint8_t *nflag;
@@ -108,8 +109,8 @@ struct DD {
 };
 
 constexpr int kLdsBatchWidth = 128;
-constexpr int kStageEntries = 256;   // coefficient staging ring: f64 entries per slot (4 per lane)
-constexpr int kTopoEntries = 1024;   // topology staging ring: u16 entries per slot (16 per lane)
+constexpr int kStageEntries = 128;   // coefficient staging ring: f64 entries per slot (2 per lane)
+constexpr int kTopoEntries = 512;    // topology staging ring: u16 entries per slot (8 per lane)
 constexpr int kStageLayers = 16;     // at most this many layers per staging group
 constexpr int kMaxRun = 4;           // exact layers folded in registers per narrow-sweep step
 constexpr uint16_t kMirParent = 127, kMirRankShift = 7, kMirAlive = 1u << 12, kMirIn = 1u << 13;
@@ -134,52 +135,45 @@ struct LdsCarve {
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-// cb = cuts per batched sweep (1 = single-cut kernels only)
-__host__ __device__ inline LdsCarve lds_carve(int Tcap, int Lcap, int cb) {
+// cb = cuts per batched sweep (1 = single-cut kernels only), us = coefficient entries per
+// layer.  At 1k arcs (L = 281, us = 5, cb = 4) this is 20 KB: eight waves per CU.
+__host__ __device__ inline LdsCarve lds_carve(int Tcap, int Lcap, int cb, int us) {
     LdsCarve c;
     size_t o = 0;
     size_t single = (size_t)2 * kLdsWidth * 8, batch = (size_t)2 * 128 * (cb > 1 ? cb : 0) * 8;
     c.o_lay = o; o = align16(o + (size_t)Tcap * 5 * 4);
-    c.o_rslot = o; o = align16(o + (size_t)Lcap * 4);
+    c.o_rslot = o; o = align16(o + (size_t)Lcap * 2);
     c.o_buf = o; o = align16(o + (single > batch ? single : batch));
-    c.o_coef = o; o = align16(o + (size_t)kMaxU * 8);
+    c.o_coef = o; o = align16(o + (size_t)us * 8);
     c.o_walk = o; o = align16(o + (size_t)Tcap * 2);
-    c.o_bcoef = o; o = align16(o + (cb > 1 ? (size_t)cb * kMaxU * 8 : 0));
+    c.o_bcoef = o; o = align16(o + (cb > 1 ? (size_t)cb * us * 8 : 0));
     c.o_w1 = o; o = align16(o + (cb > 1 ? (size_t)Tcap : 0));
     c.o_ids = o; o = align16(o + (cb > 1 ? (size_t)cb * 4 : 0));
     c.o_gs = o; o = align16(o + (cb > 1 ? (size_t)(Tcap + 1) * 2 : 0));
-    // The single-cut summaries (sm1 / xm1 / v1) and the batched-sweep staging rings are
-    // never live together in one DD (a DD takes either the batched or the single-cut
-    // loop; redo uses the batched sweep), so they share one region.
-    const size_t r0 = o;
-    c.o_sm1 = o; o = align16(o + (size_t)Tcap * 8);
-    c.o_xm1 = o; o = align16(o + (size_t)Tcap * 8);
-    c.o_v1 = o; o = align16(o + (size_t)Tcap);
-    const size_t single_end = o;
-    o = r0;
     c.o_ring = o; o = align16(o + (cb > 1 ? (size_t)2 * kStageEntries * 8 : 0));
     c.o_tring = o; o = align16(o + (cb > 1 ? (size_t)2 * kTopoEntries * 2 : 0));
-    if (o < single_end) o = single_end;
+    c.o_sm1 = c.o_xm1 = c.o_v1 = 0;
     c.bytes = o;
     return c;
 }
 
 __device__ __forceinline__ void dd_bind(DD &d, LDS uint8_t *smem, const Scratch &sc, int slot, int cb = 1) {
-    LdsCarve c = lds_carve(sc.Tcap, sc.Lcap, cb);
+    LdsCarve c = lds_carve(sc.Tcap, sc.Lcap, cb, sc.us);
     LDS uint32_t *lay = (LDS uint32_t *)(smem + c.o_lay);
     d.noff = lay;
     d.nn = lay + sc.Tcap;
     d.nalive = lay + 2 * sc.Tcap;
     d.aoff = lay + 3 * sc.Tcap;
     d.acnt = lay + 4 * sc.Tcap;
-    d.rslot = (LDS int32_t *)(smem + c.o_rslot);
+    d.rslot = (LDS int16_t *)(smem + c.o_rslot);
+    d.us = sc.us;
     d.buf0 = (LDS double *)(smem + c.o_buf);
     d.buf1 = d.buf0 + kLdsWidth;
     d.coef = (LDS double *)(smem + c.o_coef);
     d.walk = (LDS int16_t *)(smem + c.o_walk);
-    d.sm1 = (LDS double *)(smem + c.o_sm1);
-    d.xm1 = (LDS double *)(smem + c.o_xm1);
-    d.v1 = smem + c.o_v1;
+    d.sm1 = sc.sm1 + (size_t)slot * sc.Tcap;
+    d.xm1 = sc.xm1 + (size_t)slot * sc.Tcap;
+    d.v1 = sc.v1 + (size_t)slot * sc.Tcap;
     size_t N = (size_t)slot * sc.Ncap, A = (size_t)slot * sc.Acap;
     d.ntopo = sc.ntopo + N;
     d.nflag = sc.nflag + N;
@@ -225,7 +219,7 @@ __device__ __forceinline__ double arc_weight(const NetDev &net, const DD &d, int
 
 // per-layer coefficient table in LDS: coef[r] for every rank
 __device__ __forceinline__ void load_layer_coef(const NetDev &net, const DD &d, int k, const GBL double *row) {
-    if (lane() < kMaxU) {
+    if (lane() < d.us) {
         int s = (lane() == 0) ? -1 : rank_slot(net, d, k, lane());
         d.coef[lane()] = s >= 0 ? row[s] : 0.0;
     }
@@ -364,7 +358,7 @@ __device__ __forceinline__ void dd_sweep(const NetDev &net, DD &d, const GBL dou
         d.buf0[0] = root_value;
     }
     for (int k = lane(); k < d.T; k += kWave) d.v1[k] = 0;
-    wave_lds_sync();
+    wave_mem_sync();   // the summaries live in HBM: clear before the sweep sets them
     for (int k = 1; k < d.T; k++) {
         const uint32_t noff = uni(d.noff[k]), n = uni(d.nn[k]);
         const uint32_t pnoff = uni(d.noff[k - 1]), pn = uni(d.nn[k - 1]);
@@ -527,6 +521,7 @@ __device__ __forceinline__ uint64_t prune_fire(const DD &d, int base, int end, d
 // width-1 layer would lose all of its incoming arcs.
 __device__ __forceinline__ bool dd_prune(const NetDev &net, DD &d, const GBL double *row, int first, int end, double thresh,
                          double maxState) {
+    wave_mem_sync();   // summaries written by other lanes of the sweep (HBM)
     for (int base = first; base < end; base += kWave) {
         uint64_t b = prune_fire(d, base, end, maxState, thresh, d.sm1, d.xm1, 1, d.v1);
         while (b) {
@@ -1719,7 +1714,7 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
                     if (net.slot_head[q] == j) { s = q; break; }
             }
         }
-        d.rslot[t] = s;
+        d.rslot[t] = (int16_t)s;
     }
     if (!dd_build(net, d, sc, in.mask[slot], n_nodes, n_arcs, n_merged)) {
         st.status = kErrCapacity;
@@ -1727,7 +1722,7 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
     }
     st.stamp(0);
     if (CB > 1 && d.aligned) {
-        LdsCarve cv = lds_carve(sc.Tcap, sc.Lcap, CB);
+        LdsCarve cv = lds_carve(sc.Tcap, sc.Lcap, CB, sc.us);
         d.tmir = sc.tmir + (size_t)slot * sc.tmir_cap;
         d.gstart = (LDS uint16_t *)(smem + cv.o_gs);
         BatchView bv;
@@ -1909,7 +1904,7 @@ __global__ void __launch_bounds__(kWave) k_refine(NetDev net, Scratch sc, BatchI
                     if (net.slot_head[q] == j) { s = q; break; }
             }
         }
-        d.rslot[t] = s;
+        d.rslot[t] = (int16_t)s;
     }
     wave_lds_sync();
     const int id = cut_ids[w];
@@ -1975,12 +1970,12 @@ __global__ void __launch_bounds__(1024) k_scan2(const uint32_t *a, const uint32_
 
 // ------------------------------------------------------------------------------------
 // host-side launchers (called from capi.cpp)
-size_t relax_lds_bytes(int Tcap, int Lcap, int cb) { return lds_carve(Tcap, Lcap, cb).bytes; }
+size_t relax_lds_bytes(int Tcap, int Lcap, int cb, int us) { return lds_carve(Tcap, Lcap, cb, us).bytes; }
 
 hipError_t launch_relax(const NetDev &net, const Scratch &sc, const BatchIn &in, const Pool &pool,
                         const BatchOut &out, double incumbent, int cb, hipStream_t st) {
     if (in.n <= 0) return hipSuccess;
-    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, cb);
+    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, cb, sc.us);
     switch (cb) {
         case 4: hipLaunchKernelGGL(k_relax<4>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent); break;
         case 8: hipLaunchKernelGGL(k_relax<8>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent); break;
@@ -1998,7 +1993,7 @@ hipError_t launch_scan(const uint32_t *a, const uint32_t *b, int n, uint64_t *oa
 hipError_t launch_emit(const NetDev &net, const Scratch &sc, const BatchIn &in, const Pool &pool,
                        const BatchOut &out, const ChildOut &co, hipStream_t st) {
     if (in.n <= 0) return hipSuccess;
-    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, 1);
+    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, 1, sc.us);
     hipLaunchKernelGGL(k_emit_children, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, co);
     return hipGetLastError();
 }
@@ -2007,7 +2002,7 @@ hipError_t launch_refine(const NetDev &net, const Scratch &sc, const BatchIn &in
                          const BatchOut &out, const int32_t *slots, const int32_t *cut_ids,
                          const uint8_t *cut_is_feas, int n, double incumbent, hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, 1);
+    size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, 1, sc.us);
     hipLaunchKernelGGL(k_refine, dim3(n), dim3(kWave), lds, st, net, sc, in, pool, out, slots, cut_ids,
                        cut_is_feas, n, incumbent);
     return hipGetLastError();
