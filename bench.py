@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--nodes", type=int, default=4096, help="open nodes per GPU per step")
+    ap.add_argument("--nodes", type=int, default=8192, help="open nodes per GPU per step")
     ap.add_argument("--config", default="C4")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--n-feas", type=int, default=16)
