@@ -27,12 +27,16 @@ def bfs_frontier(eng: E.Engine, n: int, incumbent: float = DOUBLE_MIN) -> E.Batc
         if cur.n == 0:
             continue
         nxt_parts = []
+        got = 0
         for s in range(0, cur.n, eng.info.max_batch):
             part = E.batch_slice(cur, np.arange(s, min(cur.n, s + eng.info.max_batch)))
             eng.upload(part)
             eng.relax_async(incumbent)
             eng.sync()
             nxt_parts.append(eng.children_batch())
+            got += nxt_parts[-1].n
+            if count + got >= n:
+                break   # the first n records of BFS order are complete: stop relaxing this level
         nxt = E.batch_concat(nxt_parts)
         take = min(n - count, nxt.n)
         done.append(E.batch_slice(nxt, np.arange(take)))
