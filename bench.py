@@ -53,6 +53,13 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=2048)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-tag", default="r01")
+    ap.add_argument("--mode", choices=["relax", "bnb"], default="relax",
+                    help="relax: the headline batch relaxation; bnb: the device B&B (config C3) for --bnb-seconds")
+    ap.add_argument("--bnb-config", default="C3")
+    ap.add_argument("--bnb-seconds", type=float, default=30.0)
+    ap.add_argument("--bnb-lb", choices=["zero", "gen"], default="zero",
+                    help="zero: drop the generator's sink lower bounds so the instance is feasible and "
+                         "incumbents / optimality cuts appear (with them most C3 paths are infeasible)")
     return ap.parse_args()
 
 
@@ -81,8 +88,79 @@ def pmc_traffic(tag: str, kernel: str = "k_relax"):
     return (2.0 * np.mean(f) + np.mean(w)) * 1024.0
 
 
+def bnb_main(args):
+    """Full B&B on the device (BASELINE configs[2]: 1k-arc network, 64 scenarios): the
+    DDSolver from the root record Node{} with no incumbent, for --bnb-seconds after a short
+    warm-up run; relaxations/s = NodeExplorer::process calls (exact-leaf refinement loops
+    with the device subproblem included) per second of the timed run.  With N ranks the
+    search is shared (incumbent all-reduce, cut all-gather, work stealing; strong scaling)."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend)
+    from sgufp_solver_amd import instance
+    from sgufp_solver_amd.pools import DOUBLE_MIN
+    from sgufp_solver_amd.solver import DDSolver
+    cfg = instance.CONFIGS[args.bnb_config]
+    inst = instance.generate(cfg, args.seed)
+    if args.bnb_lb == "zero":
+        inst.lb[:] = 0
+    work = tempfile.mkdtemp(prefix=f"sgufp_bnb_r{rank}_")
+    net = os.path.join(work, "net.txt")
+    inst.write(net)
+    solver = DDSolver(net, device=local, max_batch=args.nodes, verbose=False, time_budget=2.0)
+    solver.start_solver(DOUBLE_MIN)                        # warm-up (kernels, allocations)
+    solver.eng.clear_cuts()
+    solver.eng.set_timing(True)
+    solver.time_budget = args.bnb_seconds
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    z = solver.start_solver(DOUBLE_MIN)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    c = dict(solver.counters)
+    if dist:
+        t = torch.tensor([elapsed] + [float(c[k]) for k in sorted(c)], dtype=torch.float64,
+                         device="cuda" if torch.cuda.is_available() else "cpu")
+        tmax = t[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed = float(tmax.item())
+        c = {k: int(v) for k, v in zip(sorted(c), t[1:].tolist())}
+    line = {
+        "metric": "device B&B: node relaxations/s (NodeExplorer::process incl. exact-leaf subproblems)",
+        "value": round(c["relaxed"] / elapsed, 2), "unit": "relaxations/s", "n_gpus": world,
+        "seconds": round(elapsed, 3), "rounds": solver.rounds, "complete": solver.complete, "incumbent": z,
+        "higher_is_better": True, "scaling": "strong", "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"{args.bnb_config}: {cfg.n_arcs}-arc layered network, {inst.scenarios} scenarios"
+                               f"{' (lower bounds 0)' if args.bnb_lb == 'zero' else ''}, root record, no incumbent, "
+                               f"up to {args.nodes} records per round",
+                   "instance_seed": args.seed, "total_layers": int(solver.eng.info.total_layers)},
+        "counters": c,
+        "pool": [solver.eng.cuts_count(1), solver.eng.cuts_count(0)],
+        "subproblems_per_s": round(c["subproblems"] / elapsed, 2),
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    solver.eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.mode == "bnb":
+        return bnb_main(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

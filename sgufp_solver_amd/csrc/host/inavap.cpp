@@ -207,13 +207,13 @@ double DDSolver::startSolver(double known_optimal) {
     double z = known_optimal;
     totals = sgufp_bnb_stats{};
     rounds = 0;
-    // dive depth-first with small rounds until the first exact leaf closes (no cut can
-    // prune before that), then full batches
+    // dive depth-first with small rounds until the first exact leaves are reached (no cut
+    // can prune before that), then full batches
     bool diving = true;
     for (;;) {
         sgufp_bnb_stats st{};
         dev.check(sgufp_bnb_step(g, diving ? std::min(batch, kDiveBatch) : batch, &z, &st), "B&B round");
-        if (st.exact_closed > 0) diving = false;
+        if (st.exact > 0) diving = false;
         rounds++;
         totals.popped += st.popped;
         totals.relaxed += st.relaxed;

@@ -56,6 +56,7 @@ struct SubLds {
     LDS int64_t *alpha;     // [n+1] dual node potentials
     LDS double *coef;       // [n_slots]
     LDS int32_t *misc;      // [8] flags
+    LDS int32_t *zlist;     // [n] free-supply / free-demand nodes: v | src << 30 | snk << 29
 };
 
 __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -68,6 +69,7 @@ __host__ __device__ inline size_t sub_lds_layout(int n, int m, int n_slots, size
     off[11] = o; o = a16(o + (size_t)(n + 1) * 8);
     off[12] = o; o = a16(o + (size_t)n_slots * 8);
     off[13] = o; o = a16(o + 8 * 4);
+    off[14] = o; o = a16(o + (size_t)n * 4);
     return o;
 }
 
@@ -94,7 +96,7 @@ __device__ inline void lds_add(LDS double *p, double v) {
 enum BfMode { kSsp = 0, kPotPlain = 1, kPotBigM = 2 };
 
 template <typename F>
-__device__ inline void for_residual(const SubNet &N, const SubLds &W, int nct, int mode, int64_t M, F visit) {
+__device__ inline void for_residual(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M, F visit) {
     // contracted arcs: code 2k (forward), 2k+1 (backward)
     for (int k = lane(); k < nct; k += kWave) {
         const int t = W.ct_t[k], h = W.ct_h[k];
@@ -108,11 +110,11 @@ __device__ inline void for_residual(const SubNet &N, const SubLds &W, int nct, i
             if (x > 0) visit(h, t, R + (x <= L ? M : 0), 2 * k + 1);
         }
     }
-    // Z arcs: code 2m + 2v (+1)
-    for (int v = lane(); v < N.n; v += kWave) {
-        if (N.inner[v]) continue;
-        const bool src = is_src(N, v), snk = is_snk(N, v);
-        if (src && snk) continue;
+    // Z arcs: code 2m + 2v (+1), from the LDS list of non-inner nodes (built once per wave)
+    for (int i = lane(); i < nz; i += kWave) {
+        const uint32_t e = (uint32_t)W.zlist[i];
+        const int v = (int)(e & 0x1FFFFFFFu);
+        const bool src = (e >> 30) & 1u, snk = (e >> 29) & 1u;
         if (mode == kSsp) {
             if (src) visit(N.n, v, 0, 2 * N.m + 2 * v);
             if (snk) visit(v, N.n + 1, 0, 2 * N.m + 2 * v + 1);
@@ -123,7 +125,89 @@ __device__ inline void for_residual(const SubNet &N, const SubLds &W, int nct, i
     }
 }
 
-__device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, int mode, int64_t M) {
+// One Bellman-Ford pass over the residual arcs of for_residual (same arcs, same costs).
+// The chain arcs are relaxed UNR per lane at a time: all chain data and both end labels are
+// loaded first, then the candidate labels go out as LDS atomic minima.  Labels read inside
+// a pass may be a pass old (Jacobi order); the fixed point -- shortest (cost, hops) keys --
+// is the same, and the caller iterates until a pass changes nothing.
+__device__ inline uint32_t bf_pass(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M) {
+    constexpr int UNR = 4;
+    uint32_t changed = 0;
+    auto relax = [&](int v, int64_t ku, int64_t w, int64_t kv) {
+        if (ku >= kInf) return;
+        const int64_t nk = ku + (w << kHopBits) + 1;
+        if (nk < kv) {
+            __hip_atomic_fetch_min(&W.key[v], nk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            changed = 1;
+        }
+    };
+    for (int base = 0; base < nct; base += kWave * UNR) {
+        int t[UNR], h[UNR];
+        int64_t x[UNR], L[UNR], U[UNR], R[UNR], kt[UNR], kh[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; u++) {
+            const int k = base + u * kWave + lane();
+            const bool ok = k < nct;
+            const int kk = ok ? k : 0;
+            t[u] = ok ? W.ct_t[kk] : -1;
+            h[u] = ok ? W.ct_h[kk] : -1;
+            x[u] = W.ct_x[kk]; L[u] = W.ct_L[kk]; U[u] = W.ct_U[kk]; R[u] = W.ct_R[kk];
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; u++) {
+            const bool arc = t[u] >= 0 && h[u] >= 0;
+            kt[u] = arc ? W.key[t[u]] : kInf;
+            kh[u] = arc ? W.key[h[u]] : kInf;
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; u++) {
+            if (t[u] < 0 || h[u] < 0) continue;
+            if (mode == kPotPlain) {
+                if (x[u] < U[u]) relax(h[u], kt[u], -R[u], kh[u]);
+                if (x[u] > L[u]) relax(t[u], kh[u], R[u], kt[u]);
+            } else {
+                if (x[u] < U[u]) relax(h[u], kt[u], -(R[u] + (x[u] < L[u] ? M : 0)), kh[u]);
+                if (x[u] > 0) relax(t[u], kh[u], R[u] + (x[u] <= L[u] ? M : 0), kt[u]);
+            }
+        }
+    }
+    // Z arcs (few): one at a time
+    for (int i = lane(); i < nz; i += kWave) {
+        const uint32_t e = (uint32_t)W.zlist[i];
+        const int v = (int)(e & 0x1FFFFFFFu);
+        const bool src = (e >> 30) & 1u, snk = (e >> 29) & 1u;
+        if (mode == kSsp) {
+            if (src) relax(v, W.key[N.n], 0, W.key[v]);
+            if (snk) relax(N.n + 1, W.key[v], 0, W.key[N.n + 1]);
+        } else {
+            relax(v, W.key[N.n], 0, W.key[v]);
+            relax(N.n, W.key[v], 0, W.key[N.n]);
+        }
+    }
+    return changed;
+}
+
+// Predecessors of the SSP labels: the smallest arc code among the residual arcs into each
+// node that are tight in (cost, hops).  Hops grow by one along such arcs, so the
+// predecessor graph has no cycle.  With reset, the labels of an earlier Bellman-Ford are
+// reused after an augmentation: every path of tight arcs that still have residual
+// capacity costs the old shortest distance, and shortest distances never decrease in SSP,
+// so such a path is a shortest path of the new residual graph.
+__device__ inline void ssp_preds(const SubNet &N, const SubLds &W, int nct, int nz, int64_t M, bool reset) {
+    if (reset) {
+        for (int v = lane(); v < N.n + 2; v += kWave) W.pred[v] = INT_MAX;
+        wave_lds_sync();
+    }
+    for_residual(N, W, nct, nz, kSsp, M, [&](int u, int v, int64_t w, int code) {
+        const int64_t ku = W.key[u];
+        if (ku >= kInf) return;
+        if (ku + (w << kHopBits) + 1 == W.key[v])
+            __hip_atomic_fetch_min(&W.pred[v], code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    });
+    wave_lds_sync();
+}
+
+__device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M) {
     const int nn = N.n + 2;
     for (int v = lane(); v < nn; v += kWave) {
         W.key[v] = (mode == kSsp) ? (v == N.n ? 0 : kInf) : 0;
@@ -132,28 +216,15 @@ __device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, i
     wave_lds_sync();
     bool converged = false;
     for (int it = 0; it < nn + 2; it++) {
-        uint32_t changed = 0;
-        for_residual(N, W, nct, mode, M, [&](int u, int v, int64_t w, int code) {
-            const int64_t ku = W.key[u];
-            if (ku >= kInf) return;
-            const int64_t nk = ku + (w << kHopBits) + 1;
-            if (nk < W.key[v]) {
-                __hip_atomic_fetch_min(&W.key[v], nk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                changed = 1;
-            }
-        });
+#ifdef SGUFP_SUB_TRACE
+        if (lane() == 0) W.misc[5]++;
+#endif
+        const uint32_t changed = bf_pass(N, W, nct, nz, mode, M);
         wave_lds_sync();
         if (!wave_or(changed)) { converged = true; break; }
     }
     if (mode != kSsp || !converged) return converged;
-    // predecessors: the smallest arc code among the tight arcs into each node
-    for_residual(N, W, nct, mode, M, [&](int u, int v, int64_t w, int code) {
-        const int64_t ku = W.key[u];
-        if (ku >= kInf) return;
-        if (ku + (w << kHopBits) + 1 == W.key[v])
-            __hip_atomic_fetch_min(&W.pred[v], code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    });
-    wave_lds_sync();
+    ssp_preds(N, W, nct, nz, M, false);
     return true;
 }
 
@@ -314,7 +385,7 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     const int S = N.S;
     const int p = blockIdx.x / S, s = blockIdx.x - p * S;
     if (p >= io.n_paths) return;
-    size_t off[14];
+    size_t off[15];
     sub_lds_layout(N.n, N.m, N.n_slots, off);
     SubLds W;
     W.dec = (LDS int32_t *)(smem + off[0]);
@@ -331,6 +402,7 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     W.alpha = (LDS int64_t *)(smem + off[11]);
     W.coef = (LDS double *)(smem + off[12]);
     W.misc = (LDS int32_t *)(smem + off[13]);
+    W.zlist = (LDS int32_t *)(smem + off[14]);
     const int n = N.n, m = N.m;
     const size_t so = (size_t)s * m;
     const int64_t poff = io.path_off[p], plen = io.path_off[p + 1] - poff;
@@ -370,6 +442,21 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
         nct += (int)__builtin_amdgcn_readlane((int)incl, kWave - 1);
     }
     wave_lds_sync();
+    // free-supply / free-demand nodes (structural; read by every Bellman-Ford pass from LDS)
+    int nz = 0;
+    for (int base = 0; base < n; base += kWave) {
+        const int v = base + lane();
+        bool z = false;
+        uint32_t e = 0;
+        if (v < n && !N.inner[v]) {
+            const bool src = is_src(N, v), snk = is_snk(N, v);
+            z = !(src && snk);
+            e = (uint32_t)v | (src ? 1u << 30 : 0u) | (snk ? 1u << 29 : 0u);
+        }
+        const uint32_t incl = wave_scan_incl(z ? 1u : 0u);
+        if (z) W.zlist[nz + (int)incl - 1] = (int32_t)e;
+        nz += (int)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+    }
     int first_bad = INT_MAX;   // first chain (rank) that makes the scenario infeasible up front
     for (int k = lane(); k < nct; k += kWave) {
         int a = W.ct_first[k];
@@ -439,11 +526,16 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
         wave_lds_sync();
     } else {
         // 3. successive shortest paths (max reward) from the sources to the sinks
+#ifdef SGUFP_SUB_TRACE
+        const uint64_t tr0 = wall_clock64();
+        int nbf = 1;
+#endif
         int iters = 0;
-        for (;; iters++) {
-            if (!bellman_ford(N, W, nct, kSsp, M)) { status = kSubError; break; }
+        bool fresh = true;   // labels and predecessors from a full Bellman-Ford
+        if (!bellman_ford(N, W, nct, nz, kSsp, M)) status = kSubError;
+        for (; status == kSubOptimal; iters++) {
             const int64_t kz = W.key[n + 1];
-            if (kz >= kInf || key_cost(kz) >= 0) break;
+            if (fresh && (kz >= kInf || key_cost(kz) >= 0)) break;
             if (iters > 8 * m + 64) { status = kSubError; break; }
             // bottleneck along the predecessor chain, then augment (lane 0 walks)
             if (lane() == 0) {
@@ -459,7 +551,7 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
                     delta = cap < delta ? cap : delta;
                     v = (code & 1) ? W.ct_h[k] : W.ct_t[k];
                 }
-                if (v != n || delta <= 0 || delta >= kInf) W.misc[1] = 1;
+                if (v != n || delta <= 0 || delta >= kInf) W.misc[fresh ? 1 : 2] = 1;
                 else {
                     v = n + 1;
                     while (v != n) {
@@ -473,7 +565,26 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
             }
             wave_lds_sync();
             if (W.misc[1]) { status = kSubError; break; }
+            if (W.misc[2]) {
+                // no tight path left under the old labels: recompute them
+                wave_lds_sync();
+                if (lane() == 0) W.misc[2] = 0;
+                wave_lds_sync();
+                if (!bellman_ford(N, W, nct, nz, kSsp, M)) { status = kSubError; break; }
+#ifdef SGUFP_SUB_TRACE
+                nbf++;
+#endif
+                fresh = true;
+                continue;
+            }
+            ssp_preds(N, W, nct, nz, M, true);
+            fresh = false;
         }
+#ifdef SGUFP_SUB_TRACE
+        if (blockIdx.x % 997 == 0 && lane() == 0)
+            printf("SUB blk=%d nct=%d nz=%d aug=%d bf=%d passes=%d ticks=%llu\n", (int)blockIdx.x, nct, nz, iters, nbf,
+                   W.misc[5], (unsigned long long)(wall_clock64() - tr0));
+#endif
         // lower bounds met?
         int unmet = 0;
         for (int k = lane(); k < nct; k += kWave) {
@@ -489,7 +600,7 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
             //    costs (their M-multiple is a dual ray, case (iii))
             const int mode = unmet ? kPotBigM : kPotPlain;
             if (unmet) status = kSubInfeasible;
-            if (!bellman_ford(N, W, nct, mode, M)) status = kSubError;
+            if (!bellman_ford(N, W, nct, nz, mode, M)) status = kSubError;
             const int64_t dz = key_cost(W.key[n]);
             for (int v = lane(); v < n; v += kWave) {
                 int64_t d = key_cost(W.key[v]) - dz;
@@ -593,7 +704,7 @@ __global__ void __launch_bounds__(256) k_sub_reduce(SubNet N, SubIO io) {
 
 // ---------------------------------------------------------------------------------------
 size_t sub_lds_bytes(int n, int m, int n_slots) {
-    size_t off[14];
+    size_t off[15];
     return sub_lds_layout(n, m, n_slots, off);
 }
 

@@ -42,7 +42,7 @@ STEAL_SHARE = 0.4   # PROPORTION_OF_SHARE (DDSolver.h:22-38)
 class DDSolver:
     def __init__(self, network_path: Optional[str] = None, n_workers: int = 1, device: int = 0,
                  max_batch: int = 4096, batch_nodes: int = 0, engine=None, group=None, verbose: bool = True,
-                 progress: float = 0.0, max_rounds: int = 0, dive_batch: int = 64):
+                 progress: float = 0.0, max_rounds: int = 0, dive_batch: int = 64, time_budget: float = 0.0):
         """n_workers is accepted for API compatibility with the reference (threads there);
         the parallelism here is the batch of ``batch_nodes`` (<= max_batch) records per
         round and one rank per GPU."""
@@ -56,12 +56,16 @@ class DDSolver:
         self.verbose = verbose
         self.progress = progress        # seconds between progress lines on stderr (0: none)
         self.max_rounds = max_rounds    # safety cap for tests (0: none); hitting it raises
-        # Until the first exact leaf closes there is no cut to prune with (and at most the
-        # seeded incumbent):
+        # Until the first exact leaf is reached there is no cut to prune with (and at most
+        # the seeded incumbent):
         # rounds of dive_batch records from the top of the stack go depth-first to the
         # exact leaves (like the reference's LIFO workers) instead of relaxing wide layers
         # of siblings that nothing can prune yet.
         self.dive_batch = dive_batch
+        # stop after this many seconds (0: none) with complete = False -- for throughput
+        # measurements of searches that would run for hours
+        self.time_budget = time_budget
+        self.complete = False
         self.counters = {}
         self.rounds = 0
         self.seconds = 0.0
@@ -143,13 +147,15 @@ class DDSolver:
         self.rounds = 0
         t_last = time.perf_counter()
         diving = self.dive_batch > 0
+        self.complete = False
+        t_start = time.perf_counter()
         while True:
             batch = self.batch_nodes
             if diving:
                 batch = self.dive_batch if not batch else min(batch, self.dive_batch)
             z, st = eng.bnb_step(z, batch)
-            if diving and int(getattr(st, "exact_closed", 0) if not isinstance(st, dict) else st["exact_closed"]) > 0:
-                diving = False
+            if diving and int(getattr(st, "exact", 0) if not isinstance(st, dict) else st["exact"]) > 0:
+                diving = False   # the dive reached exact leaves: cuts exist from here on
             self.rounds += 1
             if self.progress and time.perf_counter() - t_last > self.progress:
                 t_last = time.perf_counter()
@@ -160,8 +166,12 @@ class DDSolver:
                 raise RuntimeError(f"DDSolver: no termination within {self.max_rounds} rounds (z={z!r})")
             for k in keys:
                 self.counters[k] += int(getattr(st, k) if not isinstance(st, dict) else st[k])
+            over = self.time_budget > 0 and time.perf_counter() - t_start > self.time_budget
             if dist is None:
                 if eng.frontier_size() == 0:
+                    self.complete = True
+                    break
+                if over:
                     break
                 continue
             z = self._allreduce_max(dist, z)
@@ -169,6 +179,11 @@ class DDSolver:
             sizes = [None] * dist.get_world_size(self.group)
             dist.all_gather_object(sizes, eng.frontier_size(), group=self.group)
             if sum(sizes) == 0:
+                self.complete = True
+                break
+            flags = [None] * dist.get_world_size(self.group)
+            dist.all_gather_object(flags, over, group=self.group)
+            if any(flags):
                 break
             self._rebalance(dist, sizes)
         return z
