@@ -456,7 +456,21 @@ bool sgufp_ctx::sub_init() {
     if (sub_ready) return true;
     const Network &N = net;
     const int n = N.n, m = N.m, S = N.S;
-    if (sub_lds_bytes(n, m, N.n_slots) > 160 * 1024) { err = "network too large for the LDS subproblem"; return false; }
+    // chain records keep node / arc ids and bounds in 16 bits (ids already are: Cut.h:342-344)
+    if (n > 32767 || m > 32767) { err = "subproblem: more than 32767 nodes or arcs"; return false; }
+    for (size_t i = 0; i < N.lb.size(); i++)
+        if (N.lb[i] < -32768 || N.lb[i] > 32767 || N.ub[i] < -32768 || N.ub[i] > 32767) {
+            err = "subproblem: arc bounds outside 16 bits";
+            return false;
+        }
+    std::vector<int32_t> zlist;   // free-supply / free-demand nodes (no conservation row)
+    for (int v = 0; v < n; v++) {
+        const bool src = N.in_arcs[v].empty(), snk = N.out_arcs[v].empty();
+        if ((src || snk) && !(src && snk))
+            zlist.push_back((int32_t)((uint32_t)v | (src ? 1u << 30 : 0u) | (snk ? 1u << 29 : 0u)));
+    }
+    const int nz = (int)zlist.size();
+    if (sub_lds_bytes(n, m, N.n_slots, nz) > 160 * 1024) { err = "network too large for the LDS subproblem"; return false; }
     std::vector<int32_t> inner(n), arc_layer(m, -1), lb((size_t)S * m), ub((size_t)S * m), rew(m);
     std::vector<uint8_t> vb(n), in8(n);
     std::vector<int32_t> in_off(n + 1, 0), out_off(n + 1, 0), in_list, out_list;
@@ -478,22 +492,23 @@ bool sgufp_ctx::sub_init() {
             ub[(size_t)s * m + a] = N.ub[(size_t)a * S + s];
         }
     }
-    int32_t *d_tail, *d_head, *d_layer, *d_lb, *d_ub, *d_rew, *d_ioff, *d_il, *d_ooff, *d_ol, *d_soff, *d_shead;
+    int32_t *d_tail, *d_head, *d_layer, *d_lb, *d_ub, *d_rew, *d_ioff, *d_il, *d_ooff, *d_ol, *d_soff, *d_shead, *d_z;
     uint8_t *d_vb, *d_inner;
     if (!alloc(d_tail, m, "sub") || !alloc(d_head, m, "sub") || !alloc(d_layer, m, "sub") ||
         !alloc(d_lb, (size_t)S * m, "sub") || !alloc(d_ub, (size_t)S * m, "sub") || !alloc(d_rew, m, "sub") ||
         !alloc(d_ioff, n + 1, "sub") || !alloc(d_il, m, "sub") || !alloc(d_ooff, n + 1, "sub") ||
         !alloc(d_ol, m, "sub") || !alloc(d_soff, N.L + 1, "sub") || !alloc(d_shead, N.n_slots, "sub") ||
-        !alloc(d_vb, n, "sub") || !alloc(d_inner, n, "sub"))
+        !alloc(d_vb, n, "sub") || !alloc(d_inner, n, "sub") || !alloc(d_z, std::max(nz, 1), "sub"))
         return false;
     if (!upload(d_tail, N.tail.data(), m) || !upload(d_head, N.head.data(), m) || !upload(d_layer, arc_layer.data(), m) ||
         !upload(d_lb, lb.data(), lb.size()) || !upload(d_ub, ub.data(), ub.size()) || !upload(d_rew, rew.data(), m) ||
         !upload(d_ioff, in_off.data(), in_off.size()) || !upload(d_il, in_list.data(), in_list.size()) ||
         !upload(d_ooff, out_off.data(), out_off.size()) || !upload(d_ol, out_list.data(), out_list.size()) ||
         !upload(d_soff, N.slot_off.data(), N.slot_off.size()) || !upload(d_shead, N.slot_head.data(), N.slot_head.size()) ||
-        !upload(d_vb, vb.data(), n) || !upload(d_inner, in8.data(), n) || !sync())
+        !upload(d_vb, vb.data(), n) || !upload(d_inner, in8.data(), n) || (nz && !upload(d_z, zlist.data(), nz)) ||
+        !sync())
         return false;
-    sn.n = n; sn.m = m; sn.S = S; sn.L = N.L; sn.n_slots = N.n_slots;
+    sn.n = n; sn.m = m; sn.S = S; sn.L = N.L; sn.n_slots = N.n_slots; sn.nz = nz; sn.zlist = d_z;
     sn.tail = d_tail; sn.head = d_head; sn.vbar = d_vb; sn.inner = d_inner; sn.arc_layer = d_layer;
     sn.lb = d_lb; sn.ub = d_ub; sn.reward = d_rew;
     sn.in_off = d_ioff; sn.in_list = d_il; sn.out_off = d_ooff; sn.out_list = d_ol;

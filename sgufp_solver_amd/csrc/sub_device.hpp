@@ -16,7 +16,7 @@ enum SubStatus : int32_t {
 };
 
 struct SubNet {
-    int n, m, S, L, n_slots;
+    int n, m, S, L, n_slots, nz;
     const int32_t SGUFP_GBL *tail;       // [m]
     const int32_t SGUFP_GBL *head;       // [m]
     const uint8_t SGUFP_GBL *vbar;       // [n]
@@ -31,6 +31,7 @@ struct SubNet {
     const int32_t SGUFP_GBL *out_list;   // [m]
     const int32_t SGUFP_GBL *slot_off;   // [L+1]
     const int32_t SGUFP_GBL *slot_head;  // [n_slots]
+    const int32_t SGUFP_GBL *zlist;      // [nz] free-supply / free-demand nodes: v | src << 30 | snk << 29
 };
 
 struct SubIO {

@@ -44,34 +44,58 @@ constexpr int64_t kInf = INT64_MAX / 4;
 constexpr int kHopBits = 16;
 constexpr int kMaxChain = 64;      // arcs per chain (V-bar nodes in a row + 1)
 
+// Chain k of the contracted network lives in two 64-bit LDS words, so a Bellman-Ford pass
+// reads one arc with two ds_read_b64:
+//   cta: tail:16 | head:16 | reward sum:32          (-1 ends as 0xFFFF)
+//   ctb: max l:16 | min u:16 | flow x:16 | first arc:16
+// Node / arc ids fit 16 bits (Cut.h:342-344 packs them so); the host checks the bounds.
 struct SubLds {
-    LDS int32_t *dec;       // [m] decision at the head (out-arc id, -1 none, -2 head not V-bar)
-    LDS int32_t *chosen;    // [m] in-arc that chose this out-arc of a V-bar node, -1 none
-    LDS int32_t *ct_first;  // [m] first arc of chain k (chains indexed by start rank)
-    LDS int32_t *ct_t;      // [m] tail node (-1: chain starts at an unchosen V-bar out-arc)
-    LDS int32_t *ct_h;      // [m] head node (-1: chain ends at an unmatched V-bar in-arc)
-    LDS int32_t *ct_L, *ct_U, *ct_R, *ct_x;
-    LDS int64_t *key;       // [n+2] Bellman-Ford keys (cost << 16 | hops)
+    LDS int16_t *dec;       // [m] decision at the head (out-arc id, -1 none, -2 head not V-bar)
+    LDS uint64_t *cta;      // [m] chains (indexed by the rank of their first arc)
+    LDS uint64_t *ctb;      // [m]
+    LDS int32_t *chosen;    // [m] in-arc that chose this out-arc of a V-bar node (phases 1-2;
+                            //     aliases key / pred / coef)
+    LDS int64_t *key;       // [n+2] Bellman-Ford keys (cost << 16 | hops); then alpha in place
+    LDS int64_t *alpha;     // == key: dual node potentials after the last Bellman-Ford
     LDS int32_t *pred;      // [n+2]
-    LDS int64_t *alpha;     // [n+1] dual node potentials
     LDS double *coef;       // [n_slots]
+    LDS int32_t *zlist;     // [nz] free-supply / free-demand nodes: v | src << 30 | snk << 29
     LDS int32_t *misc;      // [8] flags
-    LDS int32_t *zlist;     // [n] free-supply / free-demand nodes: v | src << 30 | snk << 29
 };
 
 __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-__host__ __device__ inline size_t sub_lds_layout(int n, int m, int n_slots, size_t *off) {
+__host__ __device__ inline size_t sub_lds_layout(int n, int m, int n_slots, int nz, size_t *off) {
     size_t o = 0;
-    for (int k = 0; k < 9; k++) { off[k] = o; o = a16(o + (size_t)m * 4); }
-    off[9] = o; o = a16(o + (size_t)(n + 2) * 8);
-    off[10] = o; o = a16(o + (size_t)(n + 2) * 4);
-    off[11] = o; o = a16(o + (size_t)(n + 1) * 8);
-    off[12] = o; o = a16(o + (size_t)n_slots * 8);
-    off[13] = o; o = a16(o + 8 * 4);
-    off[14] = o; o = a16(o + (size_t)n * 4);
+    off[0] = o; o = a16(o + (size_t)m * 2);
+    off[1] = o; o = a16(o + (size_t)m * 8);
+    off[2] = o; o = a16(o + (size_t)m * 8);
+    const size_t u0 = o;                         // union: chosen | key, pred, coef
+    off[3] = o; o = a16(o + (size_t)(n + 2) * 8);
+    off[4] = o; o = a16(o + (size_t)(n + 2) * 4);
+    off[5] = o; o = a16(o + (size_t)n_slots * 8);
+    if (o < a16(u0 + (size_t)m * 4)) o = a16(u0 + (size_t)m * 4);
+    off[6] = o; o = a16(o + (size_t)nz * 4);
+    off[7] = o; o = a16(o + 8 * 4);
     return o;
 }
+
+__device__ __forceinline__ int ch_t(uint64_t a) { return (int)(int16_t)(uint16_t)a; }
+__device__ __forceinline__ int ch_h(uint64_t a) { return (int)(int16_t)(uint16_t)(a >> 16); }
+__device__ __forceinline__ int ch_R(uint64_t a) { return (int)(int32_t)(uint32_t)(a >> 32); }
+__device__ __forceinline__ int ch_L(uint64_t b) { return (int)(int16_t)(uint16_t)b; }
+__device__ __forceinline__ int ch_U(uint64_t b) { return (int)(int16_t)(uint16_t)(b >> 16); }
+__device__ __forceinline__ int ch_x(uint64_t b) { return (int)(int16_t)(uint16_t)(b >> 32); }
+__device__ __forceinline__ int ch_first(uint64_t b) { return (int)(int16_t)(uint16_t)(b >> 48); }
+__device__ __forceinline__ uint64_t pack_a(int t, int h, int R) {
+    return (uint64_t)(uint16_t)t | (uint64_t)(uint16_t)h << 16 | (uint64_t)(uint32_t)R << 32;
+}
+__device__ __forceinline__ uint64_t pack_b(int L, int U, int x, int first) {
+    return (uint64_t)(uint16_t)L | (uint64_t)(uint16_t)U << 16 | (uint64_t)(uint16_t)x << 32 |
+           (uint64_t)(uint16_t)first << 48;
+}
+// the flow field of chain k (lane 0 augments)
+__device__ __forceinline__ LDS int16_t *ch_xp(const SubLds &W, int k) { return (LDS int16_t *)&W.ctb[k] + 2; }
 
 __device__ inline bool is_src(const SubNet &N, int v) { return N.in_off[v + 1] == N.in_off[v]; }
 __device__ inline bool is_snk(const SubNet &N, int v) { return N.out_off[v + 1] == N.out_off[v]; }
@@ -99,9 +123,10 @@ template <typename F>
 __device__ inline void for_residual(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M, F visit) {
     // contracted arcs: code 2k (forward), 2k+1 (backward)
     for (int k = lane(); k < nct; k += kWave) {
-        const int t = W.ct_t[k], h = W.ct_h[k];
+        const uint64_t ca = W.cta[k], cb = W.ctb[k];
+        const int t = ch_t(ca), h = ch_h(ca);
         if (t < 0 || h < 0) continue;
-        const int64_t x = W.ct_x[k], L = W.ct_L[k], U = W.ct_U[k], R = W.ct_R[k];
+        const int64_t x = ch_x(cb), L = ch_L(cb), U = ch_U(cb), R = ch_R(ca);
         if (mode == kPotPlain) {
             if (x < U) visit(t, h, -R, 2 * k);
             if (x > L) visit(h, t, R, 2 * k + 1);
@@ -110,7 +135,7 @@ __device__ inline void for_residual(const SubNet &N, const SubLds &W, int nct, i
             if (x > 0) visit(h, t, R + (x <= L ? M : 0), 2 * k + 1);
         }
     }
-    // Z arcs: code 2m + 2v (+1), from the LDS list of non-inner nodes (built once per wave)
+    // Z arcs: code 2m + 2v (+1), from the LDS list of non-inner nodes
     for (int i = lane(); i < nz; i += kWave) {
         const uint32_t e = (uint32_t)W.zlist[i];
         const int v = (int)(e & 0x1FFFFFFFu);
@@ -149,9 +174,10 @@ __device__ inline uint32_t bf_pass(const SubNet &N, const SubLds &W, int nct, in
             const int k = base + u * kWave + lane();
             const bool ok = k < nct;
             const int kk = ok ? k : 0;
-            t[u] = ok ? W.ct_t[kk] : -1;
-            h[u] = ok ? W.ct_h[kk] : -1;
-            x[u] = W.ct_x[kk]; L[u] = W.ct_L[kk]; U[u] = W.ct_U[kk]; R[u] = W.ct_R[kk];
+            const uint64_t ca = W.cta[kk], cb = W.ctb[kk];
+            t[u] = ok ? ch_t(ca) : -1;
+            h[u] = ok ? ch_h(ca) : -1;
+            x[u] = ch_x(cb); L[u] = ch_L(cb); U[u] = ch_U(cb); R[u] = ch_R(ca);
         }
 #pragma unroll
         for (int u = 0; u < UNR; u++) {
@@ -274,13 +300,14 @@ __device__ ChainOut assemble_chain(const SubNet &N, const SubLds &W, int k, int 
     ChainOut o{0, 0};
     int arcs[kMaxChain];
     int len = 0;
-    for (int a = W.ct_first[k]; a >= 0 && len < kMaxChain;) {
+    const uint64_t ca = W.cta[k], cb = W.ctb[k];
+    for (int a = ch_first(cb); a >= 0 && len < kMaxChain;) {
         arcs[len++] = a;
         if (!N.vbar[N.head[a]]) break;
         a = W.dec[a];
     }
     if (len >= kMaxChain) { ok = false; return o; }
-    const int t = W.ct_t[k], h = W.ct_h[k];
+    const int t = ch_t(ca), h = ch_h(ca);
     const size_t so = (size_t)s * N.m;
     auto rew = [&](int a) -> int64_t { return ray_mode ? 0 : (int64_t)N.reward[a]; };
     auto cost = [&](int a, int64_t e) -> int64_t { return e >= 0 ? (int64_t)N.ub[so + a] * e : (int64_t)N.lb[so + a] * e; };
@@ -385,24 +412,19 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     const int S = N.S;
     const int p = blockIdx.x / S, s = blockIdx.x - p * S;
     if (p >= io.n_paths) return;
-    size_t off[15];
-    sub_lds_layout(N.n, N.m, N.n_slots, off);
+    size_t off[8];
+    sub_lds_layout(N.n, N.m, N.n_slots, N.nz, off);
     SubLds W;
-    W.dec = (LDS int32_t *)(smem + off[0]);
-    W.chosen = (LDS int32_t *)(smem + off[1]);
-    W.ct_first = (LDS int32_t *)(smem + off[2]);
-    W.ct_t = (LDS int32_t *)(smem + off[3]);
-    W.ct_h = (LDS int32_t *)(smem + off[4]);
-    W.ct_L = (LDS int32_t *)(smem + off[5]);
-    W.ct_U = (LDS int32_t *)(smem + off[6]);
-    W.ct_R = (LDS int32_t *)(smem + off[7]);
-    W.ct_x = (LDS int32_t *)(smem + off[8]);
-    W.key = (LDS int64_t *)(smem + off[9]);
-    W.pred = (LDS int32_t *)(smem + off[10]);
-    W.alpha = (LDS int64_t *)(smem + off[11]);
-    W.coef = (LDS double *)(smem + off[12]);
-    W.misc = (LDS int32_t *)(smem + off[13]);
-    W.zlist = (LDS int32_t *)(smem + off[14]);
+    W.dec = (LDS int16_t *)(smem + off[0]);
+    W.cta = (LDS uint64_t *)(smem + off[1]);
+    W.ctb = (LDS uint64_t *)(smem + off[2]);
+    W.chosen = (LDS int32_t *)(smem + off[3]);
+    W.key = (LDS int64_t *)(smem + off[3]);
+    W.alpha = W.key;
+    W.pred = (LDS int32_t *)(smem + off[4]);
+    W.coef = (LDS double *)(smem + off[5]);
+    W.zlist = (LDS int32_t *)(smem + off[6]);
+    W.misc = (LDS int32_t *)(smem + off[7]);
     const int n = N.n, m = N.m;
     const size_t so = (size_t)s * m;
     const int64_t poff = io.path_off[p], plen = io.path_off[p + 1] - poff;
@@ -419,9 +441,8 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
             d = (l >= 0 && l < plen) ? (int)io.paths[poff + l] : -1;
             if (d < -1 || d >= m || (d >= 0 && N.tail[d] != q)) d = -3;   // not an out-arc of q
         }
-        W.dec[a] = d;
+        W.dec[a] = (int16_t)d;
     }
-    for (int v = lane(); v < N.n_slots; v += kWave) W.coef[v] = 0.0;
     wave_lds_sync();
     for (int a = lane(); a < m; a += kWave) {
         const int d = W.dec[a];
@@ -438,28 +459,17 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
         bool st = false;
         if (a < m) st = !N.vbar[N.tail[a]] || W.chosen[a] < 0;
         const uint32_t incl = wave_scan_incl(st ? 1u : 0u);
-        if (st) W.ct_first[nct + (int)incl - 1] = a;
+        if (st) W.ctb[nct + (int)incl - 1] = pack_b(0, 0, 0, a);
         nct += (int)__builtin_amdgcn_readlane((int)incl, kWave - 1);
     }
     wave_lds_sync();
-    // free-supply / free-demand nodes (structural; read by every Bellman-Ford pass from LDS)
-    int nz = 0;
-    for (int base = 0; base < n; base += kWave) {
-        const int v = base + lane();
-        bool z = false;
-        uint32_t e = 0;
-        if (v < n && !N.inner[v]) {
-            const bool src = is_src(N, v), snk = is_snk(N, v);
-            z = !(src && snk);
-            e = (uint32_t)v | (src ? 1u << 30 : 0u) | (snk ? 1u << 29 : 0u);
-        }
-        const uint32_t incl = wave_scan_incl(z ? 1u : 0u);
-        if (z) W.zlist[nz + (int)incl - 1] = (int32_t)e;
-        nz += (int)__builtin_amdgcn_readlane((int)incl, kWave - 1);
-    }
+    // free-supply / free-demand nodes (structural, from the host; read by every pass)
+    const int nz = N.nz;
+    for (int i = lane(); i < nz; i += kWave) W.zlist[i] = N.zlist[i];
     int first_bad = INT_MAX;   // first chain (rank) that makes the scenario infeasible up front
     for (int k = lane(); k < nct; k += kWave) {
-        int a = W.ct_first[k];
+        int a = ch_first(W.ctb[k]);
+        const int first = a;
         const int t0 = N.tail[a];
         int L = N.lb[so + a], U = N.ub[so + a], R = N.reward[a];
         int h = -1, len = 1;
@@ -475,16 +485,15 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
             R += N.reward[a];
         }
         const int t = N.vbar[t0] ? -1 : t0;
-        W.ct_t[k] = t;
-        W.ct_h[k] = h;
-        W.ct_L[k] = L;
-        W.ct_U[k] = U;
-        W.ct_R[k] = R;
-        W.ct_x[k] = 0;
+        W.cta[k] = pack_a(t, h, R);
+        W.ctb[k] = pack_b(L, U, 0, first);
         const bool complete = t >= 0 && h >= 0;
         if ((complete && L > U) || (!complete && L > 0)) first_bad = min(first_bad, k);
     }
     first_bad = lane_reduce<1>(first_bad, [](int x, int y) { return x < y ? x : y; });
+    wave_lds_sync();
+    // chosen is dead from here: its space holds the coefficients (and keys / predecessors)
+    for (int v = lane(); v < N.n_slots; v += kWave) W.coef[v] = 0.0;
     wave_lds_sync();
     if (W.misc[0]) {
         if (lane() == 0) { io.status[b] = kSubError; io.obj[b] = 0; io.dual[b] = 0; io.rhs[b] = 0; }
@@ -495,9 +504,10 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     int status = kSubOptimal;
     int64_t M = 1;
     for (int k = lane(); k < nct; k += kWave) {
-        if (W.ct_t[k] >= 0 && W.ct_h[k] >= 0) {
-            const int64_t R = W.ct_R[k];
-            M += 2 * (R < 0 ? -R : R) * ((int64_t)W.ct_U[k] + 1);
+        const uint64_t ca = W.cta[k];
+        if (ch_t(ca) >= 0 && ch_h(ca) >= 0) {
+            const int64_t R = ch_R(ca);
+            M += 2 * (R < 0 ? -R : R) * ((int64_t)ch_U(W.ctb[k]) + 1);
         }
     }
     M = lane_reduce<1>(M, [](int64_t x, int64_t y) { return x + y; }) - (kWave - 1);
@@ -509,8 +519,8 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
         status = kSubInfeasible;
         ray_chain = first_bad;
         const int k = first_bad;
-        int a = W.ct_first[k];
-        const bool complete = W.ct_t[k] >= 0 && W.ct_h[k] >= 0;
+        int a = ch_first(W.ctb[k]);
+        const bool complete = ch_t(W.cta[k]) >= 0 && ch_h(W.cta[k]) >= 0;
         int bp = a, bq = a;
         int64_t bl = N.lb[so + a], bu = N.ub[so + a];
         for (int len = 0; len < kMaxChain; len++) {
@@ -546,10 +556,11 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
                     if (code == INT_MAX) break;
                     if (code >= 2 * m) { v = (code & 1) ? (code - 2 * m - 1) / 2 : n; continue; }
                     const int k = code >> 1;
-                    const int64_t x = W.ct_x[k], L = W.ct_L[k], U = W.ct_U[k];
+                    const uint64_t ca = W.cta[k], cb = W.ctb[k];
+                    const int64_t x = ch_x(cb), L = ch_L(cb), U = ch_U(cb);
                     const int64_t cap = (code & 1) ? (x > L ? x - L : x) : (x < L ? L - x : U - x);
                     delta = cap < delta ? cap : delta;
-                    v = (code & 1) ? W.ct_h[k] : W.ct_t[k];
+                    v = (code & 1) ? ch_h(ca) : ch_t(ca);
                 }
                 if (v != n || delta <= 0 || delta >= kInf) W.misc[fresh ? 1 : 2] = 1;
                 else {
@@ -558,8 +569,9 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
                         const int code = W.pred[v];
                         if (code >= 2 * m) { v = (code & 1) ? (code - 2 * m - 1) / 2 : n; continue; }
                         const int k = code >> 1;
-                        if (code & 1) { W.ct_x[k] -= (int32_t)delta; v = W.ct_h[k]; }
-                        else { W.ct_x[k] += (int32_t)delta; v = W.ct_t[k]; }
+                        const uint64_t ca = W.cta[k];
+                        if (code & 1) { *ch_xp(W, k) -= (int16_t)delta; v = ch_h(ca); }
+                        else { *ch_xp(W, k) += (int16_t)delta; v = ch_t(ca); }
                     }
                 }
             }
@@ -588,9 +600,10 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
         // lower bounds met?
         int unmet = 0;
         for (int k = lane(); k < nct; k += kWave) {
-            if (W.ct_t[k] >= 0 && W.ct_h[k] >= 0) {
-                if (W.ct_x[k] < W.ct_L[k]) unmet = 1;
-                primal += (int64_t)W.ct_R[k] * W.ct_x[k];
+            const uint64_t ca = W.cta[k], cb = W.ctb[k];
+            if (ch_t(ca) >= 0 && ch_h(ca) >= 0) {
+                if (ch_x(cb) < ch_L(cb)) unmet = 1;
+                primal += (int64_t)ch_R(ca) * ch_x(cb);
             }
         }
         primal = lane_reduce<1>(primal, [](int64_t x, int64_t y) { return x + y; });
@@ -703,14 +716,14 @@ __global__ void __launch_bounds__(256) k_sub_reduce(SubNet N, SubIO io) {
 }
 
 // ---------------------------------------------------------------------------------------
-size_t sub_lds_bytes(int n, int m, int n_slots) {
-    size_t off[15];
-    return sub_lds_layout(n, m, n_slots, off);
+size_t sub_lds_bytes(int n, int m, int n_slots, int nz) {
+    size_t off[8];
+    return sub_lds_layout(n, m, n_slots, nz, off);
 }
 
 hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st) {
     if (io.n_paths <= 0) return hipSuccess;
-    const size_t lds = sub_lds_bytes(N.n, N.m, N.n_slots);
+    const size_t lds = sub_lds_bytes(N.n, N.m, N.n_slots, N.nz);
     hipLaunchKernelGGL(k_sub_scenario, dim3((unsigned)io.n_paths * N.S), dim3(kWave), lds, st, N, io);
     hipLaunchKernelGGL(k_sub_reduce, dim3((unsigned)io.n_paths), dim3(256), 0, st, N, io);
     return hipGetLastError();
