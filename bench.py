@@ -116,7 +116,17 @@ def bnb_main(args):
     work = tempfile.mkdtemp(prefix=f"sgufp_bnb_r{rank}_")
     net = os.path.join(work, "net.txt")
     inst.write(net)
-    solver = DDSolver(net, device=local, max_batch=args.nodes, verbose=False, time_budget=2.0)
+    # a round (and its refinement loops) can run for minutes: keep a heartbeat on stderr
+    import threading
+    t_hb = time.perf_counter()
+
+    def heartbeat():
+        while True:
+            time.sleep(20.0)
+            print(f"bnb: running, {time.perf_counter() - t_hb:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
+    solver = DDSolver(net, device=local, max_batch=args.nodes, verbose=False, time_budget=2.0, progress=10.0)
     solver.start_solver(DOUBLE_MIN)                        # warm-up (kernels, allocations)
     solver.eng.clear_cuts()
     solver.eng.set_timing(True)

@@ -1,6 +1,7 @@
 // C ABI of libsgufp_hip.so (declared in include/sgufp_hip.h): context, device
 // memory, cut-pool densification, batch staging and result retrieval.
 #include "ctx.hpp"
+#include <algorithm>
 
 
 namespace {
@@ -470,6 +471,24 @@ bool sgufp_ctx::sub_init() {
             zlist.push_back((int32_t)((uint32_t)v | (src ? 1u << 30 : 0u) | (snk ? 1u << 29 : 0u)));
     }
     const int nz = (int)zlist.size();
+    // chains are numbered in the topological order of their tails, so that one sweep in
+    // chain order carries a label down a whole run of forward arcs (Kahn's order; on a
+    // cycle the remaining nodes follow in id order -- only the speed depends on it)
+    std::vector<int32_t> rank(n, -1), indeg(n, 0), arc_topo(m);
+    {
+        std::vector<int32_t> q;
+        for (int v = 0; v < n; v++) indeg[v] = (int32_t)N.in_arcs[v].size();
+        for (int v = 0; v < n; v++) if (indeg[v] == 0) q.push_back(v);
+        int r = 0;
+        for (size_t i = 0; i < q.size(); i++) {
+            const int v = q[i];
+            rank[v] = r++;
+            for (int a : N.out_arcs[v]) if (--indeg[N.head[a]] == 0) q.push_back(N.head[a]);
+        }
+        for (int v = 0; v < n; v++) if (rank[v] < 0) rank[v] = r++;
+        for (int a = 0; a < m; a++) arc_topo[a] = a;
+        std::stable_sort(arc_topo.begin(), arc_topo.end(), [&](int a, int b) { return rank[N.tail[a]] < rank[N.tail[b]]; });
+    }
     if (sub_lds_bytes(n, m, N.n_slots, nz) > 160 * 1024) { err = "network too large for the LDS subproblem"; return false; }
     std::vector<int32_t> inner(n), arc_layer(m, -1), lb((size_t)S * m), ub((size_t)S * m), rew(m);
     std::vector<uint8_t> vb(n), in8(n);
@@ -492,23 +511,24 @@ bool sgufp_ctx::sub_init() {
             ub[(size_t)s * m + a] = N.ub[(size_t)a * S + s];
         }
     }
-    int32_t *d_tail, *d_head, *d_layer, *d_lb, *d_ub, *d_rew, *d_ioff, *d_il, *d_ooff, *d_ol, *d_soff, *d_shead, *d_z;
+    int32_t *d_tail, *d_head, *d_layer, *d_lb, *d_ub, *d_rew, *d_ioff, *d_il, *d_ooff, *d_ol, *d_soff, *d_shead, *d_z, *d_topo;
     uint8_t *d_vb, *d_inner;
     if (!alloc(d_tail, m, "sub") || !alloc(d_head, m, "sub") || !alloc(d_layer, m, "sub") ||
         !alloc(d_lb, (size_t)S * m, "sub") || !alloc(d_ub, (size_t)S * m, "sub") || !alloc(d_rew, m, "sub") ||
         !alloc(d_ioff, n + 1, "sub") || !alloc(d_il, m, "sub") || !alloc(d_ooff, n + 1, "sub") ||
         !alloc(d_ol, m, "sub") || !alloc(d_soff, N.L + 1, "sub") || !alloc(d_shead, N.n_slots, "sub") ||
-        !alloc(d_vb, n, "sub") || !alloc(d_inner, n, "sub") || !alloc(d_z, std::max(nz, 1), "sub"))
+        !alloc(d_vb, n, "sub") || !alloc(d_inner, n, "sub") || !alloc(d_z, std::max(nz, 1), "sub") ||
+        !alloc(d_topo, m, "sub"))
         return false;
     if (!upload(d_tail, N.tail.data(), m) || !upload(d_head, N.head.data(), m) || !upload(d_layer, arc_layer.data(), m) ||
         !upload(d_lb, lb.data(), lb.size()) || !upload(d_ub, ub.data(), ub.size()) || !upload(d_rew, rew.data(), m) ||
         !upload(d_ioff, in_off.data(), in_off.size()) || !upload(d_il, in_list.data(), in_list.size()) ||
         !upload(d_ooff, out_off.data(), out_off.size()) || !upload(d_ol, out_list.data(), out_list.size()) ||
         !upload(d_soff, N.slot_off.data(), N.slot_off.size()) || !upload(d_shead, N.slot_head.data(), N.slot_head.size()) ||
-        !upload(d_vb, vb.data(), n) || !upload(d_inner, in8.data(), n) || (nz && !upload(d_z, zlist.data(), nz)) ||
+        !upload(d_vb, vb.data(), n) || !upload(d_inner, in8.data(), n) || (nz && !upload(d_z, zlist.data(), nz)) || !upload(d_topo, arc_topo.data(), m) ||
         !sync())
         return false;
-    sn.n = n; sn.m = m; sn.S = S; sn.L = N.L; sn.n_slots = N.n_slots; sn.nz = nz; sn.zlist = d_z;
+    sn.n = n; sn.m = m; sn.S = S; sn.L = N.L; sn.n_slots = N.n_slots; sn.nz = nz; sn.zlist = d_z; sn.arc_topo = d_topo;
     sn.tail = d_tail; sn.head = d_head; sn.vbar = d_vb; sn.inner = d_inner; sn.arc_layer = d_layer;
     sn.lb = d_lb; sn.ub = d_ub; sn.reward = d_rew;
     sn.in_off = d_ioff; sn.in_list = d_il; sn.out_off = d_ooff; sn.out_list = d_ol;

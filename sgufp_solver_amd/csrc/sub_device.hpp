@@ -32,6 +32,7 @@ struct SubNet {
     const int32_t SGUFP_GBL *slot_off;   // [L+1]
     const int32_t SGUFP_GBL *slot_head;  // [n_slots]
     const int32_t SGUFP_GBL *zlist;      // [nz] free-supply / free-demand nodes: v | src << 30 | snk << 29
+    const int32_t SGUFP_GBL *arc_topo;   // [m] arcs by topological rank of their tail (chain order)
 };
 
 struct SubIO {

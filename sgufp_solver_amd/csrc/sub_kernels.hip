@@ -43,6 +43,7 @@ namespace {
 constexpr int64_t kInf = INT64_MAX / 4;
 constexpr int kHopBits = 16;
 constexpr int kMaxChain = 64;      // arcs per chain (V-bar nodes in a row + 1)
+constexpr int64_t kNoPred = INT64_MAX;
 
 // Chain k of the contracted network lives in two 64-bit LDS words, so a Bellman-Ford pass
 // reads one arc with two ds_read_b64:
@@ -54,11 +55,12 @@ struct SubLds {
     LDS uint64_t *cta;      // [m] chains (indexed by the rank of their first arc)
     LDS uint64_t *ctb;      // [m]
     LDS int32_t *chosen;    // [m] in-arc that chose this out-arc of a V-bar node (phases 1-2;
-                            //     aliases key / pred / coef)
+                            //     aliases key / pred)
     LDS int64_t *key;       // [n+2] Bellman-Ford keys (cost << 16 | hops); then alpha in place
     LDS int64_t *alpha;     // == key: dual node potentials after the last Bellman-Ford
-    LDS int32_t *pred;      // [n+2]
-    LDS double *coef;       // [n_slots]
+    LDS int64_t *pred;      // [n+2] code of the tight in-arc << 32 | its tail (kNoPred: none)
+    LDS int32_t *plist;     // [n+2] arc codes of the augmenting path (sink to source)
+    double GBL *coef;       // [n_slots] this (path, scenario)'s row of SubIO::coef (phase 5)
     LDS int32_t *zlist;     // [nz] free-supply / free-demand nodes: v | src << 30 | snk << 29
     LDS int32_t *misc;      // [8] flags
 };
@@ -70,10 +72,11 @@ __host__ __device__ inline size_t sub_lds_layout(int n, int m, int n_slots, int 
     off[0] = o; o = a16(o + (size_t)m * 2);
     off[1] = o; o = a16(o + (size_t)m * 8);
     off[2] = o; o = a16(o + (size_t)m * 8);
-    const size_t u0 = o;                         // union: chosen | key, pred, coef
+    const size_t u0 = o;                         // union: chosen | key, pred, plist
     off[3] = o; o = a16(o + (size_t)(n + 2) * 8);
-    off[4] = o; o = a16(o + (size_t)(n + 2) * 4);
-    off[5] = o; o = a16(o + (size_t)n_slots * 8);
+    off[4] = o; o = a16(o + (size_t)(n + 2) * 8);
+    off[5] = o;
+    off[8] = o; o = a16(o + (size_t)(n + 2) * 4);
     if (o < a16(u0 + (size_t)m * 4)) o = a16(u0 + (size_t)m * 4);
     off[6] = o; o = a16(o + (size_t)nz * 4);
     off[7] = o; o = a16(o + 8 * 4);
@@ -104,10 +107,6 @@ __device__ inline int slot_of(const SubNet &N, int layer, int j) {
     for (int s = N.slot_off[layer]; s < N.slot_off[layer + 1]; s++)
         if (N.slot_head[s] == j) return s;
     return -1;
-}
-
-__device__ inline void lds_add(LDS double *p, double v) {
-    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -150,65 +149,131 @@ __device__ inline void for_residual(const SubNet &N, const SubLds &W, int nct, i
     }
 }
 
-// One Bellman-Ford pass over the residual arcs of for_residual (same arcs, same costs).
-// The chain arcs are relaxed UNR per lane at a time: all chain data and both end labels are
-// loaded first, then the candidate labels go out as LDS atomic minima.  Labels read inside
-// a pass may be a pass old (Jacobi order); the fixed point -- shortest (cost, hops) keys --
-// is the same, and the caller iterates until a pass changes nothing.
-__device__ inline uint32_t bf_pass(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M) {
-    constexpr int UNR = 4;
+// The residual arcs of chain group g (chains g*64 .. g*64+63, one per lane) for one
+// Bellman-Ford: ends packed tail | head << 16, forward / backward key increments
+// ((cost << 16) + 1) and which of the two arcs exist.  Flows only change between
+// Bellman-Fords, so the first kRegGroups groups live in registers for all its passes.
+constexpr int kRegGroups = 16;
+
+struct ChainArcs {
+    uint32_t th;
+    int64_t wf, wb;
+    bool fwd, bwd;
+};
+
+__device__ __forceinline__ ChainArcs chain_arcs(uint64_t ca, uint64_t cb, bool in_range, int n, int mode, int64_t M) {
+    ChainArcs c;
+    const int t = ch_t(ca), h = ch_h(ca);
+    const bool ok = in_range && t >= 0 && h >= 0;
+    c.th = ok ? ((uint32_t)t | (uint32_t)h << 16) : ((uint32_t)n | (uint32_t)n << 16);
+    const int x = ch_x(cb), L = ch_L(cb), U = ch_U(cb);
+    const int64_t R = ch_R(ca);
+    const int64_t w_f = (mode == kPotPlain) ? -R : -(R + (x < L ? M : 0));
+    const int64_t w_b = (mode == kPotPlain) ? R : R + (x <= L ? M : 0);
+    c.wf = (w_f << kHopBits) + 1;
+    c.wb = (w_b << kHopBits) + 1;
+    c.fwd = ok && x < U;
+    c.bwd = ok && (mode == kPotPlain ? x > L : x > 0);
+    return c;
+}
+
+struct ChainRegs {
+    uint32_t th[kRegGroups];
+    int64_t wf[kRegGroups], wb[kRegGroups];
+    uint32_t fmask, bmask;
+};
+
+__device__ __forceinline__ void load_chain_regs(const SubLds &W, int n, int nct, int mode, int64_t M, ChainRegs &C) {
+    C.fmask = 0;
+    C.bmask = 0;
+#pragma unroll
+    for (int g = 0; g < kRegGroups; g++) {
+        const int k = g * kWave + lane();
+        uint64_t ca = 0, cb = 0;
+        if (k < nct) { ca = W.cta[k]; cb = W.ctb[k]; }
+        const ChainArcs c = chain_arcs(ca, cb, k < nct, n, mode, M);
+        C.th[g] = c.th;
+        C.wf[g] = c.wf;
+        C.wb[g] = c.wb;
+        C.fmask |= (c.fwd ? 1u : 0u) << g;
+        C.bmask |= (c.bwd ? 1u : 0u) << g;
+    }
+}
+
+// One Bellman-Ford pass over the residual arcs of for_residual (same arcs, same costs):
+// a forward sweep over the chains in order (tails in topological order) relaxes the
+// forward residual arcs, a backward sweep in reverse order the backward ones, 64 chains
+// at a time, so a label travels down a run of forward arcs (or up a run of backward ones)
+// within one sweep.  LDS is in order within the wave, so a group's key loads see the
+// previous group's atomic minima (a pass that changes nothing read only settled keys, so
+// convergence never depends on that ordering).  The fixed point -- the shortest (cost,
+// hops) keys -- is unique, so the order changes only how many passes it takes; the caller
+// iterates until a pass changes nothing.
+__device__ inline uint32_t bf_pass(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M,
+                                   const ChainRegs &C) {
     uint32_t changed = 0;
-    auto relax = [&](int v, int64_t ku, int64_t w, int64_t kv) {
-        if (ku >= kInf) return;
-        const int64_t nk = ku + (w << kHopBits) + 1;
-        if (nk < kv) {
+    auto relax = [&](int v, int64_t nk) {
+        if (nk < W.key[v]) {
             __hip_atomic_fetch_min(&W.key[v], nk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             changed = 1;
         }
     };
-    for (int base = 0; base < nct; base += kWave * UNR) {
-        int t[UNR], h[UNR];
-        int64_t x[UNR], L[UNR], U[UNR], R[UNR], kt[UNR], kh[UNR];
-#pragma unroll
-        for (int u = 0; u < UNR; u++) {
-            const int k = base + u * kWave + lane();
-            const bool ok = k < nct;
-            const int kk = ok ? k : 0;
-            const uint64_t ca = W.cta[kk], cb = W.ctb[kk];
-            t[u] = ok ? ch_t(ca) : -1;
-            h[u] = ok ? ch_h(ca) : -1;
-            x[u] = ch_x(cb); L[u] = ch_L(cb); U[u] = ch_U(cb); R[u] = ch_R(ca);
+    // one arc of a group: both end keys in one LDS round trip, then the atomic minimum
+    auto arc = [&](uint32_t th, int64_t w, bool exists, bool forward) {
+        const int t = (int)(th & 0xFFFFu), h = (int)(th >> 16);
+        const int u = forward ? t : h, v = forward ? h : t;
+        const int64_t ku = W.key[u], kv = W.key[v];
+        const int64_t nk = ku + w;
+        if (exists && ku < kInf && nk < kv) {
+            __hip_atomic_fetch_min(&W.key[v], nk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            changed = 1;
         }
-#pragma unroll
-        for (int u = 0; u < UNR; u++) {
-            const bool arc = t[u] >= 0 && h[u] >= 0;
-            kt[u] = arc ? W.key[t[u]] : kInf;
-            kh[u] = arc ? W.key[h[u]] : kInf;
-        }
-#pragma unroll
-        for (int u = 0; u < UNR; u++) {
-            if (t[u] < 0 || h[u] < 0) continue;
-            if (mode == kPotPlain) {
-                if (x[u] < U[u]) relax(h[u], kt[u], -R[u], kh[u]);
-                if (x[u] > L[u]) relax(t[u], kh[u], R[u], kt[u]);
-            } else {
-                if (x[u] < U[u]) relax(h[u], kt[u], -(R[u] + (x[u] < L[u] ? M : 0)), kh[u]);
-                if (x[u] > 0) relax(t[u], kh[u], R[u] + (x[u] <= L[u] ? M : 0), kt[u]);
+    };
+    const int n = N.n;
+    // Z_out -> sources (SSP) / Z -> every free node (potentials), cost 0
+    {
+        const int64_t kz = W.key[n];
+        if (kz < kInf)
+            for (int i = lane(); i < nz; i += kWave) {
+                const uint32_t e = (uint32_t)W.zlist[i];
+                if (mode != kSsp || ((e >> 30) & 1u)) relax((int)(e & 0x1FFFFFFFu), kz + 1);
             }
-        }
     }
-    // Z arcs (few): one at a time
+    wave_lds_sync();
+    const int G = (nct + kWave - 1) / kWave;
+#pragma unroll
+    for (int g = 0; g < kRegGroups; g++) {
+        if (g >= G) break;
+        arc(C.th[g], C.wf[g], (C.fmask >> g) & 1u, true);
+    }
+    for (int g = kRegGroups; g < G; g++) {
+        const int k = g * kWave + lane();
+        uint64_t ca = 0, cb = 0;
+        if (k < nct) { ca = W.cta[k]; cb = W.ctb[k]; }
+        const ChainArcs c = chain_arcs(ca, cb, k < nct, n, mode, M);
+        arc(c.th, c.wf, c.fwd, true);
+    }
+    // sinks -> Z_in (SSP) / free nodes -> Z (potentials), cost 0
     for (int i = lane(); i < nz; i += kWave) {
         const uint32_t e = (uint32_t)W.zlist[i];
         const int v = (int)(e & 0x1FFFFFFFu);
-        const bool src = (e >> 30) & 1u, snk = (e >> 29) & 1u;
-        if (mode == kSsp) {
-            if (src) relax(v, W.key[N.n], 0, W.key[v]);
-            if (snk) relax(N.n + 1, W.key[v], 0, W.key[N.n + 1]);
-        } else {
-            relax(v, W.key[N.n], 0, W.key[v]);
-            relax(N.n, W.key[v], 0, W.key[N.n]);
-        }
+        const int64_t kv = W.key[v];
+        if (kv >= kInf) continue;
+        if (mode == kSsp) { if ((e >> 29) & 1u) relax(n + 1, kv + 1); }
+        else relax(n, kv + 1);
+    }
+    wave_lds_sync();
+    for (int g = G - 1; g >= kRegGroups; g--) {
+        const int k = g * kWave + lane();
+        uint64_t ca = 0, cb = 0;
+        if (k < nct) { ca = W.cta[k]; cb = W.ctb[k]; }
+        const ChainArcs c = chain_arcs(ca, cb, k < nct, n, mode, M);
+        arc(c.th, c.wb, c.bwd, false);
+    }
+#pragma unroll
+    for (int g = kRegGroups - 1; g >= 0; g--) {
+        if (g >= G) continue;
+        arc(C.th[g], C.wb[g], (C.bmask >> g) & 1u, false);
     }
     return changed;
 }
@@ -221,14 +286,14 @@ __device__ inline uint32_t bf_pass(const SubNet &N, const SubLds &W, int nct, in
 // so such a path is a shortest path of the new residual graph.
 __device__ inline void ssp_preds(const SubNet &N, const SubLds &W, int nct, int nz, int64_t M, bool reset) {
     if (reset) {
-        for (int v = lane(); v < N.n + 2; v += kWave) W.pred[v] = INT_MAX;
+        for (int v = lane(); v < N.n + 2; v += kWave) W.pred[v] = kNoPred;
         wave_lds_sync();
     }
     for_residual(N, W, nct, nz, kSsp, M, [&](int u, int v, int64_t w, int code) {
         const int64_t ku = W.key[u];
         if (ku >= kInf) return;
         if (ku + (w << kHopBits) + 1 == W.key[v])
-            __hip_atomic_fetch_min(&W.pred[v], code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_min(&W.pred[v], (int64_t)code << 32 | u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     });
     wave_lds_sync();
 }
@@ -237,15 +302,17 @@ __device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, i
     const int nn = N.n + 2;
     for (int v = lane(); v < nn; v += kWave) {
         W.key[v] = (mode == kSsp) ? (v == N.n ? 0 : kInf) : 0;
-        W.pred[v] = INT_MAX;
+        W.pred[v] = kNoPred;
     }
+    ChainRegs C;
+    load_chain_regs(W, N.n, nct, mode, M, C);
     wave_lds_sync();
     bool converged = false;
     for (int it = 0; it < nn + 2; it++) {
 #ifdef SGUFP_SUB_TRACE
         if (lane() == 0) W.misc[5]++;
 #endif
-        const uint32_t changed = bf_pass(N, W, nct, nz, mode, M);
+        const uint32_t changed = bf_pass(N, W, nct, nz, mode, M, C);
         wave_lds_sync();
         if (!wave_or(changed)) { converged = true; break; }
     }
@@ -272,7 +339,8 @@ struct ChainOut {
 __device__ inline void add_coef(const SubNet &N, const SubLds &W, int layer, int j, int64_t v) {
     if (v == 0) return;
     const int s = slot_of(N, layer, j);
-    if (s >= 0) lds_add(&W.coef[s], (double)v);
+    // integral values far below 2^53: the sum is exact in any order
+    if (s >= 0) __hip_atomic_fetch_add(&W.coef[s], (double)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // sigma on in-arc a of V-bar node q: every (i, q, j) of q gets u_iq * sigma (grb.cpp:257-266)
@@ -412,7 +480,7 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     const int S = N.S;
     const int p = blockIdx.x / S, s = blockIdx.x - p * S;
     if (p >= io.n_paths) return;
-    size_t off[8];
+    size_t off[9];
     sub_lds_layout(N.n, N.m, N.n_slots, N.nz, off);
     SubLds W;
     W.dec = (LDS int16_t *)(smem + off[0]);
@@ -421,8 +489,9 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     W.chosen = (LDS int32_t *)(smem + off[3]);
     W.key = (LDS int64_t *)(smem + off[3]);
     W.alpha = W.key;
-    W.pred = (LDS int32_t *)(smem + off[4]);
-    W.coef = (LDS double *)(smem + off[5]);
+    W.pred = (LDS int64_t *)(smem + off[4]);
+    W.plist = (LDS int32_t *)(smem + off[8]);
+    W.coef = io.coef + ((size_t)p * S + s) * N.n_slots;
     W.zlist = (LDS int32_t *)(smem + off[6]);
     W.misc = (LDS int32_t *)(smem + off[7]);
     const int n = N.n, m = N.m;
@@ -452,12 +521,12 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     }
     wave_lds_sync();
 
-    // 2. chains, indexed by the rank of their first arc
+    // 2. chains, numbered in the topological order of their first arc's tail
     int nct = 0;
     for (int base = 0; base < m; base += kWave) {
-        const int a = base + lane();
+        const int a = base + lane() < m ? N.arc_topo[base + lane()] : -1;
         bool st = false;
-        if (a < m) st = !N.vbar[N.tail[a]] || W.chosen[a] < 0;
+        if (a >= 0) st = !N.vbar[N.tail[a]] || W.chosen[a] < 0;
         const uint32_t incl = wave_scan_incl(st ? 1u : 0u);
         if (st) W.ctb[nct + (int)incl - 1] = pack_b(0, 0, 0, a);
         nct += (int)__builtin_amdgcn_readlane((int)incl, kWave - 1);
@@ -492,8 +561,9 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     }
     first_bad = lane_reduce<1>(first_bad, [](int x, int y) { return x < y ? x : y; });
     wave_lds_sync();
-    // chosen is dead from here: its space holds the coefficients (and keys / predecessors)
+    // chosen is dead from here: its space holds keys / predecessors
     for (int v = lane(); v < N.n_slots; v += kWave) W.coef[v] = 0.0;
+    __threadfence();   // zeros stored before any lane's atomic adds of phase 5
     wave_lds_sync();
     if (W.misc[0]) {
         if (lane() == 0) { io.status[b] = kSubError; io.obj[b] = 0; io.dual[b] = 0; io.rhs[b] = 0; }
@@ -538,64 +608,84 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
         // 3. successive shortest paths (max reward) from the sources to the sinks
 #ifdef SGUFP_SUB_TRACE
         const uint64_t tr0 = wall_clock64();
+        uint64_t t_bf = 0, t_pred = 0, t_walk = 0, tq;
         int nbf = 1;
+#define SUB_T0() tq = wall_clock64()
+#define SUB_T1(acc) acc += wall_clock64() - tq
+#else
+#define SUB_T0()
+#define SUB_T1(acc)
 #endif
         int iters = 0;
         bool fresh = true;   // labels and predecessors from a full Bellman-Ford
+        SUB_T0();
         if (!bellman_ford(N, W, nct, nz, kSsp, M)) status = kSubError;
+        SUB_T1(t_bf);
         for (; status == kSubOptimal; iters++) {
             const int64_t kz = W.key[n + 1];
             if (fresh && (kz >= kInf || key_cost(kz) >= 0)) break;
             if (iters > 8 * m + 64) { status = kSubError; break; }
-            // bottleneck along the predecessor chain, then augment (lane 0 walks)
+            // lane 0 chases the predecessors from Z_in back to Z_out into a list (one LDS
+            // round trip per arc: the entry holds the tail), then the wave takes the
+            // bottleneck and augments (a simple path uses each chain once)
             if (lane() == 0) {
-                int64_t delta = kInf;
-                int v = n + 1, steps = 0;
-                while (v != n && steps++ < n + 4) {
-                    const int code = W.pred[v];
-                    if (code == INT_MAX) break;
-                    if (code >= 2 * m) { v = (code & 1) ? (code - 2 * m - 1) / 2 : n; continue; }
-                    const int k = code >> 1;
-                    const uint64_t ca = W.cta[k], cb = W.ctb[k];
-                    const int64_t x = ch_x(cb), L = ch_L(cb), U = ch_U(cb);
-                    const int64_t cap = (code & 1) ? (x > L ? x - L : x) : (x < L ? L - x : U - x);
-                    delta = cap < delta ? cap : delta;
-                    v = (code & 1) ? ch_h(ca) : ch_t(ca);
+                int v = n + 1, len = 0;
+                while (v != n && len < n + 2) {
+                    const int64_t pr = W.pred[v];
+                    if (pr == kNoPred) break;
+                    W.plist[len++] = (int32_t)(pr >> 32);
+                    v = (int)(uint32_t)pr;
                 }
-                if (v != n || delta <= 0 || delta >= kInf) W.misc[fresh ? 1 : 2] = 1;
-                else {
-                    v = n + 1;
-                    while (v != n) {
-                        const int code = W.pred[v];
-                        if (code >= 2 * m) { v = (code & 1) ? (code - 2 * m - 1) / 2 : n; continue; }
-                        const int k = code >> 1;
-                        const uint64_t ca = W.cta[k];
-                        if (code & 1) { *ch_xp(W, k) -= (int16_t)delta; v = ch_h(ca); }
-                        else { *ch_xp(W, k) += (int16_t)delta; v = ch_t(ca); }
-                    }
+                W.misc[3] = (v == n) ? len : -1;
+            }
+            wave_lds_sync();
+            const int plen = W.misc[3];
+            int64_t delta = kInf;
+            for (int i = lane(); i < plen; i += kWave) {
+                const int code = W.plist[i];
+                if (code >= 2 * m) continue;   // Z arcs: uncapacitated
+                const uint64_t cb = W.ctb[code >> 1];
+                const int64_t x = ch_x(cb), L = ch_L(cb), U = ch_U(cb);
+                const int64_t cap = (code & 1) ? (x > L ? x - L : x) : (x < L ? L - x : U - x);
+                delta = cap < delta ? cap : delta;
+            }
+            delta = lane_reduce<1>(delta, [](int64_t p, int64_t q) { return p < q ? p : q; });
+            if (plen < 0 || delta <= 0 || delta >= kInf) {
+                if (lane() == 0) W.misc[fresh ? 1 : 2] = 1;
+            } else {
+                for (int i = lane(); i < plen; i += kWave) {
+                    const int code = W.plist[i];
+                    if (code >= 2 * m) continue;
+                    *ch_xp(W, code >> 1) += (int16_t)((code & 1) ? -delta : delta);
                 }
             }
             wave_lds_sync();
+            SUB_T1(t_walk);
             if (W.misc[1]) { status = kSubError; break; }
             if (W.misc[2]) {
                 // no tight path left under the old labels: recompute them
                 wave_lds_sync();
                 if (lane() == 0) W.misc[2] = 0;
                 wave_lds_sync();
+                SUB_T0();
                 if (!bellman_ford(N, W, nct, nz, kSsp, M)) { status = kSubError; break; }
+                SUB_T1(t_bf);
 #ifdef SGUFP_SUB_TRACE
                 nbf++;
 #endif
                 fresh = true;
                 continue;
             }
+            SUB_T0();
             ssp_preds(N, W, nct, nz, M, true);
+            SUB_T1(t_pred);
             fresh = false;
         }
 #ifdef SGUFP_SUB_TRACE
         if (blockIdx.x % 997 == 0 && lane() == 0)
-            printf("SUB blk=%d nct=%d nz=%d aug=%d bf=%d passes=%d ticks=%llu\n", (int)blockIdx.x, nct, nz, iters, nbf,
-                   W.misc[5], (unsigned long long)(wall_clock64() - tr0));
+            printf("SUB blk=%d nct=%d nz=%d aug=%d bf=%d passes=%d ticks=%llu t_bf=%llu t_pred=%llu t_walk=%llu\n",
+                   (int)blockIdx.x, nct, nz, iters, nbf, W.misc[5], (unsigned long long)(wall_clock64() - tr0),
+                   (unsigned long long)t_bf, (unsigned long long)t_pred, (unsigned long long)t_walk);
 #endif
         // lower bounds met?
         int unmet = 0;
@@ -659,7 +749,6 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
         io.dual[b] = (double)dual;
         io.rhs[b] = (double)rhs;
     }
-    for (int v = lane(); v < N.n_slots; v += kWave) io.coef[b * N.n_slots + v] = W.coef[v];
 }
 
 // Per path, in scenario order: the first infeasible scenario's ray (grb.cpp:288-350,
@@ -717,13 +806,16 @@ __global__ void __launch_bounds__(256) k_sub_reduce(SubNet N, SubIO io) {
 
 // ---------------------------------------------------------------------------------------
 size_t sub_lds_bytes(int n, int m, int n_slots, int nz) {
-    size_t off[8];
+    size_t off[9];
     return sub_lds_layout(n, m, n_slots, nz, off);
 }
 
 hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st) {
     if (io.n_paths <= 0) return hipSuccess;
-    const size_t lds = sub_lds_bytes(N.n, N.m, N.n_slots, N.nz);
+    size_t lds = sub_lds_bytes(N.n, N.m, N.n_slots, N.nz);
+#ifdef SGUFP_SUB_LDS_MIN
+    if (lds < SGUFP_SUB_LDS_MIN) lds = SGUFP_SUB_LDS_MIN;   // occupancy experiments
+#endif
     hipLaunchKernelGGL(k_sub_scenario, dim3((unsigned)io.n_paths * N.S), dim3(kWave), lds, st, N, io);
     hipLaunchKernelGGL(k_sub_reduce, dim3((unsigned)io.n_paths), dim3(256), 0, st, N, io);
     return hipGetLastError();

@@ -113,7 +113,8 @@ def _cut_at(rhs, row, keys, y):
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg,seed,S,zl,trials", [("C1", 1, 1, False, 6), ("C1", 2, 1, True, 6),
                                                    ("C2", 1, 2, False, 6), ("C2", 2, 3, True, 6),
-                                                   ("C3", 1, 4, True, 3), ("C3", 2, 3, False, 3)])
+                                                   ("C3", 1, 4, True, 3), ("C3", 2, 3, False, 3),
+                                                   ("C5", 1, 2, True, 2), ("C5", 2, 2, False, 2)])
 def test_subproblem_matches_highs(cfg, seed, S, zl, trials):
     from sgufp_solver_amd import engine as E
     inst, path, net = _net(cfg, seed, S, zl)
