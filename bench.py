@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=2048)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-tag", default="r01")
+    ap.add_argument("--sub-paths", type=int, default=32, help="subproblem leg: random full-matching paths (0: skip)")
+    ap.add_argument("--cpu-sub-seconds", type=float, default=8.0)
     ap.add_argument("--mode", choices=["relax", "bnb"], default="relax",
                     help="relax: the headline batch relaxation; bnb: the device B&B (config C3) for --bnb-seconds")
     ap.add_argument("--bnb-config", default="C3")
@@ -253,6 +255,7 @@ def main():
 
     total_nodes = mine.n * world
     value = total_nodes * args.steps / elapsed
+    sub = subproblem_leg(eng, inst, net, args) if rank == 0 else None
     line = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -291,14 +294,84 @@ def main():
             "children_record_bytes": r_out,
         },
         "cpu_baseline": None,
+        "subproblem": sub,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(work, net, pool, mine, incumbent, args)
+        if sub is not None:
+            i0, n0 = sub["_inst0"]
+            sub["cpu_baseline"] = cpu_subproblem_baseline(inst, net, sub["_paths"], args, i0, n0)
+    if sub is not None:
+        sub.pop("_paths", None)
+        sub.pop("_inst0", None)
     if rank == 0:
         print(json.dumps(line), flush=True)
     eng.close()
     if dist:
         dist.destroy_process_group()
+
+
+def subproblem_leg(eng, inst, net, args):
+    """The exact-leaf half of a relaxation: GuroSolver::solveSubProblem (grb.cpp:139-360)
+    on the device (k_sub_scenario + k_sub_reduce) for --sub-paths random full matchings,
+    every scenario; scenario LPs per second of the synchronous call (paths uploaded, cut
+    rows downloaded).  Two cases: the bench instance itself (its sink-arc lower bounds
+    make most matchings infeasible: Farkas rays, feasibility cuts) and the same network
+    with lower bounds 0 (every scenario optimal: full max-reward flows, optimality cuts)."""
+    from sgufp_solver_amd import engine as E
+    from sgufp_solver_amd import instance
+    if args.sub_paths <= 0:
+        return None
+    _, la, _ = E.probe_network(net)
+    rng = np.random.default_rng(args.seed + 7)
+    paths = [instance.random_matching_path(inst, la, rng) for _ in range(args.sub_paths)]
+    inst0 = instance.generate(instance.CONFIGS[args.config], args.seed)
+    inst0.lb[:] = 0
+    net0 = os.path.join(os.path.dirname(net), "net_lb0.txt")
+    inst0.write(net0)
+    out = {"kernel": "k_sub_scenario", "paths": len(paths), "scenarios": int(inst.scenarios), "_paths": paths}
+    eng0 = E.Engine(net0, eng.device, 64)
+    for name, e in (("generated_bounds", eng), ("lower_bounds_0", eng0)):
+        e.subproblem(paths)                                 # warm-up
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            typ, _, _, _ = e.subproblem(paths)
+            ts.append(time.perf_counter() - t0)
+        t = float(np.mean(ts))
+        lps = len(paths) * inst.scenarios
+        out[name] = {"ms_per_call": round(t * 1e3, 3), "scenario_lps_per_s": round(lps / t, 1),
+                     "paths_per_s": round(len(paths) / t, 2),
+                     "cut_types": {str(k): int(v) for k, v in zip(*np.unique(typ, return_counts=True))}}
+    eng0.close()
+    out["_inst0"] = (inst0, net0)
+    return out
+
+
+def cpu_subproblem_baseline(inst, net, paths, args, inst0=None, net0=None):
+    """The reference solves each scenario LP with Gurobi 11 (absent here): its dual LP
+    restated (oracle/subproblem_oracle.py) and solved with scipy HiGHS on one core, on a
+    bounded sample of the same (path, scenario) pairs (lower bounds 0 case when given)."""
+    from oracle import subproblem_oracle as so
+    from sgufp_solver_amd import engine as E
+    if inst0 is not None:
+        inst, net = inst0, net0
+    _, la, _ = E.probe_network(net)
+    sn = so.from_instance(inst, la)
+    done, t0 = 0, time.perf_counter()
+    for p in paths:
+        y = so.ybar_of_path(sn, p)
+        for s in range(inst.scenarios):
+            so.dual_lp(sn, y, s)
+            done += 1
+            if time.perf_counter() - t0 > args.cpu_sub_seconds:
+                break
+        if time.perf_counter() - t0 > args.cpu_sub_seconds:
+            break
+    t = time.perf_counter() - t0
+    return {"value": round(done / t, 2), "unit": "scenario LPs/s", "cores": 1, "kind": "port",
+            "sample": f"{done} (path, scenario) dual LPs of the reference formulation"
+                      f"{' (lower bounds 0)' if inst0 is not None else ''}, scipy HiGHS, {t:.1f} s"}
 
 
 def cpu_baseline(work, net, pool, batch, incumbent, args):

@@ -217,6 +217,7 @@ class Engine:
 
     def __init__(self, network_path: str, device: int = 0, max_batch: int = 4096):
         self.lib = load_library()
+        self.device = device
         err = C.c_int(0)
         self.ctx = self.lib.sgufp_create_from_file(network_path.encode(), device, max_batch, C.byref(err))
         if not self.ctx:

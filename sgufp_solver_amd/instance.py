@@ -177,3 +177,27 @@ def generate(cfg: InstanceConfig, seed: int, scenarios: int | None = None) -> In
 
 def generate_text(name: str, seed: int, scenarios: int | None = None) -> str:
     return generate(CONFIGS[name], seed, scenarios).to_text()
+
+
+def random_matching_path(inst: Instance, layer_arcs, rng) -> list:
+    """DD decision vector (one entry per layer, GuroSolver::solveSubProblem's input,
+    grb.cpp:139-150) of a random full matching at every V-bar node: each incoming arc
+    of q is matched to a distinct out-arc of q while both last.  Layer l decides the
+    in-arc processingOrder[l] (layer_arcs[l]); the decision is the chosen out-arc's id
+    or -1.  Synthetic exact-leaf paths for subproblem throughput runs."""
+    m = len(inst.tails)
+    outs = {}
+    for b in range(m):
+        outs.setdefault(int(inst.tails[b]), []).append(b)
+    vb = set(int(v) for v in inst.vbar)
+    choice = {}
+    for q in sorted(vb):
+        ins = [a for a in range(m) if int(inst.heads[a]) == q]
+        free = list(outs.get(q, []))
+        rng.shuffle(ins)
+        rng.shuffle(free)
+        for a in ins:
+            if free:
+                choice[a] = free.pop()
+    return [int(choice.get(int(a), -1)) for a in layer_arcs]
+
