@@ -159,6 +159,9 @@ class DDSolver {
     double startSolver(double optimal);
     // counters of the last solve (SOLVER_COUNTERS, DDSolver.h:380-392)
     sgufp_bnb_stats totals{};
+    // the reference's printWorkerStats report (DDSolver.h:441-501) for the last solve: one
+    // "worker" (the device); start() prints it when built with -DSOLVER_COUNTERS
+    std::string workerStats() const;
     int64_t rounds = 0;
     sgufp_ctx *context() const { return dev.get(); }
 };

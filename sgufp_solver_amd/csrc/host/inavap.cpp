@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <sstream>
 #include <cstdio>
 #include <fstream>
 #include <iostream>
@@ -236,11 +237,36 @@ double DDSolver::startSolver(double known_optimal) {
     return z;
 }
 
+std::string DDSolver::workerStats() const {
+    // DDSolver.h:441-501: the dash line is 72 wide (its size is taken before the list fills)
+    const std::string dash(72, '-');
+    const double processed = (double)totals.relaxed;   // nProcessed of the single device worker
+    std::ostringstream o;
+    o << dash << "\n";
+    o << "Processed: " << totals.relaxed << "  " << "\n";
+    o << "Total: " << processed << "\t Mean: " << processed << "\t Deviation: " << 0.0 << "\t Min: " << processed
+      << "\t Max: " << processed << "\n";
+    o << dash << "\n\n";
+    o << "Cuts (feasibility, optimality): " << sgufp_cuts_count(dev.get(), 1) << " , " << sgufp_cuts_count(dev.get(), 0)
+      << "\n";
+    o << dash << "\n";
+    o << "Nodes pruned (feasibility, optimality, bound): " << "\n";
+    o << "(" << totals.pruned_feasibility << ", " << totals.pruned_optimality << ", " << totals.pruned_bound << ")"
+      << "  " << "\n";
+    o << dash << "\n";
+    o << "Waiting Time (seconds): " << 0 << "   " << "\n";
+    o << dash << "\n\n";
+    return o.str();
+}
+
 std::pair<double, double> DDSolver::start(double known_opt) {
     const auto t0 = std::chrono::high_resolution_clock::now();
     const double solution = startSolver(known_opt);
     const auto t1 = std::chrono::high_resolution_clock::now();
     const double secs = std::chrono::duration<double>(t1 - t0).count();
+#ifdef SOLVER_COUNTERS
+    std::cout << workerStats();
+#endif
     // DDSolver.cpp:863-865 ("Explored" = children enqueued, sum of nQueue)
     std::cout << "Optimal solution: " << solution << ". Explored " << totals.children
               << " nodes (entire search space) in " << secs << " seconds." << std::endl;

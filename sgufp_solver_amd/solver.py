@@ -188,19 +188,53 @@ class DDSolver:
             self._rebalance(dist, sizes)
         return z
 
-    def start(self, known_opt: float):
-        """DDSolver::start (DDSolver.cpp:848-867): solve, time, print the reference's line."""
+    def start(self, known_opt: float, solver_counters: bool = False):
+        """DDSolver::start (DDSolver.cpp:848-867): solve, time, print the reference's line
+        (and, with solver_counters -- the reference's SOLVER_COUNTERS build -- its
+        printWorkerStats report first, one worker per rank)."""
         t0 = time.perf_counter()
         solution = self.start_solver(known_opt)
         self.seconds = time.perf_counter() - t0
         # "Explored N nodes" = sum of nQueue = children produced (DDSolver.cpp:742, 856-865)
         explored = self.counters.get("children", 0)
         dist = self._dist()
+        per_rank = [dict(self.counters)]
         if dist is not None:
             tot = [None] * dist.get_world_size(self.group)
             dist.all_gather_object(tot, explored, group=self.group)
             explored = sum(tot)
+            per_rank = [None] * dist.get_world_size(self.group)
+            dist.all_gather_object(per_rank, dict(self.counters), group=self.group)
+        if self.verbose and solver_counters and (dist is None or dist.get_rank(self.group) == 0):
+            print(worker_stats_text(per_rank, self.eng.cuts_count(1), self.eng.cuts_count(0)), end="")
         if self.verbose and (dist is None or dist.get_rank(self.group) == 0):
             print(f"Optimal solution: {solution}. Explored {explored} nodes (entire search space) in "
                   f"{self.seconds} seconds.")
         return solution, self.seconds
+
+
+def worker_stats_text(per_worker, n_feas_cuts: int, n_opt_cuts: int) -> str:
+    """DDSolver::printWorkerStats (DDSolver.h:441-501) for per-worker counter dicts (one per
+    rank here): processed counts with total / mean / absolute deviation / min / max, the
+    global cut counts, per-worker (feasibility, optimality, bound) prunes, waiting times
+    (none: ranks do not sleep).  The dash line is 72 wide as in the reference (its length
+    is computed before the list fills)."""
+    dash = "-" * 72
+    processed = [float(c.get("relaxed", 0)) for c in per_worker]
+    mean = sum(processed) / len(processed) if processed else 0.0
+    absdev = sum(abs(p - mean) for p in processed) / len(processed) if processed else 0.0
+    lines = [dash, "Processed: " + "".join(f"{int(p)}  " for p in processed),
+             f"Total: {_g(sum(processed))}\t Mean: {_g(mean)}\t Deviation: {_g(absdev)}\t "
+             f"Min: {_g(min(processed) if processed else 0.0)}\t Max: {_g(max(processed) if processed else 0.0)}",
+             dash, "", f"Cuts (feasibility, optimality): {n_feas_cuts} , {n_opt_cuts}", dash,
+             "Nodes pruned (feasibility, optimality, bound): ",
+             "".join(f"({c.get('pruned_feasibility', 0)}, {c.get('pruned_optimality', 0)}, {c.get('pruned_bound', 0)})  "
+                     for c in per_worker),
+             dash, "Waiting Time (seconds): " + "".join("0   " for _ in per_worker), dash, ""]
+    return "\n".join(lines) + "\n"
+
+
+def _g(x: float) -> str:
+    """std::cout's default formatting of a double (%g with 6 significant digits)."""
+    return f"{x:g}"
+

@@ -181,3 +181,18 @@ def test_toy_frontier_order_is_a_stack():
     bot = eng.frontier_take(2, from_bottom=True)
     assert list(bot.ub) == [0.0, 1.0]
     assert batch_concat([bot, top]).n == 4 and batch_slice(bot, np.array([1])).ub[0] == 1.0
+
+
+def test_worker_stats_format():
+    """printWorkerStats (DDSolver.h:441-501): 72-wide dash lines, processed counts with
+    total / mean / absolute deviation / min / max, cut counts, per-worker prunes."""
+    from sgufp_solver_amd.solver import worker_stats_text
+    txt = worker_stats_text([{"relaxed": 10, "pruned_optimality": 3, "pruned_feasibility": 1},
+                             {"relaxed": 14, "pruned_bound": 2}], 1, 5)
+    lines = txt.split("\n")
+    assert lines[0] == "-" * 72
+    assert lines[1] == "Processed: 10  14  "
+    assert lines[2] == "Total: 24\t Mean: 12\t Deviation: 2\t Min: 10\t Max: 14"
+    assert "Cuts (feasibility, optimality): 1 , 5" in lines
+    assert "(1, 3, 0)  (0, 0, 2)  " in lines
+    assert lines[-3] == "-" * 72 and lines[-2] == "" and lines[-1] == ""   # dash, endl, endl
