@@ -2,6 +2,7 @@
 // memory, cut-pool densification, batch staging and result retrieval.
 #include "ctx.hpp"
 #include <algorithm>
+#include <cstdlib>
 
 
 namespace {
@@ -225,9 +226,43 @@ static sgufp_ctx *finish_create(sgufp_ctx *ctx, int *err) {
     return ctx;
 }
 
+// Dispatch order of k_relax.  Neighbouring records of a batch are often siblings (one
+// parent's cutset) of similar cost, so in batch order heavy records start together, share
+// CUs, and a run of them can start last.  Workgroup b relaxes record perm[b], a fixed
+// pseudo-random permutation per batch size (results stay indexed by record).  Bench batch
+// (8192 C4 records): 59.7 ms in batch order, 53.8 ms permuted.  SGUFP_RELAX_ORDER=0 keeps
+// batch order.
+bool sgufp_ctx::relax_order(BatchIn &in) {
+    static const bool enabled = [] {
+        const char *e = std::getenv("SGUFP_RELAX_ORDER");
+        return !(e && e[0] == '0');
+    }();
+    in.perm = nullptr;
+    if (!enabled || in.n < 3) return true;
+    if (!d_perm && !alloc(d_perm, (size_t)max_batch, "dispatch order")) return false;
+    if (perm_n != in.n) {
+        std::vector<int32_t> p(in.n);
+        for (int i = 0; i < in.n; i++) p[i] = i;
+        uint64_t x = 0x9E3779B97F4A7C15ull ^ (uint64_t)in.n;
+        for (int i = in.n - 1; i > 0; i--) {   // Fisher-Yates, splitmix64
+            x += 0x9E3779B97F4A7C15ull;
+            uint64_t z = x;
+            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+            z ^= z >> 31;
+            std::swap(p[i], p[(int)(z % (uint64_t)(i + 1))]);
+        }
+        if (!upload(d_perm, p.data(), (size_t)in.n) || !sync()) return false;
+        perm_n = in.n;
+    }
+    in.perm = d_perm;
+    return true;
+}
+
 bool sgufp_ctx::relax_current(double optimal_lb) {
     if (!push_orders()) return false;
-    const BatchIn &in = cur;
+    BatchIn in = cur;
+    if (!relax_order(in)) return false;
     const Pool p = pool();
     hipStream_t st = stream;
     if (timing) hipEventRecord(ev[0], st);

@@ -97,9 +97,12 @@ struct sgufp_ctx {
     bool frontier_reserve(int64_t entries, size_t sol_entries);
     // B&B step staging (host mirrors + small device index arrays)
     int32_t *d_bidx = nullptr;                // [max_batch] node indices (paths / parents)
+    int32_t *d_perm = nullptr;                // [max_batch] k_relax dispatch order (relax_current)
+    int perm_n = -1;                          // batch size d_perm was drawn for
     int64_t *d_boff = nullptr, *d_bsol = nullptr;  // [max_batch + 1]
     int16_t *d_bpaths = nullptr;              // [max_batch * Lcap] gathered paths
     bool relax_current(double optimal_lb);
+    bool relax_order(BatchIn &in);
     void encode_records(int n, const uint16_t *gl, const int64_t *states_off, const int16_t *states,
                         const int64_t *sol_off, const int16_t *sol, EncodedRecords &e) const;
     // device records [count] (mask over the layer's universe) -> host states, as sgufp_batch_children
@@ -213,6 +216,7 @@ struct sgufp_ctx {
         b.n = n; b.gl = d_gl; b.lb = d_lb; b.ub = d_ub; b.mask = d_mask; b.valid = d_valid;
         b.sol_off = d_soloff; b.sol_len = d_sollen; b.sol = d_sol;
         b.bound_prune = 0;
+        b.perm = nullptr;
         return b;
     }
     BatchIn frontier_slice(int64_t base, int count) const {
@@ -220,6 +224,7 @@ struct sgufp_ctx {
         b.n = count; b.gl = fr.gl + base; b.lb = fr.lb + base; b.ub = fr.ub + base; b.mask = fr.mask + base;
         b.valid = fr.valid + base; b.sol_off = fr.sol_off + base; b.sol_len = fr.sol_len + base; b.sol = fr.sol;
         b.bound_prune = 1;   // Worker::startWorker skips nodes with ub <= zOpt (DDSolver.cpp:707-711)
+        b.perm = nullptr;
         return b;
     }
     const BatchIn &batch() const { return cur; }

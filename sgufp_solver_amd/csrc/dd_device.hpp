@@ -103,6 +103,8 @@ struct BatchIn {
     const uint16_t SGUFP_GBL *sol_len;
     const int16_t SGUFP_GBL *sol;
     int bound_prune;                     // 1: records with ub <= incumbent are pruned unprocessed
+    const int32_t SGUFP_GBL *perm;       // k_relax dispatch order: workgroup b relaxes record
+                                         // perm[b] (null: b), see sgufp_ctx::relax_current
 };
 
 // Device frontier (B&B open nodes), SoA stack; sol_off are absolute offsets into sol.

@@ -1674,8 +1674,8 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
                                                 double incumbent) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
-    const int slot = blockIdx.x;
-    if (slot >= in.n) return;
+    if ((int)blockIdx.x >= in.n) return;
+    const int slot = in.perm ? in.perm[blockIdx.x] : (int)blockIdx.x;
     const uint64_t t_start = wall_clock64();
     DD d;
     dd_bind(d, smem, sc, slot, CB);
