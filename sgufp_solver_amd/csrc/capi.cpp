@@ -493,7 +493,8 @@ bool sgufp_ctx::sub_init() {
     const Network &N = net;
     const int n = N.n, m = N.m, S = N.S;
     // chain records keep node / arc ids and bounds in 16 bits (ids already are: Cut.h:342-344)
-    if (n > 32767 || m > 32767) { err = "subproblem: more than 32767 nodes or arcs"; return false; }
+    // (predecessor words pack arc code << 15 | node: 2 (m + n + 1) codes must fit 16 bits)
+    if (n > 32767 || m > 32767 || 2 * (m + n + 1) > 65535) { err = "subproblem: more than 32766 nodes + arcs"; return false; }
     for (size_t i = 0; i < N.lb.size(); i++)
         if (N.lb[i] < -32768 || N.lb[i] > 32767 || N.ub[i] < -32768 || N.ub[i] > 32767) {
             err = "subproblem: arc bounds outside 16 bits";

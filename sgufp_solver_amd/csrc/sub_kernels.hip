@@ -43,7 +43,7 @@ namespace {
 constexpr int64_t kInf = INT64_MAX / 4;
 constexpr int kHopBits = 16;
 constexpr int kMaxChain = 64;      // arcs per chain (V-bar nodes in a row + 1)
-constexpr int64_t kNoPred = INT64_MAX;
+constexpr int32_t kNoPred = INT32_MAX;
 
 // Chain k of the contracted network lives in two 64-bit LDS words, so a Bellman-Ford pass
 // reads one arc with two ds_read_b64:
@@ -51,15 +51,16 @@ constexpr int64_t kNoPred = INT64_MAX;
 //   ctb: max l:16 | min u:16 | flow x:16 | first arc:16
 // Node / arc ids fit 16 bits (Cut.h:342-344 packs them so); the host checks the bounds.
 struct SubLds {
-    LDS int16_t *dec;       // [m] decision at the head (out-arc id, -1 none, -2 head not V-bar)
+    LDS int16_t *dec;       // [m] decision at the head (out-arc id, -1 none, -2 head not V-bar);
+                            //     phases 1-2 only (union), phase 5 reads dec_of from HBM
     LDS uint64_t *cta;      // [m] chains (indexed by the rank of their first arc)
     LDS uint64_t *ctb;      // [m]
     LDS int32_t *chosen;    // [m] in-arc that chose this out-arc of a V-bar node (phases 1-2;
                             //     aliases key / pred)
     LDS int64_t *key;       // [n+2] Bellman-Ford keys (cost << 16 | hops); then alpha in place
     LDS int64_t *alpha;     // == key: dual node potentials after the last Bellman-Ford
-    LDS int64_t *pred;      // [n+2] code of the tight in-arc << 32 | its tail (kNoPred: none)
-    LDS int32_t *plist;     // [n+2] arc codes of the augmenting path (sink to source)
+    LDS int32_t *pred;      // [n+2] code of the tight in-arc << 15 | its tail (kNoPred: none)
+    LDS uint16_t *plist;    // [n+2] arc codes of the augmenting path (sink to source)
     double GBL *coef;       // [n_slots] this (path, scenario)'s row of SubIO::coef (phase 5)
     LDS int32_t *zlist;     // [nz] free-supply / free-demand nodes: v | src << 30 | snk << 29
     LDS int32_t *misc;      // [8] flags
@@ -67,17 +68,19 @@ struct SubLds {
 
 __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+// LDS: chains, then a union -- phases 1-2: chosen (int32 [m]) and dec (int16 [m]);
+// phases 3-5: key (alpha), pred, plist -- then the free-node list and flags.
 __host__ __device__ inline size_t sub_lds_layout(int n, int m, int n_slots, int nz, size_t *off) {
     size_t o = 0;
-    off[0] = o; o = a16(o + (size_t)m * 2);
     off[1] = o; o = a16(o + (size_t)m * 8);
     off[2] = o; o = a16(o + (size_t)m * 8);
-    const size_t u0 = o;                         // union: chosen | key, pred, plist
-    off[3] = o; o = a16(o + (size_t)(n + 2) * 8);
-    off[4] = o; o = a16(o + (size_t)(n + 2) * 8);
+    const size_t u0 = o;
+    off[3] = o; o = a16(o + (size_t)(n + 2) * 8);   // key | chosen
+    off[4] = o; o = a16(o + (size_t)(n + 2) * 4);   // pred
+    off[8] = o; o = a16(o + (size_t)(n + 2) * 2);   // plist
+    off[0] = a16(u0 + (size_t)m * 4);               // dec, after chosen
+    if (o < a16(off[0] + (size_t)m * 2)) o = a16(off[0] + (size_t)m * 2);
     off[5] = o;
-    off[8] = o; o = a16(o + (size_t)(n + 2) * 4);
-    if (o < a16(u0 + (size_t)m * 4)) o = a16(u0 + (size_t)m * 4);
     off[6] = o; o = a16(o + (size_t)nz * 4);
     off[7] = o; o = a16(o + 8 * 4);
     return o;
@@ -293,7 +296,7 @@ __device__ inline void ssp_preds(const SubNet &N, const SubLds &W, int nct, int 
         const int64_t ku = W.key[u];
         if (ku >= kInf) return;
         if (ku + (w << kHopBits) + 1 == W.key[v])
-            __hip_atomic_fetch_min(&W.pred[v], (int64_t)code << 32 | u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_min(&W.pred[v], code << 15 | u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     });
     wave_lds_sync();
 }
@@ -362,9 +365,20 @@ __device__ inline int64_t alpha_of(const SubNet &N, const SubLds &W, int v) {
     return (v >= 0 && N.inner[v] && !N.vbar[v]) ? W.alpha[v] : 0;
 }
 
+// Decision at the head of arc a from the path in HBM (phase 1 keeps it in LDS as dec; the
+// dual assembly re-reads it, the LDS space being reused)
+__device__ inline int dec_of(const SubNet &N, const SubIO &io, int64_t poff, int64_t plen, int a) {
+    const int q = N.head[a];
+    if (!N.vbar[q]) return -2;
+    const int l = N.arc_layer[a];
+    int d = (l >= 0 && l < plen) ? (int)io.paths[poff + l] : -1;
+    if (d < -1 || d >= N.m || (d >= 0 && N.tail[d] != q)) d = -3;   // not an out-arc of q
+    return d;
+}
+
 // ray_mode: r = 0; e_target[m] given for every arc (only used when ray_mode)
-__device__ ChainOut assemble_chain(const SubNet &N, const SubLds &W, int k, int s, bool ray_mode, int ray_p,
-                                   int ray_q, bool &ok) {
+__device__ ChainOut assemble_chain(const SubNet &N, const SubLds &W, const SubIO &io, int64_t poff, int64_t plen,
+                                   int k, int s, bool ray_mode, int ray_p, int ray_q, bool &ok) {
     ChainOut o{0, 0};
     int arcs[kMaxChain];
     int len = 0;
@@ -372,7 +386,7 @@ __device__ ChainOut assemble_chain(const SubNet &N, const SubLds &W, int k, int 
     for (int a = ch_first(cb); a >= 0 && len < kMaxChain;) {
         arcs[len++] = a;
         if (!N.vbar[N.head[a]]) break;
-        a = W.dec[a];
+        a = dec_of(N, io, poff, plen, a);
     }
     if (len >= kMaxChain) { ok = false; return o; }
     const int t = ch_t(ca), h = ch_h(ca);
@@ -489,8 +503,8 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     W.chosen = (LDS int32_t *)(smem + off[3]);
     W.key = (LDS int64_t *)(smem + off[3]);
     W.alpha = W.key;
-    W.pred = (LDS int64_t *)(smem + off[4]);
-    W.plist = (LDS int32_t *)(smem + off[8]);
+    W.pred = (LDS int32_t *)(smem + off[4]);
+    W.plist = (LDS uint16_t *)(smem + off[8]);
     W.coef = io.coef + ((size_t)p * S + s) * N.n_slots;
     W.zlist = (LDS int32_t *)(smem + off[6]);
     W.misc = (LDS int32_t *)(smem + off[7]);
@@ -503,14 +517,7 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     if (lane() < 8) W.misc[lane()] = 0;
     for (int a = lane(); a < m; a += kWave) {
         W.chosen[a] = -1;
-        const int q = N.head[a];
-        int d = -2;
-        if (N.vbar[q]) {
-            const int l = N.arc_layer[a];
-            d = (l >= 0 && l < plen) ? (int)io.paths[poff + l] : -1;
-            if (d < -1 || d >= m || (d >= 0 && N.tail[d] != q)) d = -3;   // not an out-arc of q
-        }
-        W.dec[a] = (int16_t)d;
+        W.dec[a] = (int16_t)dec_of(N, io, poff, plen, a);
     }
     wave_lds_sync();
     for (int a = lane(); a < m; a += kWave) {
@@ -631,10 +638,10 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
             if (lane() == 0) {
                 int v = n + 1, len = 0;
                 while (v != n && len < n + 2) {
-                    const int64_t pr = W.pred[v];
+                    const int32_t pr = W.pred[v];
                     if (pr == kNoPred) break;
-                    W.plist[len++] = (int32_t)(pr >> 32);
-                    v = (int)(uint32_t)pr;
+                    W.plist[len++] = (uint16_t)(pr >> 15);
+                    v = (int)(pr & 0x7FFF);
                 }
                 W.misc[3] = (v == n) ? len : -1;
             }
@@ -726,7 +733,7 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
         const bool ray = status == kSubInfeasible;
         for (int k = lane(); k < nct; k += kWave) {
             if (ray && ray_chain >= 0 && k != ray_chain) continue;   // (i)/(ii): only the bad chain
-            ChainOut c = assemble_chain(N, W, k, s, ray, (k == ray_chain) ? ray_p : -1,
+            ChainOut c = assemble_chain(N, W, io, poff, plen, k, s, ray, (k == ray_chain) ? ray_p : -1,
                                         (k == ray_chain) ? ray_q : -1, ok);
             rhs += c.rhs;
             dual += c.obj;
