@@ -525,7 +525,7 @@ bool sgufp_ctx::sub_init() {
         for (int a = 0; a < m; a++) arc_topo[a] = a;
         std::stable_sort(arc_topo.begin(), arc_topo.end(), [&](int a, int b) { return rank[N.tail[a]] < rank[N.tail[b]]; });
     }
-    if (sub_lds_bytes(n, m, N.n_slots, nz) > 160 * 1024) { err = "network too large for the LDS subproblem"; return false; }
+    if (sub_lds_bytes(n, m, m, nz) > 160 * 1024) { err = "network too large for the LDS subproblem"; return false; }
     std::vector<int32_t> inner(n), arc_layer(m, -1), lb((size_t)S * m), ub((size_t)S * m), rew(m);
     std::vector<uint8_t> vb(n), in8(n);
     std::vector<int32_t> in_off(n + 1, 0), out_off(n + 1, 0), in_list, out_list;
@@ -627,6 +627,26 @@ int sgufp_subproblem(sgufp_ctx *ctx, int n, const int64_t *path_off, const int16
         return SGUFP_ERR_HIP;
     SubIO io = ctx->sio;
     io.n_paths = n;
+    // chains of a path = m minus its matched out-arcs (distinct valid decisions); the LDS
+    // holds the most any path of the batch needs (a wave that finds more flags an error)
+    {
+        const int m = ctx->net.m;
+        std::vector<uint8_t> used((size_t)m, 0);
+        int cap = 0;
+        for (int k = 0; k < n; k++) {
+            int matched = 0;
+            for (int64_t i = path_off[k]; i < path_off[k + 1]; i++) {
+                const int d = paths[i];
+                if (d >= 0 && d < m && !used[d]) { used[d] = 1; matched++; }
+            }
+            for (int64_t i = path_off[k]; i < path_off[k + 1]; i++) {
+                const int d = paths[i];
+                if (d >= 0 && d < m) used[d] = 0;
+            }
+            cap = std::max(cap, m - matched);
+        }
+        io.nct_cap = std::max(cap, 1);
+    }
     io.path_off = ctx->d_spoff;
     io.paths = ctx->d_spaths;
     if (!ctx->hip_ok(launch_subproblem(ctx->sn, io, ctx->stream), "subproblem launch")) return SGUFP_ERR_HIP;

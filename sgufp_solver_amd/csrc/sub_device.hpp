@@ -37,6 +37,8 @@ struct SubNet {
 
 struct SubIO {
     int n_paths;
+    int nct_cap;                         // chains per (path, scenario) the LDS holds: m minus the
+                                         // fewest decided arcs over the batch (host, per call)
     const int64_t SGUFP_GBL *path_off;   // [n_paths+1]
     const int16_t SGUFP_GBL *paths;
     // per (path, scenario)

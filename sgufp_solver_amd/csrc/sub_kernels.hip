@@ -70,10 +70,10 @@ __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15;
 
 // LDS: chains, then a union -- phases 1-2: chosen (int32 [m]) and dec (int16 [m]);
 // phases 3-5: key (alpha), pred, plist -- then the free-node list and flags.
-__host__ __device__ inline size_t sub_lds_layout(int n, int m, int n_slots, int nz, size_t *off) {
+__host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int nz, size_t *off) {
     size_t o = 0;
-    off[1] = o; o = a16(o + (size_t)m * 8);
-    off[2] = o; o = a16(o + (size_t)m * 8);
+    off[1] = o; o = a16(o + (size_t)nct_cap * 8);
+    off[2] = o; o = a16(o + (size_t)nct_cap * 8);
     const size_t u0 = o;
     off[3] = o; o = a16(o + (size_t)(n + 2) * 8);   // key | chosen
     off[4] = o; o = a16(o + (size_t)(n + 2) * 4);   // pred
@@ -495,7 +495,7 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     const int p = blockIdx.x / S, s = blockIdx.x - p * S;
     if (p >= io.n_paths) return;
     size_t off[9];
-    sub_lds_layout(N.n, N.m, N.n_slots, N.nz, off);
+    sub_lds_layout(N.n, N.m, io.nct_cap, N.nz, off);
     SubLds W;
     W.dec = (LDS int16_t *)(smem + off[0]);
     W.cta = (LDS uint64_t *)(smem + off[1]);
@@ -535,8 +535,12 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
         bool st = false;
         if (a >= 0) st = !N.vbar[N.tail[a]] || W.chosen[a] < 0;
         const uint32_t incl = wave_scan_incl(st ? 1u : 0u);
-        if (st) W.ctb[nct + (int)incl - 1] = pack_b(0, 0, 0, a);
+        if (st && nct + (int)incl - 1 < io.nct_cap) W.ctb[nct + (int)incl - 1] = pack_b(0, 0, 0, a);
         nct += (int)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+    }
+    if (nct > io.nct_cap) {   // more chains than the host counted: not a valid path
+        if (lane() == 0) W.misc[0] = 1;
+        nct = io.nct_cap;
     }
     wave_lds_sync();
     // free-supply / free-demand nodes (structural, from the host; read by every pass)
@@ -812,14 +816,14 @@ __global__ void __launch_bounds__(256) k_sub_reduce(SubNet N, SubIO io) {
 }
 
 // ---------------------------------------------------------------------------------------
-size_t sub_lds_bytes(int n, int m, int n_slots, int nz) {
+size_t sub_lds_bytes(int n, int m, int nct_cap, int nz) {
     size_t off[9];
-    return sub_lds_layout(n, m, n_slots, nz, off);
+    return sub_lds_layout(n, m, nct_cap, nz, off);
 }
 
 hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st) {
     if (io.n_paths <= 0) return hipSuccess;
-    size_t lds = sub_lds_bytes(N.n, N.m, N.n_slots, N.nz);
+    size_t lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz);
 #ifdef SGUFP_SUB_LDS_MIN
     if (lds < SGUFP_SUB_LDS_MIN) lds = SGUFP_SUB_LDS_MIN;   // occupancy experiments
 #endif
