@@ -55,7 +55,7 @@ struct SubLds {
                             //     phases 1-2 only (union), phase 5 reads dec_of from HBM
     LDS uint64_t *cta;      // [m] chains (indexed by the rank of their first arc)
     LDS uint64_t *ctb;      // [m]
-    LDS int32_t *chosen;    // [m] in-arc that chose this out-arc of a V-bar node (phases 1-2;
+    LDS int16_t *chosen;    // [m] in-arc that chose this out-arc of a V-bar node (phases 1-2;
                             //     aliases key / pred)
     LDS int64_t *key;       // [n+2] Bellman-Ford keys (cost << 16 | hops); then alpha in place
     LDS int64_t *alpha;     // == key: dual node potentials after the last Bellman-Ford
@@ -78,7 +78,7 @@ __host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int 
     off[3] = o; o = a16(o + (size_t)(n + 2) * 8);   // key | chosen
     off[4] = o; o = a16(o + (size_t)(n + 2) * 4);   // pred
     off[8] = o; o = a16(o + (size_t)(n + 2) * 2);   // plist
-    off[0] = a16(u0 + (size_t)m * 4);               // dec, after chosen
+    off[0] = a16(u0 + (size_t)m * 2);               // dec, after chosen
     if (o < a16(off[0] + (size_t)m * 2)) o = a16(off[0] + (size_t)m * 2);
     off[5] = o;
     off[6] = o; o = a16(o + (size_t)nz * 4);
@@ -500,7 +500,7 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     W.dec = (LDS int16_t *)(smem + off[0]);
     W.cta = (LDS uint64_t *)(smem + off[1]);
     W.ctb = (LDS uint64_t *)(smem + off[2]);
-    W.chosen = (LDS int32_t *)(smem + off[3]);
+    W.chosen = (LDS int16_t *)(smem + off[3]);
     W.key = (LDS int64_t *)(smem + off[3]);
     W.alpha = W.key;
     W.pred = (LDS int32_t *)(smem + off[4]);
@@ -523,9 +523,13 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     for (int a = lane(); a < m; a += kWave) {
         const int d = W.dec[a];
         if (d == -3) W.misc[0] = 1;
-        if (d >= 0 && __hip_atomic_exchange(&W.chosen[d], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != -1)
-            W.misc[0] = 1;   // two in-arcs chose one out-arc: not a path of an exact DD
+        if (d >= 0) W.chosen[d] = (int16_t)a;   // one of several writers wins ...
     }
+    wave_lds_sync();
+    for (int a = lane(); a < m; a += kWave) {
+        const int d = W.dec[a];
+        if (d >= 0 && W.chosen[d] != a) W.misc[0] = 1;   // ... the others: two in-arcs chose one
+    }                                                    // out-arc, not a path of an exact DD
     wave_lds_sync();
 
     // 2. chains, numbered in the topological order of their first arc's tail
