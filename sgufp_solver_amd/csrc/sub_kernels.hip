@@ -283,15 +283,8 @@ __device__ inline uint32_t bf_pass(const SubNet &N, const SubLds &W, int nct, in
 
 // Predecessors of the SSP labels: the smallest arc code among the residual arcs into each
 // node that are tight in (cost, hops).  Hops grow by one along such arcs, so the
-// predecessor graph has no cycle.  With reset, the labels of an earlier Bellman-Ford are
-// reused after an augmentation: every path of tight arcs that still have residual
-// capacity costs the old shortest distance, and shortest distances never decrease in SSP,
-// so such a path is a shortest path of the new residual graph.
-__device__ inline void ssp_preds(const SubNet &N, const SubLds &W, int nct, int nz, int64_t M, bool reset) {
-    if (reset) {
-        for (int v = lane(); v < N.n + 2; v += kWave) W.pred[v] = kNoPred;
-        wave_lds_sync();
-    }
+// predecessor graph has no cycle and the walk from Z_in ends at Z_out.
+__device__ inline void ssp_preds(const SubNet &N, const SubLds &W, int nct, int nz, int64_t M) {
     for_residual(N, W, nct, nz, kSsp, M, [&](int u, int v, int64_t w, int code) {
         const int64_t ku = W.key[u];
         if (ku >= kInf) return;
@@ -301,10 +294,13 @@ __device__ inline void ssp_preds(const SubNet &N, const SubLds &W, int nct, int 
     wave_lds_sync();
 }
 
-__device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M) {
+// warm: keep the keys (exact or infinite, see invalidate_subtrees) instead of starting from
+// Z_out alone -- Bellman-Ford from any upper bounds of the shortest keys reaches them.
+__device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M,
+                                    bool warm = false) {
     const int nn = N.n + 2;
     for (int v = lane(); v < nn; v += kWave) {
-        W.key[v] = (mode == kSsp) ? (v == N.n ? 0 : kInf) : 0;
+        if (!warm) W.key[v] = (mode == kSsp) ? (v == N.n ? 0 : kInf) : 0;
         W.pred[v] = kNoPred;
     }
     ChainRegs C;
@@ -320,11 +316,42 @@ __device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, i
         if (!wave_or(changed)) { converged = true; break; }
     }
     if (mode != kSsp || !converged) return converged;
-    ssp_preds(N, W, nct, nz, M, false);
+    ssp_preds(N, W, nct, nz, M);
     return true;
 }
 
 __device__ inline int64_t key_cost(int64_t k) { return k >> kHopBits; }
+
+// After an augmentation along the predecessor path of Z_in, whose used-up arcs (those whose
+// residual segment the bottleneck exhausted: the arc vanishes or its big-M cost changes)
+// already had their heads' keys set to infinity by the caller: every node whose predecessor-
+// tree path crosses one of them restarts at infinity, the others keep their keys.  Those are
+// still the shortest: the tree path survives, and SSP keys never decrease -- also in (cost,
+// hops) order, since a new path uses reverse arcs of the augmenting path, which come back
+// at equal cost with more hops.  Pointer jumping over the tree (ancestor in the path list's
+// space, dead = infinite key): a wave reads one group's entries before it writes them, and
+// later groups read after earlier ones wrote, so no lane sees a half-updated pair.
+__device__ inline void invalidate_subtrees(const SubNet &N, const SubLds &W) {
+    const int nn = N.n + 2;
+    LDS uint16_t *anc = W.plist;
+    for (int v = lane(); v < nn; v += kWave) {
+        const int32_t pr = W.pred[v];
+        anc[v] = (uint16_t)(pr == kNoPred ? v : (pr & 0x7FFF));
+    }
+    wave_lds_sync();
+    for (int r = 0; r < 32; r++) {
+        uint32_t moved = 0;
+        for (int v = lane(); v < nn; v += kWave) {
+            const int a = anc[v];
+            const int aa = anc[a];
+            const bool dead_a = W.key[a] >= kInf, dead_v = W.key[v] >= kInf;
+            if (dead_a && !dead_v) W.key[v] = kInf;
+            if (aa != a) { anc[v] = (uint16_t)aa; moved = 1; }
+        }
+        wave_lds_sync();
+        if (!wave_or(moved)) break;
+    }
+}
 
 // ---------------------------------------------------------------------------------------
 // Dual assembly for one chain a_1..a_k.  e_a = r_a - P_a - V_a is the arc's reduced reward
@@ -624,7 +651,7 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
 #ifdef SGUFP_SUB_TRACE
         const uint64_t tr0 = wall_clock64();
         uint64_t t_bf = 0, t_pred = 0, t_walk = 0, tq;
-        int nbf = 1;
+        int nbf = 0;
 #define SUB_T0() tq = wall_clock64()
 #define SUB_T1(acc) acc += wall_clock64() - tq
 #else
@@ -632,17 +659,23 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
 #define SUB_T1(acc)
 #endif
         int iters = 0;
-        bool fresh = true;   // labels and predecessors from a full Bellman-Ford
-        SUB_T0();
-        if (!bellman_ford(N, W, nct, nz, kSsp, M)) status = kSubError;
-        SUB_T1(t_bf);
+        // Each round: Bellman-Ford labels and predecessors, stop when the shortest Z_out ->
+        // Z_in path no longer gains, else augment along it.  After the first round the
+        // Bellman-Ford resumes from the previous labels, with only the subtrees under the
+        // used-up arcs restarted (invalidate_subtrees).  (Reusing the labels without any
+        // Bellman-Ford while a tight residual path survives never found one on C3 / C4.)
+        bool warm = false;
         for (; status == kSubOptimal; iters++) {
+            SUB_T0();
+            if (!bellman_ford(N, W, nct, nz, kSsp, M, warm)) { status = kSubError; break; }
+            SUB_T1(t_bf);
             const int64_t kz = W.key[n + 1];
-            if (fresh && (kz >= kInf || key_cost(kz) >= 0)) break;
+            if (kz >= kInf || key_cost(kz) >= 0) break;
             if (iters > 8 * m + 64) { status = kSubError; break; }
             // lane 0 chases the predecessors from Z_in back to Z_out into a list (one LDS
             // round trip per arc: the entry holds the tail), then the wave takes the
             // bottleneck and augments (a simple path uses each chain once)
+            SUB_T0();
             if (lane() == 0) {
                 int v = n + 1, len = 0;
                 while (v != n && len < n + 2) {
@@ -665,36 +698,24 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
                 delta = cap < delta ? cap : delta;
             }
             delta = lane_reduce<1>(delta, [](int64_t p, int64_t q) { return p < q ? p : q; });
-            if (plen < 0 || delta <= 0 || delta >= kInf) {
-                if (lane() == 0) W.misc[fresh ? 1 : 2] = 1;
-            } else {
-                for (int i = lane(); i < plen; i += kWave) {
-                    const int code = W.plist[i];
-                    if (code >= 2 * m) continue;
-                    *ch_xp(W, code >> 1) += (int16_t)((code & 1) ? -delta : delta);
-                }
+            if (plen < 0 || delta <= 0 || delta >= kInf) { status = kSubError; break; }
+            for (int i = lane(); i < plen; i += kWave) {
+                const int code = W.plist[i];
+                if (code >= 2 * m) continue;
+                const int k = code >> 1;
+                const uint64_t ca = W.cta[k], cb = W.ctb[k];
+                const int64_t x = ch_x(cb), L = ch_L(cb), U = ch_U(cb);
+                const int64_t cap = (code & 1) ? (x > L ? x - L : x) : (x < L ? L - x : U - x);
+                *ch_xp(W, k) += (int16_t)((code & 1) ? -delta : delta);
+                if (cap == delta) W.key[(code & 1) ? ch_t(ca) : ch_h(ca)] = kInf;   // segment used up
             }
             wave_lds_sync();
+            invalidate_subtrees(N, W);
+            warm = true;
             SUB_T1(t_walk);
-            if (W.misc[1]) { status = kSubError; break; }
-            if (W.misc[2]) {
-                // no tight path left under the old labels: recompute them
-                wave_lds_sync();
-                if (lane() == 0) W.misc[2] = 0;
-                wave_lds_sync();
-                SUB_T0();
-                if (!bellman_ford(N, W, nct, nz, kSsp, M)) { status = kSubError; break; }
-                SUB_T1(t_bf);
 #ifdef SGUFP_SUB_TRACE
-                nbf++;
+            nbf++;
 #endif
-                fresh = true;
-                continue;
-            }
-            SUB_T0();
-            ssp_preds(N, W, nct, nz, M, true);
-            SUB_T1(t_pred);
-            fresh = false;
         }
 #ifdef SGUFP_SUB_TRACE
         if (blockIdx.x % 997 == 0 && lane() == 0)
