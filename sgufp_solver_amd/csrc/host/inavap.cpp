@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <ctime>
 #include <sstream>
 #include <cstdio>
 #include <fstream>
@@ -215,6 +216,12 @@ double DDSolver::startSolver(double known_optimal) {
         sgufp_bnb_stats st{};
         dev.check(sgufp_bnb_step(g, diving ? std::min(batch, kDiveBatch) : batch, &z, &st), "B&B round");
         if (st.exact > 0) diving = false;
+#ifdef SOLVER_COUNTERS
+        if (st.improved) {   // DDSolver.cpp:732-738 (the device is worker 0)
+            const auto t_c = std::chrono::system_clock::to_time_t(std::chrono::system_clock::now());
+            std::cout << "Thread: " << 0 << " , optimal lb: " << z << " set at, " << std::ctime(&t_c) << std::endl;
+        }
+#endif
         rounds++;
         totals.popped += st.popped;
         totals.relaxed += st.relaxed;

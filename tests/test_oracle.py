@@ -153,3 +153,23 @@ def test_oracle_vs_reference_fresh_instances(oracle_bin, tmp_path, seed):
         subprocess.run([oracle_bin, "relax", str(net), str(tmp_path / "cuts.txt"), str(tmp_path / "nodes.txt"),
                         inc.hex(), str(tmp_path / "b.txt")], check=True)
         assert (tmp_path / "a.txt").read_text() == (tmp_path / "b.txt").read_text()
+
+
+@pytest.mark.parametrize("name", ["c2_s2_dfs", "c3_s1_dfs"])
+def test_oracle_clean_under_sanitizers(tmp_path, name):
+    """The restatement built with -fsanitize=address,undefined (oracle/Makefile `asan`, SURVEY.md
+    §5) reproduces the reference fixture with no sanitizer report (reports abort the run)."""
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "asan"], capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.skip("sanitizer runtime unavailable: " + r.stderr[-200:])
+    exe = os.path.join(ROOT, "oracle", "_build", "dd_oracle_asan")
+    d = golden_io.case_dir(name)
+    case = [c for c in golden_io.manifest() if c["name"] == name][0]
+    run = case["runs"][0]
+    out = tmp_path / "o.txt"
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1")
+    p = subprocess.run([exe, "relax", f"{d}/net.txt", f"{d}/cuts.txt", f"{d}/nodes.txt", run["incumbent"], str(out)],
+                       capture_output=True, text=True, env=env, timeout=600)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "runtime error" not in p.stderr and "AddressSanitizer" not in p.stderr
+    assert out.read_text() == golden_io.read_golden(name, run["file"])
