@@ -13,8 +13,9 @@
 //      arc with bounds [max l, min u] and reward sum r, any other chain is fixed at 0.
 //   3. Max-reward flow on the contracted DAG (free supply at sources, free demand at
 //      sinks): successive shortest paths (Bellman-Ford in LDS over the residual graph,
-//      wave-parallel relaxation, 64-bit (cost, hops) keys so the predecessor graph of
-//      equal-cost paths has no cycles).  Lower bounds ride on a big-M reward; a lower
+//      Gauss-Seidel sweeps in topological chain order, 64-bit (cost, hops) keys so the
+//      predecessor graph of equal-cost paths has no cycles, resumed after each
+//      augmentation from the labels it left intact).  Lower bounds ride on a big-M reward; a lower
 //      bound left unmet at the end is primal infeasibility.
 //   4. An optimal dual of the reference formulation (alpha from shortest-path potentials
 //      of the final residual, beta / gamma from reduced costs, lambda / mu as the free
@@ -53,8 +54,8 @@ constexpr int32_t kNoPred = INT32_MAX;
 struct SubLds {
     LDS int16_t *dec;       // [m] decision at the head (out-arc id, -1 none, -2 head not V-bar);
                             //     phases 1-2 only (union), phase 5 reads dec_of from HBM
-    LDS uint64_t *cta;      // [m] chains (indexed by the rank of their first arc)
-    LDS uint64_t *ctb;      // [m]
+    LDS uint64_t *cta;      // [nct_cap] chains, in the topological order of their tails
+    LDS uint64_t *ctb;      // [nct_cap]
     LDS int16_t *chosen;    // [m] in-arc that chose this out-arc of a V-bar node (phases 1-2;
                             //     aliases key / pred)
     LDS int64_t *key;       // [n+2] Bellman-Ford keys (cost << 16 | hops); then alpha in place
@@ -68,7 +69,7 @@ struct SubLds {
 
 __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-// LDS: chains, then a union -- phases 1-2: chosen (int32 [m]) and dec (int16 [m]);
+// LDS: chains, then a union -- phases 1-2: chosen and dec (int16 [m] each);
 // phases 3-5: key (alpha), pred, plist -- then the free-node list and flags.
 __host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int nz, size_t *off) {
     size_t o = 0;
