@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-sample", type=int, default=2048)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--profile-tag", default="r01")
+    ap.add_argument("--profile-tag", default="r02")
     ap.add_argument("--sub-paths", type=int, default=32, help="subproblem leg: random full-matching paths (0: skip)")
     ap.add_argument("--cpu-sub-seconds", type=float, default=8.0)
     ap.add_argument("--mode", choices=["relax", "bnb"], default="relax",
@@ -65,11 +65,33 @@ def parse():
     return ap.parse_args()
 
 
+def lib_sha256() -> str:
+    import hashlib
+    path = os.path.join(ROOT, "sgufp_solver_amd", "lib", "libsgufp_hip.so")
+    with open(path, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()
+
+
+# FETCH_SIZE correction on gfx950, measured by tools/calib (profiles/r02_fetch_calibration.json):
+# a coalesced 1 GiB stream of 4-, 8- or 16-byte loads per lane reports exactly 0.5 GiB of
+# FETCH_SIZE, and WRITE_SIZE reports stores of every width at 1.00 (1-byte stores 1.01).
+FETCH_CORRECTION = 2.0
+
+
 def pmc_traffic(tag: str, kernel: str = "k_relax"):
-    """HBM bytes per launch of `kernel` from committed rocprofv3 --pmc CSVs
-    (profiles/<tag>_pmc_fetch/*counter_collection.csv, profiles/<tag>_pmc_write/...).
-    gfx950: FETCH_SIZE (KB) reads half of a wide coalesced stream -> x2
-    (MI355X_MICROARCH.md §HBM); WRITE_SIZE (KB) is exact for 16-B stores."""
+    """(HBM bytes per launch of `kernel`, source) from the rocprofv3 --pmc CSVs of the same
+    bench command (profiles/<tag>_pmc_fetch/*counter_collection.csv, profiles/<tag>_pmc_write/...),
+    only when they were collected with this very library (lib.sha256 next to the CSVs);
+    otherwise (None, reason).  FETCH_SIZE x FETCH_CORRECTION + WRITE_SIZE; both count the
+    L2's fabric-side requests (Infinity-Cache hits included), so this is L2-miss traffic."""
+    want = lib_sha256()
+    for sub in ("pmc_fetch", "pmc_write"):
+        shafile = os.path.join(ROOT, "profiles", f"{tag}_{sub}", "lib.sha256")
+        if not os.path.exists(shafile):
+            return None, f"profiles/{tag}_{sub}/lib.sha256 missing"
+        with open(shafile) as fh:
+            if fh.read().strip() != want:
+                return None, f"profiles/{tag}_{sub} was collected with another build of libsgufp_hip.so"
     def load(pattern, counter):
         # only the bench launches (largest grid): the 1024-node probe launch is excluded
         rows = []
@@ -83,11 +105,13 @@ def pmc_traffic(tag: str, kernel: str = "k_relax"):
             return []
         g = max(r[0] for r in rows)
         return [v for gs, v in rows if gs == g]
-    f = load(f"{tag}_pmc_fetch*/*counter_collection.csv", "FETCH_SIZE")
-    w = load(f"{tag}_pmc_write*/*counter_collection.csv", "WRITE_SIZE")
+    f = load(f"{tag}_pmc_fetch/*counter_collection.csv", "FETCH_SIZE")
+    w = load(f"{tag}_pmc_write/*counter_collection.csv", "WRITE_SIZE")
     if not f or not w:
-        return None
-    return (2.0 * np.mean(f) + np.mean(w)) * 1024.0
+        return None, f"no {kernel} rows in profiles/{tag}_pmc_*"
+    src = (f"profiles/{tag}_pmc_fetch + {tag}_pmc_write (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of "
+           f"bench.py --steps 2, libsgufp_hip.so sha256 {want[:16]}); FETCH_SIZE x {FETCH_CORRECTION}")
+    return (FETCH_CORRECTION * np.mean(f) + np.mean(w)) * 1024.0, src
 
 
 def bnb_main(args):
@@ -251,7 +275,7 @@ def main():
     r_out = float(np.sum(2 * ch.gl.astype(np.float64) + 2 * np.diff(ch.states_off) + 24)) if ch.n else 0.0
     t_relax = float(np.mean(relax_ms)) / 1e3
     achieved = bytes_relax / t_relax / 1e9
-    traffic = pmc_traffic(args.profile_tag)
+    traffic, traffic_src = pmc_traffic(args.profile_tag)
 
     total_nodes = mine.n * world
     value = total_nodes * args.steps / elapsed
@@ -281,13 +305,19 @@ def main():
         },
         "hbm_gbps_algorithmic": round(achieved, 2),
         "roofline": {
+            # the roofline that bounds this class of kernel (no MFMA work); the kernel itself
+            # is limited by instruction issue and LDS latency, not by HBM
             "bound": "hbm",
+            "limiter": "latency/issue (measured HBM traffic is a fraction of the algorithmic bytes)",
             "kernel": "k_relax",
             "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
+            "traffic_gbps": round(traffic / t_relax / 1e9, 2) if traffic else None,
+            "frac_traffic": round(traffic / t_relax / 1e9 / HBM_PEAK_GBPS, 4) if traffic else None,
+            "traffic_source": traffic_src,
             "bytes_per_launch": bytes_relax,
             "avg_launch_ms": round(t_relax * 1e3, 4),
             "emit_ms": round(float(np.mean(emit_ms)), 4),

@@ -1,6 +1,9 @@
 """Native build: hipcc for gfx950, in-tree outputs (they travel to the GPU box).
 
     libsgufp_hip.so   kernels + C ABI (include/sgufp_hip.h)
+    lib_verify/libsgufp_hip.so
+                      the same with SGUFP_SUB_VERIFY: every warm-started Bellman-Ford of the
+                      subproblem is re-run cold and compared (debug build for tests)
     libsgufp_host.so  C++ mirror of the reference's host API (Network / NodeExplorer /
                       GuroSolver / DDSolver, include/sgufp/inavap.hpp) on top of the C ABI
     host_api_test     C++ driver of that API (tests/host/host_api_test.cpp)
@@ -61,6 +64,17 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
     lib = os.path.join(LIBDIR, "libsgufp_hip.so")
     if force or _stale(lib, objs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs])
+    # debug variant: subproblem kernels with the warm Bellman-Ford cross-check
+    vdir = os.path.join(HERE, "lib_verify")
+    os.makedirs(vdir, exist_ok=True)
+    vsrc = os.path.join(CSRC, "sub_kernels.hip")
+    vobj = os.path.join(objdir, "sub_kernels_verify.o")
+    if force or _stale(vobj, [vsrc] + headers):
+        _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-DSGUFP_SUB_VERIFY", "-x", "hip", "-c", vsrc, "-o", vobj])
+    vlib = os.path.join(vdir, "libsgufp_hip.so")
+    vobjs = [vobj if os.path.basename(o) == "sub_kernels.hip.o" else o for o in objs]
+    if force or _stale(vlib, vobjs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", vlib, *vobjs])
     host_srcs = [os.path.join(CSRC, s) for s in HOST_SOURCES if os.path.exists(os.path.join(CSRC, s))]
     if host_srcs:
         hlib = os.path.join(LIBDIR, "libsgufp_host.so")

@@ -65,6 +65,9 @@ struct SubLds {
     double GBL *coef;       // [n_slots] this (path, scenario)'s row of SubIO::coef (phase 5)
     LDS int32_t *zlist;     // [nz] free-supply / free-demand nodes: v | src << 30 | snk << 29
     LDS int32_t *misc;      // [8] flags
+#ifdef SGUFP_SUB_VERIFY
+    LDS int64_t *vkey;      // [n+2] warm Bellman-Ford keys, compared with a cold run
+#endif
 };
 
 __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -84,6 +87,9 @@ __host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int 
     off[5] = o;
     off[6] = o; o = a16(o + (size_t)nz * 4);
     off[7] = o; o = a16(o + 8 * 4);
+#ifdef SGUFP_SUB_VERIFY
+    off[9] = o; o = a16(o + (size_t)(n + 2) * 8);
+#endif
     return o;
 }
 
@@ -317,6 +323,27 @@ __device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, i
         if (!wave_or(changed)) { converged = true; break; }
     }
     if (mode != kSsp || !converged) return converged;
+#ifdef SGUFP_SUB_VERIFY
+    // Debug build: the labels a warm start converged to must equal those of a cold
+    // Bellman-Ford from Z_out alone (invalidate_subtrees' exactness argument, checked).
+    if (warm) {
+        for (int v = lane(); v < nn; v += kWave) {
+            W.vkey[v] = W.key[v];
+            W.key[v] = (v == N.n) ? 0 : kInf;
+        }
+        wave_lds_sync();
+        bool cold_ok = false;
+        for (int it = 0; it < nn + 2; it++) {
+            const uint32_t changed = bf_pass(N, W, nct, nz, mode, M, C);
+            wave_lds_sync();
+            if (!wave_or(changed)) { cold_ok = true; break; }
+        }
+        uint32_t diff = cold_ok ? 0u : 1u;
+        for (int v = lane(); v < nn; v += kWave) diff |= (W.vkey[v] != W.key[v]) ? 1u : 0u;
+        if (wave_or(diff) && lane() == 0) W.misc[6] = 1;
+        wave_lds_sync();
+    }
+#endif
     ssp_preds(N, W, nct, nz, M);
     return true;
 }
@@ -522,7 +549,7 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     const int S = N.S;
     const int p = blockIdx.x / S, s = blockIdx.x - p * S;
     if (p >= io.n_paths) return;
-    size_t off[9];
+    size_t off[10];
     sub_lds_layout(N.n, N.m, io.nct_cap, N.nz, off);
     SubLds W;
     W.dec = (LDS int16_t *)(smem + off[0]);
@@ -536,6 +563,9 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     W.coef = io.coef + ((size_t)p * S + s) * N.n_slots;
     W.zlist = (LDS int32_t *)(smem + off[6]);
     W.misc = (LDS int32_t *)(smem + off[7]);
+#ifdef SGUFP_SUB_VERIFY
+    W.vkey = (LDS int64_t *)(smem + off[9]);
+#endif
     const int n = N.n, m = N.m;
     const size_t so = (size_t)s * m;
     const int64_t poff = io.path_off[p], plen = io.path_off[p + 1] - poff;
@@ -615,15 +645,20 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     }
 
     int status = kSubOptimal;
-    int64_t M = 1;
+    int64_t M = 1, max_aug = 0;
     for (int k = lane(); k < nct; k += kWave) {
         const uint64_t ca = W.cta[k];
         if (ch_t(ca) >= 0 && ch_h(ca) >= 0) {
-            const int64_t R = ch_R(ca);
-            M += 2 * (R < 0 ? -R : R) * ((int64_t)ch_U(W.ctb[k]) + 1);
+            const int64_t R = ch_R(ca), U = ch_U(W.ctb[k]);
+            M += 2 * (R < 0 ? -R : R) * (U + 1);
+            max_aug += U > 0 ? U : 0;
         }
     }
     M = lane_reduce<1>(M, [](int64_t x, int64_t y) { return x + y; }) - (kWave - 1);
+    // Every augmentation moves delta >= 1 more units from Z_out to Z_in, and that flow
+    // crosses at least one complete chain, so the number of augmentations is at most the
+    // sum of the chains' capacities (min u): the loop below stops after that many.
+    max_aug = lane_reduce<1>(max_aug, [](int64_t x, int64_t y) { return x + y; });
     int ray_chain = -1, ray_p = -1, ray_q = -1;
     int64_t primal = 0;
 
@@ -670,9 +705,12 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
             SUB_T0();
             if (!bellman_ford(N, W, nct, nz, kSsp, M, warm)) { status = kSubError; break; }
             SUB_T1(t_bf);
+#ifdef SGUFP_SUB_VERIFY
+            if (W.misc[6]) { status = kSubError; break; }
+#endif
             const int64_t kz = W.key[n + 1];
             if (kz >= kInf || key_cost(kz) >= 0) break;
-            if (iters > 8 * m + 64) { status = kSubError; break; }
+            if (iters >= max_aug) { status = kSubError; break; }   // cannot happen (bound above)
             // lane 0 chases the predecessors from Z_in back to Z_out into a list (one LDS
             // round trip per arc: the entry holds the tail), then the wave takes the
             // bottleneck and augments (a simple path uses each chain once)
@@ -843,7 +881,7 @@ __global__ void __launch_bounds__(256) k_sub_reduce(SubNet N, SubIO io) {
 
 // ---------------------------------------------------------------------------------------
 size_t sub_lds_bytes(int n, int m, int nct_cap, int nz) {
-    size_t off[9];
+    size_t off[10];
     return sub_lds_layout(n, m, nct_cap, nz, off);
 }
 

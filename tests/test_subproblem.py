@@ -166,3 +166,36 @@ def test_subproblem_matches_highs(cfg, seed, S, zl, trials):
         assert "opt" in seen            # optimality cuts exercised
     else:
         assert "feas" in seen           # feasibility rays exercised
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,seed,S,n_paths", [("C3", 1, 8, 8), ("C3", 2, 8, 8), ("C5", 1, 2, 4)])
+def test_warm_bellman_ford_matches_cold(cfg, seed, S, n_paths, tmp_path):
+    """The warm-started Bellman-Ford after each augmentation (invalidate_subtrees) must
+    reach the labels a cold Bellman-Ford reaches.  The verify build (lib_verify,
+    -DSGUFP_SUB_VERIFY) re-runs every warm Bellman-Ford cold and turns any difference into
+    kSubError; its results must be identical to the production library's."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    helper = os.path.join(here, "tests", "helpers", "sub_run.py")
+    vlib = os.path.join(here, "sgufp_solver_amd", "lib_verify", "libsgufp_hip.so")
+    assert os.path.exists(vlib), "verify build missing: run __graft_entry__.build()"
+    res = {}
+    for name, lib in (("prod", None), ("verify", vlib)):
+        env = dict(os.environ)
+        env.pop("SGUFP_LIB_PATH", None)
+        if lib:
+            env["SGUFP_LIB_PATH"] = lib
+        out = str(tmp_path / f"{name}.npz")
+        subprocess.run([sys.executable, helper, cfg, str(seed), str(S), str(n_paths), out], env=env,
+                       check=True, timeout=240)
+        res[name] = np.load(out)
+    assert str(res["verify"]["lib"]).endswith("lib_verify/libsgufp_hip.so")
+    a, b = res["prod"], res["verify"]
+    assert (b["st"] != 2).all(), "a warm Bellman-Ford disagreed with the cold one (or another error)"
+    assert (a["st"] == 0).any()
+    for k in ("typ", "st"):
+        np.testing.assert_array_equal(a[k], b[k])
+    for k in ("rhs", "rows", "obj_mean", "obj", "dual"):
+        np.testing.assert_array_equal(a[k].view(np.uint64), b[k].view(np.uint64))
