@@ -112,7 +112,8 @@ constexpr int kLdsBatchWidth = 128;
 constexpr int kStageEntries = 128;   // coefficient staging ring: f64 entries per slot (2 per lane)
 constexpr int kTopoEntries = 512;    // topology staging ring: u16 entries per slot (8 per lane)
 constexpr int kStageLayers = 16;     // at most this many layers per staging group
-constexpr int kMaxRun = 4;           // exact layers folded in registers per narrow-sweep step
+constexpr int kMaxRun = 5;           // exact layers folded in registers per narrow-sweep step (odd)
+constexpr uint32_t kNarrowMax = 127;  // widest narrow layer; value slot 127 holds the NaN sentinel
 constexpr uint16_t kMirParent = 127, kMirRankShift = 7, kMirAlive = 1u << 12, kMirIn = 1u << 13;
 
 // Packed topology of the narrow layers (HBM, per DD slot): node word = parent:7 | rank:5 |
@@ -125,7 +126,8 @@ __device__ __forceinline__ void mir_node_clear(DD &d, uint32_t node, uint16_t bi
     if (d.stream && node < d.Nn) d.tmir[node] &= (uint16_t)~bits;
 }
 __device__ __forceinline__ void mir_arc_clear(DD &d, uint32_t a) {
-    if (d.stream) d.tmir[d.Nn + a] &= (uint16_t)~kMirAlive;
+    // dead: no alive bit, parent slot = the NaN sentinel of the narrow sweep
+    if (d.stream) d.tmir[d.Nn + a] = (uint16_t)((d.tmir[d.Nn + a] & ~(kMirAlive | kMirParent)) | kNarrowMax);
 }
 
 struct LdsCarve {
@@ -741,7 +743,7 @@ __device__ __forceinline__ void build_stream(DD &d, uint32_t n_merged_arcs, int 
     int kg = d.T - 1;
     for (int base = 0; base < d.T - 1; base += kWave) {
         int k = base + lane();
-        uint64_t b = __ballot(k < d.T - 1 && (d.nn[k]) > (uint32_t)kLdsBatchWidth);
+        uint64_t b = __ballot(k < d.T - 1 && (d.nn[k]) > kNarrowMax);
         if (b) { kg = base + (int)(__ffsll((unsigned long long)b) - 1); break; }
     }
     d.kg = kg;
@@ -772,8 +774,10 @@ __device__ __forceinline__ void build_stream(DD &d, uint32_t n_merged_arcs, int 
     }
     for (uint32_t a = lane(); a < d.Amir; a += kWave) {
         uint32_t t = d.atopo[a];
-        d.tmir[d.Nn + a] = (uint16_t)((t & kMirParent) | (((t >> kRankShift) & 31u) << kMirRankShift) |
-                                      ((d.aflag[a] & kAlive) ? kMirAlive : 0));
+        // a dead merged arc points at the NaN sentinel slot (see sweep_narrow)
+        const bool al = (d.aflag[a] & kAlive) != 0;
+        d.tmir[d.Nn + a] = (uint16_t)((al ? (t & kMirParent) : kNarrowMax) | (((t >> kRankShift) & 31u) << kMirRankShift) |
+                                      (al ? kMirAlive : 0));
     }
     wave_mem_sync();
 }
@@ -810,6 +814,9 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
         bv.vb[c] = rv;
         if (c == nb - 1) d.s2[0] = rv;
     }
+    // NaN sentinel in slot kNarrowMax of both value buffers (dead merged arcs point there)
+    if (lane() < 2 * CB)
+        bv.vb[(size_t)(lane() / CB) * kLdsBatchWidth * CB + kNarrowMax * CB + (lane() % CB)] = __builtin_nan("");
     if (d.ng == 0) return;
     double pf[PC] = {};
     uint32_t pt[PT] = {};
@@ -842,117 +849,120 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
 #pragma unroll
         for (int jj = 0; jj < PT; jj++) tr[lane() + jj * kWave] = (uint16_t)pt[jj];
     };
-    // Exact run [ka, kb] (see the call site).  Items: nodes lane and lane + 64 of layer kb.
-    // Per-level layer metadata is read by lane s in one LDS access and moved to SGPRs;
-    // the walk packs the decision rank and in-arc flag (6 bits) and node index (7 bits)
-    // of every level into two u64 registers; the coefficients of all levels are loaded
-    // together before the fold, so a run costs the walk (one LDS access per level) plus
-    // two more LDS round trips.
-    auto fold_run = [&](int ka, int kb, int slot_, int k0_, uint32_t gn0_) {
-        const int dep = kb - ka + 1;
+    // Per-group layer metadata in registers: lane l <-> layer k0 + l of the current staging
+    // group (and the layers after it): node offset, merged-arc offset and a packed word
+    // nn:8 | acnt:12 | w1 (bit 31), read per layer with v_readlane instead of a serialised
+    // LDS round trip per field; mmask: which of those layers are merged layers.
+    uint32_t m_noff = 0, m_aoff = 0, m_pk = 0;
+    uint64_t mmask = 0;
+    auto load_meta = [&](int kw) {
+        const int k = kw + lane();
+        const bool ok = k < d.T;
+        const int kk = ok ? k : 0;
+        const uint32_t no = d.noff[kk], ao = d.aoff[kk], nn = d.nn[kk], ac = d.acnt[kk];
+        const uint32_t w = bv.w1[kk];
+        sched_fence();
+        m_noff = no;
+        m_aoff = ao;
+        m_pk = (nn < 255u ? nn : 255u) | ((ac & 0xFFFu) << 8) | (w ? 0x80000000u : 0u);
+        mmask = __ballot(ok && ac != 0);
+    };
+    auto rl = [](uint32_t v, int l) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); };
+
+    // Exact run [ka, kb] of odd depth D (see the call site).  Every node has one in-arc, so
+    // a node's value is the fold of its ancestors' steps from layer ka - 1,
+    // x = !in ? DMIN : (reg ? x + coef : x) -- the same operations in the same order as
+    // layer by layer.  Lanes are (node of layer kb, cut) pairs: item i = pass * G + grp,
+    // cut c.  A lane walks up its node's ancestors' topology words (one dependent LDS read
+    // per level, batched over the lane's U items), then loads the root value and the
+    // coefficients of every level in one batch and folds.  Only layer kb goes through LDS;
+    // odd depth puts layers ka - 1 and kb in different value buffers, so items write their
+    // results as they go.  Every alive node of the run is an ancestor of an alive node of
+    // layer kb (the deletion cascade removes childless parents), so the width-1 summaries
+    // and walk state2 of the inner layers are written on the way (lanes that share an
+    // ancestor write the same value; items past the layer repeat its last node).
+    auto fold_run = [&](auto Dc, int ka, int slot_, int k0_, uint32_t gn0_) {
+        constexpr int D = decltype(Dc)::value;
+        const int kb = ka + D - 1;
         const LDS uint16_t *tr = bv.tring + (size_t)slot_ * kTopoEntries;
         const LDS double *ring = bv.cring + (size_t)slot_ * kStageEntries;
         const LDS double *pb = bv.vb + (size_t)((ka - 1) & 1) * kLdsBatchWidth * CB;
         LDS double *ob = bv.vb + (size_t)(kb & 1) * kLdsBatchWidth * CB;
-        const int tl = min(ka + min(lane(), kMaxRun - 1), kb);
-        const uint32_t l_noff = d.noff[tl], l_w1 = bv.w1[tl], l_anx = d.acnt[tl + 1];
-        const uint32_t nlast = uni(d.nn[kb]);
-        uint32_t ebase[kMaxRun], nofs[kMaxRun];
-        bool w1s[kMaxRun], wrs[kMaxRun];
+        const int l0 = ka - k0_;
+        uint32_t ebase[D], nofs[D];
+        bool w1s[D], wrs[D];
 #pragma unroll
-        for (int s = 0; s < kMaxRun; s++) {
-            nofs[s] = (uint32_t)__builtin_amdgcn_readlane((int)l_noff, s);
+        for (int s = 0; s < D; s++) {
+            nofs[s] = rl(m_noff, l0 + s);
             ebase[s] = nofs[s] - gn0_;
-            w1s[s] = s < dep && __builtin_amdgcn_readlane((int)l_w1, s) != 0;
-            wrs[s] = s < dep && ka + s < kS && (kS >= d.T || __builtin_amdgcn_readlane((int)l_anx, s) != 0);
+            w1s[s] = (rl(m_pk, l0 + s) >> 31) != 0;
+            wrs[s] = ka + s < kS && (kS >= d.T || ((mmask >> (l0 + s + 1)) & 1ull) != 0);
         }
-        const int nu = nlast > (uint32_t)kWave ? 2 : 1;
-        double res[2][CB];
-        // one item at a time (the second one, only for layers wider than a wave, behind a
-        // uniform branch): the per-level coefficient registers are not doubled
-        auto item = [&](const int u, double (&out)[CB]) {
-            {
-                const uint32_t i = (uint32_t)lane() + (uint32_t)u * kWave;
-                const bool ok = i < nlast;
-                uint64_t code = 0, ids = 0;
-                uint32_t cur = ok ? i : 0u;
-                bool alive = false;
+        const uint32_t nlast = rl(m_pk, l0 + D - 1) & 255u;
+        const bool wlane = c == nb - 1;   // the lane whose cut's state2 the path walks read
+        auto items = [&](auto Uc, uint32_t base) {
+            constexpr int U = decltype(Uc)::value;
+            uint32_t cur[U], wl[U][D];   // wl: topology word | node index << 16, per level
 #pragma unroll
-                for (int s = kMaxRun - 1; s >= 0; s--) {
-                    if (s < dep) {
-                        const uint32_t wd = (uint32_t)tr[ebase[s] + cur];
-                        if (s == dep - 1) alive = ok && (wd & kMirAlive) != 0;
-                        code |= (uint64_t)(((wd >> kMirRankShift) & 31u) | ((wd & kMirIn) ? 32u : 0u)) << (6 * s);
-                        ids |= (uint64_t)cur << (7 * s);
-                        cur = wd & kMirParent;
+            for (int u = 0; u < U; u++) {
+                const uint32_t i = base + (uint32_t)(u * G + grp);
+                cur[u] = i < nlast ? i : nlast - 1u;
+            }
+#pragma unroll
+            for (int s = D - 1; s >= 0; s--) {
+                uint32_t w[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) w[u] = (uint32_t)tr[ebase[s] + cur[u]];
+                sched_fence();
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    wl[u][s] = w[u] | (cur[u] << 16);
+                    cur[u] = w[u] & kMirParent;
+                }
+            }
+            double x[U], cf[U][D];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                x[u] = pb[cur[u] * CB + c];
+#pragma unroll
+                for (int s = 0; s < D; s++)
+                    cf[u][s] = ring[(size_t)(l0 + s) * per_layer + c * us + ((wl[u][s] >> kMirRankShift) & 31u)];
+            }
+            sched_fence();
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const bool alive = (wl[u][D - 1] & kMirAlive) != 0;
+                double xv = x[u];
+#pragma unroll
+                for (int s = 0; s < D; s++) {
+                    const uint32_t w = wl[u][s];
+                    const bool in = (w & kMirIn) != 0, reg = (w & (31u << kMirRankShift)) != 0;
+                    const double xn = !in ? DMIN : (reg ? xv + cf[u][s] : xv);
+                    if (alive && w1s[s] && cv) {
+                        bv.sm[(size_t)(ka + s) * CB + c] = xn;
+                        bv.xm[(size_t)(ka + s) * CB + c] = !in ? DMAX : (reg ? xn : xv + 0.0);
                     }
+                    xv = xn;
+                    if (alive && wrs[s] && wlane) d.s2[nofs[s] + (w >> 16)] = xv;
                 }
-                double x[CB], cfs[kMaxRun][CB];
-#pragma unroll
-                for (int c2 = 0; c2 < CB; c2++) x[c2] = pb[cur * CB + c2];
-#pragma unroll
-                for (int s = 0; s < kMaxRun; s++) {
-                    const uint32_t r = (uint32_t)(code >> (6 * s)) & 31u;
-                    const LDS double *cf = ring + (size_t)(ka + s - k0_) * per_layer + r;
-#pragma unroll
-                    for (int c2 = 0; c2 < CB; c2++) cfs[s][c2] = (s < dep && c2 < nb) ? cf[c2 * us] : 0.0;
-                }
-#pragma unroll
-                for (int s = 0; s < kMaxRun; s++) {
-                    if (s < dep) {
-                        const uint32_t cd = (uint32_t)(code >> (6 * s)) & 63u;
-                        const bool in = (cd & 32u) != 0;
-                        const bool reg = (cd & 31u) != 0;
-#pragma unroll
-                        for (int c2 = 0; c2 < CB; c2++) {
-                            if (c2 < nb) {
-                                const double xn = !in ? DMIN : (reg ? x[c2] + cfs[s][c2] : x[c2]);
-                                if (alive && w1s[s]) {
-                                    bv.sm[(size_t)(ka + s) * CB + c2] = xn;
-                                    bv.xm[(size_t)(ka + s) * CB + c2] = !in ? DMAX : (reg ? xn : x[c2] + 0.0);
-                                }
-                                x[c2] = xn;
-                            }
-                        }
-                        if (alive && wrs[s]) {
-                            double v = x[0];
-#pragma unroll
-                            for (int c2 = 1; c2 < CB; c2++) v = (c2 == nb - 1) ? x[c2] : v;
-                            d.s2[nofs[s] + (uint32_t)((ids >> (7 * s)) & 127u)] = v;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int c2 = 0; c2 < CB; c2++) out[c2] = x[c2];
+                ob[(wl[u][D - 1] >> 16) * CB + c] = xv;
             }
         };
-        item(0, res[0]);
-        if (nu == 2) item(1, res[1]);
-        // both items read their root values before either writes layer kb (the two
-        // buffers coincide when the run has an even number of layers)
-        wave_lds_sync();
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-            const uint32_t i = (uint32_t)lane() + (uint32_t)u * kWave;
-            if (u < nu && i < nlast) {
-#pragma unroll
-                for (int c2 = 0; c2 < CB; c2++)
-                    if (c2 < nb) ob[i * CB + c2] = res[u][c2];
-            }
-        }
+        const uint32_t per = (nlast + G - 1) / G;
+        if (per <= 1) items(std::integral_constant<int, 1>{}, 0u);
+        else
+            for (uint32_t base = 0; base < nlast; base += 2 * G) items(std::integral_constant<int, 2>{}, base);
     };
 
     issue(0);
     commit(0);
     issue(1);
-    wave_lds_sync();
     int j = 0, slot = 0;
     int k0 = uni((int)d.gstart[0]), k1 = uni((int)d.gstart[1]);
-    uint32_t gn0 = uni(d.noff[k0]), gnN = uni(d.noff[k1]) - gn0, ga0 = uni(d.aoff[k0]);
+    load_meta(k0);
+    uint32_t gn0 = rl(m_noff, 0), gnN = rl(m_noff, k1 - k0) - gn0, ga0 = rl(m_aoff, 0);
+    wave_lds_sync();
     for (int k = 1; k < d.kg;) {
-#ifdef SGUFP_PROF
-        uint64_t t0 = wall_clock64();
-#endif
         if (k == k1) {
             // next group: its words and coefficients were issued one group ago
             j++;
@@ -961,83 +971,75 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
             issue(j + 1);
             k0 = k1;
             k1 = uni((int)d.gstart[j + 1]);
-            gn0 = uni(d.noff[k0]);
-            gnN = uni(d.noff[k1]) - gn0;
-            ga0 = uni(d.aoff[k0]);
+            load_meta(k0);
+            gn0 = rl(m_noff, 0);
+            gnN = rl(m_noff, k1 - k0) - gn0;
+            ga0 = rl(m_aoff, 0);
             wave_lds_sync();
         }
-#ifdef SGUFP_PROF
-        uint64_t t1 = wall_clock64();
-        bv.prof[0] += t1 - t0;
-#endif
-#ifdef SGUFP_TRACE
-        const uint64_t tl0 = __builtin_amdgcn_s_memtime();
-#endif
-        const LDS double *coefk = bv.cring + (size_t)slot * kStageEntries + (size_t)(k - k0) * per_layer;
+        const int l = k - k0;
+        const LDS double *coefk = bv.cring + (size_t)slot * kStageEntries + (size_t)l * per_layer;
         const LDS uint16_t *tr = bv.tring + (size_t)slot * kTopoEntries;
-        const uint32_t noff = uni(d.noff[k]), n = uni(d.nn[k]);
+        const uint32_t pk = rl(m_pk, l);
+        const uint32_t noff = rl(m_noff, l), acnt = (pk >> 8) & 0xFFFu;
         const LDS double *pbuf = bv.vb + (size_t)((k - 1) & 1) * kLdsBatchWidth * CB;
         LDS double *cbuf = bv.vb + (size_t)(k & 1) * kLdsBatchWidth * CB;
-        const bool w1 = uni(bv.w1[k]) != 0;
-        const uint32_t acnt = uni(d.acnt[k]);
-        // state2 of the last batch cut: only what a path walk reads (merged nodes and their
-        // parents) unless every layer is asked for (kS = T: the exact redo of one cut)
-        const bool wr = k < kS && (kS >= d.T || acnt > 0 || uni(d.acnt[k + 1]) > 0);
-        auto word = [&](uint32_t e) -> uint32_t { return (uint32_t)tr[e]; };
-        // U independent items per lane per step (U sized to the layer): all topology words
-        // first, then all parent values / coefficients, so one step costs two LDS round
-        // trips and a narrow layer runs no idle unrolled items.
-        auto dispatch = [&](uint32_t count, auto &&step) {
-            const uint32_t per = (count + G - 1) / G;
-            if (per <= 1) step(std::integral_constant<int, 1>{}, 0u);
-            else if (per <= 2) step(std::integral_constant<int, 2>{}, 0u);
-            else if (per <= 4) step(std::integral_constant<int, 4>{}, 0u);
-            else
-                for (uint32_t base = 0; base < count; base += G * 8) step(std::integral_constant<int, 8>{}, base);
-        };
+        const bool w1 = (pk >> 31) != 0;
         if (acnt) {
-            const uint32_t aoff = uni(d.aoff[k]);
+            // state2 of the last batch cut: only what a path walk reads (merged nodes and
+            // their parents) unless every layer is asked for (kS = T: the exact redo)
+            const bool wr = k < kS;
+            const uint32_t aoff = rl(m_aoff, l);
             const uint32_t ebase = gnN + (aoff - ga0);   // ring entry of the layer's first arc
-            // Fast path: a plain max over the candidates.  The (value, priority) pick of the
-            // reference's mixed-order folds only differs from it when the maximum is a zero
-            // (equal doubles differ only in the sign of zero); that case re-runs the layer
+            auto word = [&](uint32_t e) -> uint32_t { return (uint32_t)tr[e]; };
+            // U independent items per lane per step (U sized to the layer): all topology
+            // words first, then all parent values / coefficients, so one step costs two LDS
+            // round trips and a narrow layer runs no idle unrolled items.
+            auto dispatch = [&](uint32_t count, auto &&step) {
+                const uint32_t per = (count + G - 1) / G;
+                if (per <= 1) step(std::integral_constant<int, 1>{}, 0u);
+                else if (per <= 2) step(std::integral_constant<int, 2>{}, 0u);
+                else if (per <= 4) step(std::integral_constant<int, 4>{}, 0u);
+                else
+                    for (uint32_t base = 0; base < count; base += G * 8) step(std::integral_constant<int, 8>{}, base);
+            };
+            // Fast path: a plain max / min over the candidates parent + coefficient.  Dead
+            // arcs carry parent slot 127 (kNarrowMax), whose value is a quiet NaN that
+            // fmax / fmin skip; items past the layer repeat its last arc; the decision -1
+            // (rank 0) has coefficient +0.0, so its candidate is parent + 0.0, which is what
+            // the width-1 summary takes and equals the parent except for the sign of zero.
+            // The (value, priority) pick of the reference's mixed-order folds differs from
+            // the plain max only when the maximum is a zero; that case re-runs the layer
             // with the exact pick below.
-            double mx = -INFINITY;
-            double xmin = DMAX;
-            bool any = false;
+            double mx = -INFINITY, xmin = INFINITY;
+            const uint32_t alast = acnt - 1u;
             dispatch(acnt, [&](auto Uc, uint32_t base) {
                 constexpr int U = decltype(Uc)::value;
-                uint32_t p[U], r[U];
-                bool al[U];
-                // branch-free: out-of-range items read entry 0 and are masked afterwards,
-                // so all loads of a step issue back to back
+                uint32_t wd[U];
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    const uint32_t a = base + u * G + grp;
-                    const bool ok = (a < acnt) & cv;
-                    const uint32_t wd = word(ebase + (ok ? a : 0u));
-                    p[u] = wd & kMirParent; r[u] = (wd >> kMirRankShift) & 31u; al[u] = ok & ((wd & kMirAlive) != 0);
+                    const uint32_t a = base + (uint32_t)(u * G + grp);
+                    wd[u] = word(ebase + (a < alast ? a : alast));
                 }
+                sched_fence();
                 double px[U], cf[U];
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    px[u] = pbuf[(al[u] ? p[u] : 0u) * CB + c];
-                    cf[u] = coefk[(al[u] ? c * us + r[u] : 0u)];
+                    px[u] = pbuf[(wd[u] & kMirParent) * CB + c];
+                    cf[u] = coefk[c * us + ((wd[u] >> kMirRankShift) & 31u)];
                 }
+                sched_fence();
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    const bool reg = r[u] != 0;
-                    const double v = reg ? px[u] + cf[u] : px[u];
-                    const double y = reg ? v : px[u] + 0.0;
-                    mx = (al[u] & (v > mx)) ? v : mx;
-                    xmin = al[u] ? fmin(xmin, y) : xmin;
-                    any = any | al[u];
+                    const double v = px[u] + cf[u];
+                    mx = __builtin_fmax(mx, v);
+                    xmin = __builtin_fmin(xmin, v);
                 }
             });
             mx = lane_reduce<CB>(mx, [](double a, double b) { return (b > a) ? b : a; });
             // across the lane groups of each cut (lanes that differ in bits >= log2(CB))
-            xmin = lane_reduce<CB>(xmin, [](double a, double b) { return fmin(a, b); });
-            any = lane_reduce<CB>((uint32_t)any, [](uint32_t a, uint32_t b) { return a | b; }) != 0;
+            xmin = lane_reduce<CB>(xmin, [](double a, double b) { return __builtin_fmin(a, b); });
+            const bool any = mx != -INFINITY;
             VP best{mx, any ? 0 : INT_MIN};
             if (__ballot(mx == 0.0) != 0) {
                 best = VP{0.0, INT_MIN};
@@ -1061,15 +1063,6 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
                 });
                 best = wave_vp<CB>(best);
             }
-#ifdef SGUFP_TRACE
-            const uint64_t tla = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef SGUFP_TRACE
-            const uint64_t tlb = __builtin_amdgcn_s_memtime();
-            if (blockIdx.x == 0 && lane() == 0 && bv.trace_on)
-                printf("M k=%d acnt=%u loop=%llu red=%llu\n", k, acnt, (unsigned long long)(tla - tl0),
-                       (unsigned long long)(tlb - tla));
-#endif
             if (grp == 0 && cv) {
                 double v = (best.p == INT_MIN) ? DMIN : smax(best.v, DMIN);
                 cbuf[c] = v;
@@ -1079,38 +1072,25 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
                     bv.xm[(size_t)k * CB + c] = any ? xmin : DMAX;
                 }
             }
-#ifdef SGUFP_PROF
-            wave_lds_sync();
-            bv.prof[1] += wall_clock64() - t1;
-#endif
             wave_lds_sync();
             k++;
             continue;
         }
-        // A run of exact (tree) layers [k, kb] inside the staging group: every node has one
-        // in-arc, so a node's value is the fold of its ancestors' steps from the layer
-        // before the run, x = !in ? DMIN : (reg ? x + coef : x) -- the same operations in the
-        // same order as layer by layer.  Each lane owns nodes of layer kb, walks up their
-        // ancestors' topology words once (shared by the CB cuts) and folds in registers;
-        // only layer kb goes through LDS.  Every alive node of the run is an ancestor of an
-        // alive node of layer kb (the deletion cascade removes childless parents), so the
-        // width-1 summaries and walk state2 of the inner layers are written on the way
-        // (lanes that share an ancestor write the same value).
+        // A run of exact (tree) layers [k, kb] inside the staging group, ended by the next
+        // merged layer; odd depth (see fold_run).
         int kb = min(min(k1, d.kg) - 1, k + kMaxRun - 1);
         {
-            const int t = k + lane();
-            const uint64_t b = __ballot(lane() < kMaxRun && t <= kb && d.acnt[t] != 0);
+            const int span = kb - k + 1;
+            const uint64_t b = (mmask >> l) & ((1ull << span) - 1ull);
             if (b) kb = k + (int)(__ffsll((unsigned long long)b) - 1) - 1;
+            if (((kb - k) & 1) != 0) kb--;
         }
-        fold_run(k, kb, slot, k0, gn0);
+        switch (kb - k) {
+            case 0: fold_run(std::integral_constant<int, 1>{}, k, slot, k0, gn0); break;
+            case 2: fold_run(std::integral_constant<int, 3>{}, k, slot, k0, gn0); break;
+            default: fold_run(std::integral_constant<int, 5>{}, k, slot, k0, gn0); break;
+        }
         wave_lds_sync();
-#ifdef SGUFP_TRACE
-        {
-            const uint64_t tl1 = __builtin_amdgcn_s_memtime();
-            if (blockIdx.x == 0 && lane() == 0 && bv.trace_on)
-                printf("L k=%d kb=%d n=%u acnt=0 w1=%d cyc=%llu\n", k, kb, n, (int)w1, (unsigned long long)(tl1 - tl0));
-        }
-#endif
         k = kb + 1;
     }
 #ifdef SGUFP_TRACE

@@ -32,6 +32,12 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// Scheduling fence: the compiler moves no instruction across it.  At 256 VGPRs the
+// machine scheduler otherwise interleaves each LDS load with its first use (one
+// s_waitcnt lgkmcnt(0) per load); a fence after a block of independent loads keeps them
+// issued back to back, so the block costs one LDS latency instead of one per load.
+__device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+
 // Global-memory hand-off between lanes of the wave (stores complete, then loads).
 __device__ __forceinline__ void wave_mem_sync() { __syncthreads(); }
 
