@@ -1105,51 +1105,119 @@ __device__ __forceinline__ double batch_value(const DD &d, const BatchView &bv, 
     return bv.vb[(size_t)(k & 1) * kLdsBatchWidth * CB + p * CB + c];
 }
 
-// One tail layer (k >= kg, exact expansion) into HBM: several independent nodes per
-// lane per step so that the loads overlap.
+// Values of the layer before a wide layer: node p, all CB batch cuts (32 contiguous
+// bytes at CB = 4).  In LDS when that layer is narrow (k - 1 < kg), else in HBM (s2b).
+template <int CB, bool PV_LDS>
+struct ParentVals {
+    const LDS double *lds;
+    const GBL double *gbl;
+    __device__ __forceinline__ void load(uint32_t p, double (&x)[CB]) const {
+#pragma unroll
+        for (int c = 0; c < CB; c++) x[c] = PV_LDS ? lds[p * CB + c] : gbl[(size_t)p * CB + c];
+    }
+};
+template <int CB, bool PV_LDS>
+__device__ __forceinline__ ParentVals<CB, PV_LDS> parent_vals(const DD &d, const BatchView &bv, int k) {
+    ParentVals<CB, PV_LDS> pv;
+    pv.lds = bv.vb + (size_t)(k & 1) * kLdsBatchWidth * CB;
+    pv.gbl = PV_LDS ? nullptr : bv.s2b + (size_t)(uni(d.noff[k]) - bv.gbase) * CB;
+    return pv;
+}
+
+// Wide layers (k >= kg) stream through HBM: one node per lane per item, U items per lane
+// per step, the CB cut values of a node in registers.  Software pipeline: the topology
+// words of step s + 1 are in flight while step s loads its parent values, and the parent
+// values of step s + 1 while step s computes (loads issued back to back, fenced).
 template <int CB>
-__device__ __forceinline__ void sweep_tail_layer(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int k, int nb, int kS) {
-    constexpr int G = kWave / CB;
-    constexpr int U = 8;
+struct WideTopo {
+    static constexpr int U = CB >= 8 ? 1 : 16 / CB;
+    uint32_t t[U], f[U];
+};
+
+template <int CB, bool PV_LDS>
+__device__ __forceinline__ void sweep_tail_layer_t(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int k, int nb,
+                                                   int kS) {
+    constexpr int U = WideTopo<CB>::U;
+    constexpr uint32_t STEP = (uint32_t)U * kWave;
     batch_coef_direct(net, d, bv, pool, k, nb);
-    const int c = lane() % CB, grp = lane() / CB;
-    const bool cv = c < nb;
     const int us = pool.ustride;
     const uint32_t noff = uni(d.noff[k]), n = uni(d.nn[k]);
     // state2 of tail layers is read only by the exact redo (kS = T); see sweep_narrow
     const bool w1 = uni(bv.w1[k]) != 0, wr = kS >= d.T;
-    for (uint32_t base = 0; base < n; base += G * U) {
-        uint32_t t[U];
-        uint8_t f[U];
+    const ParentVals<CB, PV_LDS> pv = parent_vals<CB, PV_LDS>(d, bv, k - 1);
+    GBL double *out = bv.s2b + (size_t)(noff - bv.gbase) * CB;
+    auto load_topo = [&](uint32_t base, WideTopo<CB> &tp) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            uint32_t i = base + u * G + grp;
-            bool ok = i < n && cv;
-            t[u] = ok ? d.ntopo[noff + i] : 0u;
-            f[u] = ok ? d.nflag[noff + i] : (uint8_t)0;
+            const uint32_t i = base + (uint32_t)u * kWave + lane();
+            const uint32_t ic = i < n ? i : 0u;
+            tp.t[u] = d.ntopo[noff + ic];
+            tp.f[u] = i < n ? (uint32_t)d.nflag[noff + ic] : 0u;
         }
-        double px[U];
+    };
+    auto load_px = [&](const WideTopo<CB> &tp, double (&px)[U][CB]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) pv.load((tp.f[u] & kAlive) ? (tp.t[u] & kParentMask) : 0u, px[u]);
+    };
+    WideTopo<CB> ta, tb;
+    double pxa[U][CB];
+    load_topo(0, ta);
+    load_px(ta, pxa);
+    load_topo(STEP, tb);
+    for (uint32_t base = 0; base < n; base += STEP) {
+        double pxb[U][CB];
+        load_px(tb, pxb);
+        WideTopo<CB> tn;
+        load_topo(base + 2 * STEP, tn);
+        double cf[U][CB];
 #pragma unroll
         for (int u = 0; u < U; u++)
-            px[u] = (f[u] & kAlive) ? batch_value<CB>(d, bv, k - 1, t[u] & kParentMask, c) : 0.0;
+#pragma unroll
+            for (int c = 0; c < CB; c++) cf[u][c] = bv.coef[c * us + (ta.t[u] >> kRankShift)];
+        sched_fence();
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            if (!(f[u] & kAlive)) continue;
-            uint32_t i = base + u * G + grp;
-            uint32_t node = noff + i, r = t[u] >> kRankShift;
-            double x, y = DMAX;
-            if (!(f[u] & kInAlive)) x = DMIN;
-            else if (r != 0) { x = px[u] + bv.coef[c * us + r]; y = x; }
-            else { x = px[u]; y = px[u] + 0.0; }
-            bv.s2b[(size_t)(node - bv.gbase) * CB + c] = x;
-            if (wr && c == nb - 1) d.s2[node] = x;
+            const uint32_t i = base + (uint32_t)u * kWave + lane();
+            if (!(ta.f[u] & kAlive)) continue;
+            const uint32_t r = ta.t[u] >> kRankShift;
+            const bool inal = (ta.f[u] & kInAlive) != 0;
+            double x[CB];
+#pragma unroll
+            for (int c = 0; c < CB; c++) {
+                x[c] = !inal ? DMIN : (r != 0 ? pxa[u][c] + cf[u][c] : pxa[u][c]);
+                out[(size_t)i * CB + c] = x[c];
+            }
+            if (wr) {
+                double v = x[0];
+#pragma unroll
+                for (int c = 1; c < CB; c++) v = (c == nb - 1) ? x[c] : v;
+                d.s2[noff + i] = v;
+            }
             if (w1) {
-                bv.sm[(size_t)k * CB + c] = x;
-                bv.xm[(size_t)k * CB + c] = y;
+#pragma unroll
+                for (int c = 0; c < CB; c++) {
+                    if (c < nb) {
+                        bv.sm[(size_t)k * CB + c] = x[c];
+                        bv.xm[(size_t)k * CB + c] = !inal ? DMAX : (r != 0 ? x[c] : pxa[u][c] + 0.0);
+                    }
+                }
             }
         }
+        ta = tb;
+        tb = tn;
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int c = 0; c < CB; c++) pxa[u][c] = pxb[u][c];
     }
     wave_mem_sync();
+}
+
+template <int CB>
+__device__ __forceinline__ void sweep_tail_layer(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int k, int nb,
+                                                 int kS) {
+    if (k - 1 < d.kg) sweep_tail_layer_t<CB, true>(net, d, bv, pool, k, nb, kS);
+    else sweep_tail_layer_t<CB, false>(net, d, bv, pool, k, nb, kS);
 }
 
 // Pruning test of one cut from the batch summaries over layers [first, end): true =
@@ -1167,78 +1235,139 @@ __device__ __forceinline__ bool dd_prune_check(const DD &d, const BatchView &bv,
 // Pass A: per cut the terminal state after the running-min update and maxState; it
 // commits the terminal weights of all nb cuts (the common case) and keeps the previous
 // weights in `keep`.  Pass B, only when the replay stops inside the batch: the weights of
-// cuts 0 .. capply from the kept ones.  Leaves are processed U per lane per step with the
-// next step's topology loads in flight while the current step computes.
-template <int CB, bool PASS_A>
-__device__ __forceinline__ void fused_leaf(const DD &d, BatchView &bv, const Pool &pool, int ncut, GBL double *keep,
-                                           VP *term, VP *mxs) {
-    constexpr int U = CB >= 8 ? 1 : 16 / CB;
+// cuts 0 .. capply from the kept ones.  Streaming as in sweep_tail_layer_t.  The maxima
+// are plain maxima; the (value, priority) pick of the reference's ordered folds differs
+// from them only when a maximum is a zero, and then fused_leaf_pick recomputes that cut's
+// pick exactly.
+template <int CB, bool PV_LDS>
+__device__ __forceinline__ void fused_leaf_pick(const DD &d, const BatchView &bv, const Pool &pool, int ncut, const GBL double *keep,
+                                             int cc, VP &term, VP &mxs) {
     const int last = d.T - 1;
     const uint32_t lo = uni(d.noff[last]), ln = uni(d.nn[last]);
     const int us = pool.ustride;
-    if (PASS_A) {
-#pragma unroll
-        for (int c = 0; c < CB; c++) { term[c] = VP{0.0, INT_MIN}; mxs[c] = VP{0.0, INT_MIN}; }
+    const ParentVals<CB, PV_LDS> pv = parent_vals<CB, PV_LDS>(d, bv, last - 1);
+    term = VP{0.0, INT_MIN};
+    mxs = VP{0.0, INT_MIN};
+    for (uint32_t i = lane(); i < ln; i += kWave) {
+        const uint32_t f = d.nflag[lo + i];
+        if (!(f & kAlive)) continue;
+        const uint32_t t = d.ntopo[lo + i], r = t >> kRankShift;
+        const bool inal = (f & kInAlive) != 0;
+        double px[CB];
+        pv.load(t & kParentMask, px);
+        double ww = keep[(size_t)i * CB], v = 0.0;
+        for (int c = 0; c <= cc; c++) {
+            v = !inal ? DMIN : (r != 0 ? px[c] + bv.coef[c * us + r] : px[c]);
+            const double nw = smin(ww, v);
+            if (c < ncut) ww = nw;
+        }
+        term = vp_pick(term, VP{ww, prio_old((int)i)});
+        mxs = vp_pick(mxs, VP{v, prio_old((int)i)});
     }
-    uint32_t t[U], f[U];
-    double w[U];
-    auto load_topo = [&](uint32_t base) {
+    term = wave_vp(term);
+    mxs = wave_vp(mxs);
+}
+
+template <int CB, bool PASS_A, bool PV_LDS>
+__device__ __forceinline__ void fused_leaf_t(const DD &d, BatchView &bv, const Pool &pool, int ncut, GBL double *keep,
+                                             VP *term, VP *mxs) {
+    constexpr int U = WideTopo<CB>::U;
+    constexpr uint32_t STEP = (uint32_t)U * kWave;
+    const int last = d.T - 1;
+    const uint32_t lo = uni(d.noff[last]), ln = uni(d.nn[last]);
+    const int us = pool.ustride;
+    const ParentVals<CB, PV_LDS> pv = parent_vals<CB, PV_LDS>(d, bv, last - 1);
+    double tmx[CB], vmx[CB];
+#pragma unroll
+    for (int c = 0; c < CB; c++) { tmx[c] = -INFINITY; vmx[c] = -INFINITY; }
+    auto load_topo = [&](uint32_t base, WideTopo<CB> &tp) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t i = base + u * kWave + lane();
+            const uint32_t i = base + (uint32_t)u * kWave + lane();
             const uint32_t ic = i < ln ? i : 0u;
-            t[u] = d.ntopo[lo + ic];
-            f[u] = i < ln ? (uint32_t)d.nflag[lo + ic] : 0u;
+            tp.t[u] = d.ntopo[lo + ic];
+            tp.f[u] = i < ln ? (uint32_t)d.nflag[lo + ic] : 0u;
+        }
+    };
+    // parent values and the previous terminal weights of one step
+    auto load_px = [&](uint32_t base, const WideTopo<CB> &tp, double (&px)[U][CB], double (&w)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t i = base + (uint32_t)u * kWave + lane();
+            const uint32_t ic = i < ln ? i : 0u;
+            pv.load((tp.f[u] & kAlive) ? (tp.t[u] & kParentMask) : 0u, px[u]);
             w[u] = PASS_A ? d.tw[lo + ic] : keep[(size_t)ic * CB];
         }
     };
-    load_topo(0);
-    for (uint32_t base = 0; base < ln; base += U * kWave) {
-        // parent values of all leaves and cuts of this step, issued together
-        double px[U][CB];
+    WideTopo<CB> ta, tb;
+    double pxa[U][CB], wa[U];
+    load_topo(0, ta);
+    load_px(0, ta, pxa, wa);
+    load_topo(STEP, tb);
+    for (uint32_t base = 0; base < ln; base += STEP) {
+        double pxb[U][CB], wb[U];
+        load_px(base + STEP, tb, pxb, wb);
+        WideTopo<CB> tn;
+        load_topo(base + 2 * STEP, tn);
+        double cf[U][CB];
 #pragma unroll
         for (int u = 0; u < U; u++)
 #pragma unroll
-            for (int c = 0; c < CB; c++)
-                px[u][c] = batch_value<CB>(d, bv, last - 1, (f[u] & kAlive) ? (t[u] & kParentMask) : 0u, c);
-        uint32_t tc[U], fc[U];
-        double wc[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) { tc[u] = t[u]; fc[u] = f[u]; wc[u] = w[u]; }
-        if (base + U * kWave < ln) load_topo(base + U * kWave);
+            for (int c = 0; c < CB; c++) cf[u][c] = bv.coef[c * us + (ta.t[u] >> kRankShift)];
+        sched_fence();
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t i = base + u * kWave + lane();
-            const bool alive = (fc[u] & kAlive) != 0;
-            const uint32_t r = tc[u] >> kRankShift;
-            const bool inal = (fc[u] & kInAlive) != 0;
-            double ww = wc[u];
+            const uint32_t i = base + (uint32_t)u * kWave + lane();
+            const bool alive = (ta.f[u] & kAlive) != 0;
+            const uint32_t r = ta.t[u] >> kRankShift;
+            const bool inal = (ta.f[u] & kInAlive) != 0;
+            double ww = wa[u];
 #pragma unroll
             for (int c = 0; c < CB; c++) {
-                const double cf = bv.coef[c * us + r];
-                const double v = !inal ? DMIN : ((r != 0) ? px[u][c] + cf : px[u][c]);
+                const double v = !inal ? DMIN : ((r != 0) ? pxa[u][c] + cf[u][c] : pxa[u][c]);
                 const double nw = smin(ww, v);
                 if (c < ncut) ww = nw;
                 if (PASS_A) {
                     const bool use = alive & (c < ncut);
-                    term[c] = vp_pick(term[c], VP{ww, use ? prio_old((int)i) : INT_MIN});
-                    mxs[c] = vp_pick(mxs[c], VP{v, use ? prio_old((int)i) : INT_MIN});
+                    tmx[c] = (use && ww > tmx[c]) ? ww : tmx[c];
+                    vmx[c] = (use && v > vmx[c]) ? v : vmx[c];
                 }
             }
             if (alive) {
-                if (PASS_A) keep[(size_t)i * CB] = wc[u];
+                if (PASS_A) keep[(size_t)i * CB] = wa[u];
                 d.tw[lo + i] = ww;
             }
         }
-    }
-    if (PASS_A) {
+        ta = tb;
+        tb = tn;
 #pragma unroll
-        for (int c = 0; c < CB; c++) {
-            term[c] = wave_vp(term[c]);
-            mxs[c] = wave_vp(mxs[c]);
+        for (int u = 0; u < U; u++) {
+            wa[u] = wb[u];
+#pragma unroll
+            for (int c = 0; c < CB; c++) pxa[u][c] = pxb[u][c];
         }
     }
     wave_mem_sync();
+    if (PASS_A) {
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            tmx[c] = lane_reduce<1>(tmx[c], [](double a, double b) { return (b > a) ? b : a; });
+            vmx[c] = lane_reduce<1>(vmx[c], [](double a, double b) { return (b > a) ? b : a; });
+            term[c] = VP{tmx[c], tmx[c] != -INFINITY ? 0 : INT_MIN};
+            mxs[c] = VP{vmx[c], vmx[c] != -INFINITY ? 0 : INT_MIN};
+        }
+#pragma unroll
+        for (int c = 0; c < CB; c++)
+            if (c < ncut && (tmx[c] == 0.0 || vmx[c] == 0.0))
+                fused_leaf_pick<CB, PV_LDS>(d, bv, pool, ncut, keep, c, term[c], mxs[c]);
+    }
+}
+
+template <int CB, bool PASS_A>
+__device__ __forceinline__ void fused_leaf(const DD &d, BatchView &bv, const Pool &pool, int ncut, GBL double *keep,
+                                           VP *term, VP *mxs) {
+    if (d.T - 2 < d.kg) fused_leaf_t<CB, PASS_A, true>(d, bv, pool, ncut, keep, term, mxs);
+    else fused_leaf_t<CB, PASS_A, false>(d, bv, pool, ncut, keep, term, mxs);
 }
 
 // getPathForNode (DD.cpp:3796-3820): walk up, first in-arc whose parent.state2 + weight
