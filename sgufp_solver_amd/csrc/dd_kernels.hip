@@ -1220,15 +1220,50 @@ __device__ __forceinline__ void sweep_tail_layer(const NetDev &net, DD &d, Batch
     else sweep_tail_layer_t<CB, false>(net, d, bv, pool, k, nb, kS);
 }
 
-// Pruning test of one cut from the batch summaries over layers [first, end): true =
-// redo this cut exactly (some arc is pruned, or a width-1 layer has no summary because
-// deletions made it width-1 inside the batch).
+// Pruning test of the batch cuts c0 .. c1-1 from the batch summaries over layers
+// [first, end): bit c set = redo cut c exactly (some arc is pruned, or a width-1 layer
+// has no summary because deletions made it width-1 inside the batch).  The summary loads
+// of two 64-layer windows are issued together, independent of the layer flags.
+template <int CB>
+__device__ __forceinline__ uint32_t dd_prune_mask(const DD &d, const BatchView &bv, int c0, int c1, int first, int end,
+                                                  double thresh, const double (&maxState)[CB]) {
+    constexpr int W = 2;
+    uint32_t mask = 0;
+    for (int base = first; base < end; base += W * kWave) {
+        bool need[W], val[W];
+        double sm[W][CB], xm[W][CB];
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+            const int k = base + w * kWave + lane();
+            const int kk = k < end ? k : first;
+            need[w] = k < end && d.nalive[kk] == 1;
+            val[w] = bv.w1[kk] != 0;
+#pragma unroll
+            for (int c = 0; c < CB; c++) {
+                sm[w][c] = bv.sm[(size_t)kk * CB + c];
+                xm[w][c] = bv.xm[(size_t)kk * CB + c];
+            }
+        }
+        sched_fence();
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            if (c < c0 || c >= c1) continue;
+            bool fire = false;
+#pragma unroll
+            for (int w = 0; w < W; w++) fire |= need[w] && (!val[w] || (xm[w][c] + (maxState[c] - sm[w][c])) <= thresh);
+            if (__ballot(fire)) mask |= 1u << c;
+        }
+    }
+    return mask;
+}
+
 template <int CB>
 __device__ __forceinline__ bool dd_prune_check(const DD &d, const BatchView &bv, int c, int first, int end, double thresh,
                                double maxState) {
-    for (int base = first; base < end; base += kWave)
-        if (prune_fire(d, base, end, maxState, thresh, bv.sm + c, bv.xm + c, CB, bv.w1)) return true;
-    return false;
+    double ms[CB];
+#pragma unroll
+    for (int cc = 0; cc < CB; cc++) ms[cc] = maxState;
+    return dd_prune_mask<CB>(d, bv, c, c + 1, first, end, thresh, ms) != 0;
 }
 
 // Fused last layer of an optimality batch (leaf value = parent value + coefficient).
@@ -1483,20 +1518,34 @@ __device__ __forceinline__ int dd_solution_path(const NetDev &net, DD &d, const 
 // (NodeExplorer.cpp:935-944 / 975-983).
 __device__ __forceinline__ int seq_id(const Pool &pool, int s) { return s < pool.nf ? pool.f_order[s] : pool.o_order[s - pool.nf]; }
 
-// root fold (DD.cpp:3938-3949) of the cuts at pool positions s0 + lane
-__device__ __forceinline__ double root_fold_seq(const Pool &pool, const DD &d, int s0, int total) {
-    int s = s0 + lane();
-    double v = 0.0;
-    if (s < total) {
-        int id = seq_id(pool, s);
-        const GBL double *row = pool.rows + (size_t)id * pool.stride;
-        v = pool.rhs[id];
-        for (int t = 0; t < d.len; t++) {
-            int sl = d.rslot[t];
-            if (sl >= 0) v = v + row[sl];
+// Root prefix (DD.cpp:3938-3949): v = RHS, then v = v + coef for each decision of the
+// record's solution vector in order, skipping -1.  The fold is sequential; its loads are
+// independent, so they are issued kFoldBatch at a time ahead of the adds.
+constexpr int kFoldBatch = 16;
+__device__ __forceinline__ double root_fold(const GBL double *row, double v, const DD &d) {
+    for (int t0 = 0; t0 < d.len; t0 += kFoldBatch) {
+        double x[kFoldBatch];
+        bool ok[kFoldBatch];
+#pragma unroll
+        for (int j = 0; j < kFoldBatch; j++) {
+            const int t = t0 + j;
+            const int sl = t < d.len ? (int)d.rslot[t] : -1;
+            ok[j] = sl >= 0;
+            x[j] = row[ok[j] ? sl : 0];
         }
+        sched_fence();
+#pragma unroll
+        for (int j = 0; j < kFoldBatch; j++)
+            if (ok[j]) v = v + x[j];
     }
     return v;
+}
+
+// root fold of the cuts at pool positions s0 + lane (lanes past the pool fold the last)
+__device__ __forceinline__ double root_fold_seq(const Pool &pool, const DD &d, int s0, int total) {
+    const int s = min(s0 + lane(), total - 1);
+    const int id = seq_id(pool, s);
+    return root_fold(pool.rows + (size_t)id * pool.stride, pool.rhs[id], d);
 }
 
 struct LoopState {
@@ -1625,13 +1674,7 @@ __device__ __forceinline__ double screen_leaf(const DD &d, BatchView &bv, const 
 
 // root fold (DD.cpp:3938-3949) of pool row `id` (lane-uniform or per lane)
 __device__ __forceinline__ double root_fold_row(const Pool &pool, const DD &d, int id) {
-    const GBL double *row = pool.rows + (size_t)id * pool.stride;
-    double v = pool.rhs[id];
-    for (int t = 0; t < d.len; t++) {
-        int sl = d.rslot[t];
-        if (sl >= 0) v = v + row[sl];
-    }
-    return v;
+    return root_fold(pool.rows + (size_t)id * pool.stride, pool.rhs[id], d);
 }
 
 // true: the screen proves the optimality prune
@@ -1645,7 +1688,7 @@ __device__ __forceinline__ bool screen_opt(const NetDev &net, DD &d, BatchView &
         const int nb = min(CB, n - sp);
         if (lane() < nb) bv.ids[lane()] = pool.o_rank[sp + lane()];
         for (int k = lane(); k < d.T; k += kWave) bv.w1[k] = ((d.nalive[k]) == 1) ? 1 : 0;
-        const double rv = (lane() < nb) ? root_fold_row(pool, d, pool.o_rank[sp + lane()]) : 0.0;
+        const double rv = root_fold_row(pool, d, pool.o_rank[sp + min(lane(), nb - 1)]);
         wave_lds_sync();
         sweep_narrow<CB>(net, d, bv, pool, nb, rv, 0);
         if (d.kg == 0 && lane() < nb) bv.s2b[lane()] = rv;
@@ -1728,17 +1771,21 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
             GBL double *keep = bv.s2b + (size_t)(uni(d.noff[last]) - bv.gbase) * CB;  // free in O batches
             fused_leaf<CB, true>(d, bv, pool, nb, keep, term, mxs);
             st.stamp(3);
-            // replay in pool order (unrolled: term / mxs stay in registers)
+            // replay in pool order (unrolled: term / mxs stay in registers); the width-1
+            // pruning tests of all batch cuts in one pass (no edit happens before a redo)
             int capply = nb - 1, redo = -1;
             bool stop = false, pruned = false;
             double redo_v = DMIN, redo_ms = DMIN;
+            double mstate[CB];
+#pragma unroll
+            for (int c = 0; c < CB; c++) mstate[c] = (mxs[c].p == INT_MIN) ? DMIN : smax(DMIN, mxs[c].v);
+            const uint32_t fire = d.exact ? 0u : dd_prune_mask<CB>(d, bv, 0, nb, 3, last - 1, incumbent - 0.01, mstate);
 #pragma unroll
             for (int c = 0; c < CB; c++) {
                 if (stop || c >= nb) continue;
                 double v = (term[c].p == INT_MIN) ? DMIN : smax(DMIN, term[c].v);
-                double maxState = (mxs[c].p == INT_MIN) ? DMIN : smax(DMIN, mxs[c].v);
-                if (v > incumbent && !d.exact &&
-                    dd_prune_check<CB>(d, bv, c, 3, last - 1, incumbent - 0.01, maxState)) {
+                double maxState = mstate[c];
+                if (v > incumbent && !d.exact && ((fire >> c) & 1u)) {
                     capply = c;
                     redo = c;
                     redo_v = v;
@@ -2018,15 +2065,7 @@ __global__ void __launch_bounds__(kWave) k_refine(NetDev net, Scratch sc, BatchI
     wave_lds_sync();
     const int id = cut_ids[w];
     const GBL double *row = pool.rows + (size_t)id * pool.stride;
-    double rv = 0.0;
-    if (lane() == 0) {
-        rv = pool.rhs[id];
-        for (int t = 0; t < d.len; t++) {
-            int s = d.rslot[t];
-            if (s >= 0) rv = rv + row[s];
-        }
-    }
-    rv = lane_get(rv, 0);
+    const double rv = root_fold(row, pool.rhs[id], d);
     dd_sweep(net, d, row, rv);
     int status = kNeedsSubproblem;
     double ub = sc.ubv[slot];
