@@ -229,15 +229,21 @@ __device__ __forceinline__ void load_layer_coef(const NetDev &net, const DD &d, 
 
 // ------------------------------------------------------------------------------------
 // Build (buildTree + buildNextLayer).  Returns false on capacity overflow.
+// The state masks of a layer of at most kBuildLds nodes are also kept in LDS (the value
+// buffers, unused during the build), so that the next layer reads them without an HBM
+// round trip and the layer step waits for no store; wider layers go through HBM.
+constexpr uint32_t kBuildLds = (uint32_t)kLdsWidth * 2;   // u32 masks per parity half of buf0/buf1
 __device__ __forceinline__ bool dd_build(const NetDev &net, DD &d, const Scratch &sc, uint32_t root_mask, uint32_t &n_nodes,
                          uint32_t &n_arcs, uint32_t &n_merged) {
     const int L = net.L;
+    LDS uint32_t *mb = (LDS uint32_t *)d.buf0;     // [2][kBuildLds]
     if (lane() == 0) {
         d.ntopo[0] = kNoRank << kRankShift;
         d.nflag[0] = kAlive | kInAlive;
         d.nmask[0] = root_mask;
         d.s2[0] = DMIN;
         d.noff[0] = 0; d.nn[0] = 1; d.nalive[0] = 1; d.aoff[0] = 0; d.acnt[0] = 0;
+        mb[0] = root_mask;
     }
     wave_mem_sync();
     uint32_t total_nodes = 1, total_arcs = 0, merged_nodes = 0;
@@ -245,17 +251,24 @@ __device__ __forceinline__ bool dd_build(const NetDev &net, DD &d, const Scratch
     int idx = 0;
     int exact = 1;
     bool ok = true;
+    bool in_lds = true;                            // masks of the current layer in mb[idx & 1]
     for (int a = d.g; a < L; a++, idx++) {
         if (idx + 2 > sc.Tcap) { ok = false; break; }
         const uint32_t cnoff = uni(d.noff[idx]), cn = uni(d.nn[idx]);
+        LDS uint32_t *cm = mb + (size_t)(idx & 1) * kBuildLds;        // current layer (LDS copy)
+        LDS uint32_t *nm = mb + (size_t)((idx + 1) & 1) * kBuildLds;  // next layer (LDS copy)
         const int upd = net.layer_update[a];
+        uint32_t full = 0;
         if (upd >= 0) {  // stateUpdateMap.contains(a): every current-layer node takes the full set
             const int sl = net.set_len[upd];
-            const uint32_t full = (sl >= 32) ? 0xFFFFFFFFu : ((1u << sl) - 1u);
+            full = (sl >= 32) ? 0xFFFFFFFFu : ((1u << sl) - 1u);
             for (uint32_t i = lane(); i < cn; i += kWave) d.nmask[cnoff + i] = full;
             next_size = cn * (uint32_t)sl;
-            wave_mem_sync();
         }
+        auto mask_of = [&](uint32_t i) -> uint32_t {
+            if (upd >= 0) return full;
+            return in_lds ? cm[i] : d.nmask[cnoff + i];
+        };
         if (next_size >= kCollapseWidth && (unsigned)(d.g + idx) < net.L5) {
             // collapse into one node; one arc per (parent, state) in order
             exact = 0;
@@ -264,7 +277,7 @@ __device__ __forceinline__ bool dd_build(const NetDev &net, DD &d, const Scratch
             for (uint32_t base = 0; base < cn; base += kWave) {
                 uint32_t i = base + lane();
                 bool valid = i < cn;
-                uint32_t m = valid ? d.nmask[cnoff + i] : 0u;
+                uint32_t m = valid ? mask_of(i) : 0u;
                 uint32_t c = __popc(m);
                 uint32_t incl = wave_scan_incl(c);
                 uint32_t off = base_arc + carry + incl - c;
@@ -291,11 +304,13 @@ __device__ __forceinline__ bool dd_build(const NetDev &net, DD &d, const Scratch
                 d.s2[mnode] = DMIN;
                 d.noff[idx + 1] = mnode; d.nn[idx + 1] = 1; d.nalive[idx + 1] = 1;
                 d.aoff[idx + 1] = base_arc; d.acnt[idx + 1] = carry;
+                nm[0] = uni;
             }
             total_nodes += 1;
             merged_nodes += 1;
             total_arcs += carry;
             next_size = __popc(uni);
+            in_lds = true;
         } else {
             // exact expansion: one child per (parent, state), child states = parent minus decision
             const uint32_t first = total_nodes;
@@ -303,7 +318,7 @@ __device__ __forceinline__ bool dd_build(const NetDev &net, DD &d, const Scratch
             for (uint32_t base = 0; base < cn; base += kWave) {
                 uint32_t i = base + lane();
                 bool valid = i < cn;
-                uint32_t m = valid ? d.nmask[cnoff + i] : 0u;
+                uint32_t m = valid ? mask_of(i) : 0u;
                 uint32_t c = __popc(m);
                 uint32_t incl = wave_scan_incl(c);
                 uint32_t off = first + carry + incl - c;
@@ -314,11 +329,13 @@ __device__ __forceinline__ bool dd_build(const NetDev &net, DD &d, const Scratch
                     while (mm) {
                         uint32_t r = __ffs(mm) - 1;
                         mm &= mm - 1;
-                        uint32_t ch = off + t;
+                        const uint32_t ch = off + t;
+                        const uint32_t cmask = (r == 0) ? m : (m & ~(1u << r));
                         d.ntopo[ch] = i | (r << kRankShift);
                         d.nflag[ch] = kAlive | kInAlive;
-                        d.nmask[ch] = (r == 0) ? m : (m & ~(1u << r));
+                        d.nmask[ch] = cmask;
                         d.s2[ch] = DMIN;
+                        if (ch - first < kBuildLds) nm[ch - first] = cmask;
                         t++;
                     }
                     d.outcnt[cnoff + i] = c;
@@ -333,8 +350,11 @@ __device__ __forceinline__ bool dd_build(const NetDev &net, DD &d, const Scratch
             }
             total_nodes += carry;
             next_size = ns;
+            in_lds = carry <= kBuildLds;
         }
-        wave_mem_sync();
+        // the next layer reads its masks from LDS, or from HBM after the stores completed
+        if (in_lds) wave_lds_sync();
+        else wave_mem_sync();
     }
     if (!ok) return false;
     d.T = idx + 1;
@@ -542,6 +562,87 @@ struct LastVals {
     __device__ __forceinline__ double operator()(uint32_t i) const { return p[(size_t)i * stride]; }
 };
 
+// Bottom-up deletion cascade (removeNode / bottomUpDelete / updateTree,
+// DD.cpp:4040-4153): last-layer nodes marked for removal die, and a parent dies when its
+// last alive out-arc dies in this batch.  code = 0: the last layer's marks are kKill;
+// code > 0: they are the feasibility scan's first-removing-cut codes (nflag bits 3..7 ==
+// code, see f_leaf_scan_t).  Node flags of a layer are read U per lane at a time and the
+// parents' out-degree decrements issued together.
+__device__ __forceinline__ void dd_cascade(DD &d, uint32_t code) {
+    constexpr int U = 4;
+    const int last = d.T - 1;
+    for (int k = last; k >= 1; k--) {
+        const uint32_t noff = uni(d.noff[k]), n = uni(d.nn[k]), pnoff = uni(d.noff[k - 1]);
+        const uint32_t acnt = uni(d.acnt[k]);
+        uint32_t killed = 0, parent_killed = 0;
+        if (acnt) {
+            const uint32_t M = noff;
+            if (d.nflag[M] & kKill) {
+                killed = 1;
+                const uint32_t aoff = uni(d.aoff[k]);
+                for (uint32_t base = 0; base < acnt; base += kWave) {
+                    uint32_t a = base + lane();
+                    bool pk = false;
+                    if (a < acnt && (d.aflag[aoff + a] & kAlive)) {
+                        uint32_t p = d.atopo[aoff + a] & kParentMask;
+                        d.aflag[aoff + a] = 0;
+                        mir_arc_clear(d, aoff + a);
+                        if (gsub(&d.outcnt[pnoff + p], 1u) == 1u) {
+                            d.nflag[pnoff + p] |= kKill;
+                            pk = true;
+                        }
+                    }
+                    parent_killed += (uint32_t)__popcll(__ballot(pk));
+                }
+                wave_mem_sync();
+                if (lane() == 0) {
+                    d.nflag[M] = 0;
+                    mir_node_clear(d, M, kMirAlive | kMirIn);
+                }
+            }
+        } else {
+            const bool by_code = code != 0 && k == last;
+            for (uint32_t base = 0; base < n; base += U * kWave) {
+                uint32_t f[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const uint32_t i = base + (uint32_t)u * kWave + lane();
+                    f[u] = i < n ? (uint32_t)d.nflag[noff + i] : 0u;
+                }
+                sched_fence();
+                bool kk[U];
+                uint32_t p[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const uint32_t i = base + (uint32_t)u * kWave + lane();
+                    kk[u] = by_code ? ((f[u] & kAlive) != 0 && (f[u] >> 3) == code) : (f[u] & kKill) != 0;
+                    p[u] = (kk[u] && (f[u] & kInAlive)) ? (d.ntopo[noff + (i < n ? i : 0u)] & kParentMask) : 0u;
+                }
+                uint32_t old[U];
+#pragma unroll
+                for (int u = 0; u < U; u++)
+                    old[u] = (kk[u] && (f[u] & kInAlive)) ? gsub(&d.outcnt[pnoff + p[u]], 1u) : 0u;
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const uint32_t i = base + (uint32_t)u * kWave + lane();
+                    if (kk[u]) {
+                        d.nflag[noff + i] = 0;
+                        mir_node_clear(d, noff + i, kMirAlive | kMirIn);
+                    }
+                    // exactly one decrement sees 1: that lane marks the parent
+                    const bool pk = old[u] == 1u;
+                    if (pk) d.nflag[pnoff + p[u]] |= kKill;
+                    killed += (uint32_t)__popcll(__ballot(kk[u]));
+                    parent_killed += (uint32_t)__popcll(__ballot(pk));
+                }
+            }
+        }
+        if (lane() == 0) d.nalive[k] -= killed;
+        wave_mem_sync();
+        if (!parent_killed) break;
+    }
+}
+
 // Last-layer removal (state2 < -0.01, DD.cpp:3880-3893) and the bottom-up deletion
 // cascade (removeNode / bottomUpDelete / updateTree, DD.cpp:4040-4153).  Returns false
 // when every alive last-layer node would go (the reference returns false there).
@@ -581,64 +682,7 @@ __device__ __forceinline__ bool dd_remove_last(DD &d, const LastVals &lv, double
     if (rm == uni(d.nalive[last])) return false;
     if (rm) {
         wave_mem_sync();
-        // a parent dies when its last alive out-arc dies in this batch
-        for (int k = last; k >= 1; k--) {
-            const uint32_t noff = uni(d.noff[k]), n = uni(d.nn[k]), pnoff = uni(d.noff[k - 1]);
-            const uint32_t acnt = uni(d.acnt[k]);
-            uint32_t killed = 0, parent_killed = 0;
-            if (acnt) {
-                const uint32_t M = noff;
-                if (d.nflag[M] & kKill) {
-                    killed = 1;
-                    const uint32_t aoff = uni(d.aoff[k]);
-                    for (uint32_t base = 0; base < acnt; base += kWave) {
-                        uint32_t a = base + lane();
-                        bool pk = false;
-                        if (a < acnt && (d.aflag[aoff + a] & kAlive)) {
-                            uint32_t p = d.atopo[aoff + a] & kParentMask;
-                            d.aflag[aoff + a] = 0;
-                            mir_arc_clear(d, aoff + a);
-                            if (gsub(&d.outcnt[pnoff + p], 1u) == 1u) {
-                                d.nflag[pnoff + p] |= kKill;
-                                pk = true;
-                            }
-                        }
-                        parent_killed += wave_sum(pk ? 1u : 0u);
-                    }
-                    wave_mem_sync();
-                    if (lane() == 0) {
-                        d.nflag[M] = 0;
-                        mir_node_clear(d, M, kMirAlive | kMirIn);
-                    }
-                }
-            } else {
-                for (uint32_t base = 0; base < n; base += kWave) {
-                    uint32_t i = base + lane();
-                    bool kk = false, pk = false;
-                    if (i < n) {
-                        uint8_t f = d.nflag[noff + i];
-                        if (f & kKill) {
-                            kk = true;
-                            if (f & kInAlive) {
-                                uint32_t p = d.ntopo[noff + i] & kParentMask;
-                                // exactly one decrement sees 1: that lane marks the parent
-                                if (gsub(&d.outcnt[pnoff + p], 1u) == 1u) {
-                                    d.nflag[pnoff + p] |= kKill;
-                                    pk = true;
-                                }
-                            }
-                            d.nflag[noff + i] = 0;
-                            mir_node_clear(d, noff + i, kMirAlive | kMirIn);
-                        }
-                    }
-                    killed += wave_sum(kk ? 1u : 0u);
-                    parent_killed += wave_sum(pk ? 1u : 0u);
-                }
-            }
-            if (lane() == 0) d.nalive[k] -= killed;
-            wave_mem_sync();
-            if (!parent_killed) break;
-        }
+        dd_cascade(d, 0u);
     }
     return true;
 }
@@ -1405,6 +1449,130 @@ __device__ __forceinline__ void fused_leaf(const DD &d, BatchView &bv, const Poo
     else fused_leaf_t<CB, PASS_A, false>(d, bv, pool, ncut, keep, term, mxs);
 }
 
+// Feasibility batch, last layer.  One streaming pass (as sweep_tail_layer_t) computes
+// every alive leaf's values for the nb batch cuts and the first batch cut that removes it
+// (state2 < -0.01, DD.cpp:3884-3889), stored as cut + 1 in nflag bits 3..7 (0: none);
+// per cut it counts the removals and takes maxState over the leaves that survive the cut.
+// Removing leaves never changes the values of the others, so the per-cut replay needs no
+// further leaf values: dd_cascade(d, c + 1) removes cut c's leaves.  maxState is a plain
+// maximum; for a zero maximum f_leaf_pick recomputes the reference's ordered pick.
+template <int CB, bool PV_LDS>
+__device__ __forceinline__ void f_leaf_pick(const DD &d, const BatchView &bv, const Pool &pool, int c, double &maxState) {
+    const int last = d.T - 1;
+    const uint32_t lo = uni(d.noff[last]), ln = uni(d.nn[last]);
+    const int us = pool.ustride;
+    const ParentVals<CB, PV_LDS> pv = parent_vals<CB, PV_LDS>(d, bv, last - 1);
+    VP mx{0.0, INT_MIN};
+    for (uint32_t i = lane(); i < ln; i += kWave) {
+        const uint32_t f = d.nflag[lo + i];
+        const uint32_t code = f >> 3;
+        if (!(f & kAlive) || (code != 0 && code <= (uint32_t)c + 1u)) continue;
+        const uint32_t t = d.ntopo[lo + i], r = t >> kRankShift;
+        double px[CB];
+        pv.load(t & kParentMask, px);
+        const double v = !(f & kInAlive) ? DMIN : (r != 0 ? px[c] + bv.coef[c * us + r] : px[c]);
+        mx = vp_pick(mx, VP{v, prio_old((int)i)});
+    }
+    mx = wave_vp(mx);
+    maxState = (mx.p == INT_MIN) ? DMIN : smax(DMIN, mx.v);
+}
+
+template <int CB, bool PV_LDS>
+__device__ __forceinline__ void f_leaf_scan_t(DD &d, BatchView &bv, const Pool &pool, int nb, int kS, uint32_t (&rm)[CB],
+                                              double (&maxState)[CB]) {
+    constexpr int U = WideTopo<CB>::U;
+    constexpr uint32_t STEP = (uint32_t)U * kWave;
+    const int last = d.T - 1;
+    const uint32_t lo = uni(d.noff[last]), ln = uni(d.nn[last]);
+    const int us = pool.ustride;
+    const bool wr = kS >= d.T;   // state2 of the last batch cut, as sweep_tail_layer_t
+    const ParentVals<CB, PV_LDS> pv = parent_vals<CB, PV_LDS>(d, bv, last - 1);
+    uint32_t cnt[CB];
+    double vmx[CB];
+#pragma unroll
+    for (int c = 0; c < CB; c++) { cnt[c] = 0; vmx[c] = -INFINITY; }
+    auto load_topo = [&](uint32_t base, WideTopo<CB> &tp) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t i = base + (uint32_t)u * kWave + lane();
+            const uint32_t ic = i < ln ? i : 0u;
+            tp.t[u] = d.ntopo[lo + ic];
+            tp.f[u] = i < ln ? (uint32_t)d.nflag[lo + ic] : 0u;
+        }
+    };
+    auto load_px = [&](const WideTopo<CB> &tp, double (&px)[U][CB]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) pv.load((tp.f[u] & kAlive) ? (tp.t[u] & kParentMask) : 0u, px[u]);
+    };
+    WideTopo<CB> ta, tb;
+    double pxa[U][CB];
+    load_topo(0, ta);
+    load_px(ta, pxa);
+    load_topo(STEP, tb);
+    for (uint32_t base = 0; base < ln; base += STEP) {
+        double pxb[U][CB];
+        load_px(tb, pxb);
+        WideTopo<CB> tn;
+        load_topo(base + 2 * STEP, tn);
+        double cf[U][CB];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int c = 0; c < CB; c++) cf[u][c] = bv.coef[c * us + (ta.t[u] >> kRankShift)];
+        sched_fence();
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t i = base + (uint32_t)u * kWave + lane();
+            const uint32_t f = ta.f[u];
+            if (!(f & kAlive)) continue;
+            const uint32_t r = ta.t[u] >> kRankShift;
+            const bool inal = (f & kInAlive) != 0;
+            double v[CB];
+            int kc = nb;
+#pragma unroll
+            for (int c = CB - 1; c >= 0; c--) {
+                v[c] = !inal ? DMIN : (r != 0 ? pxa[u][c] + cf[u][c] : pxa[u][c]);
+                if (c < nb && v[c] < -0.01) kc = c;
+            }
+#pragma unroll
+            for (int c = 0; c < CB; c++) {
+                cnt[c] += (kc == c) ? 1u : 0u;
+                vmx[c] = (kc > c && v[c] > vmx[c]) ? v[c] : vmx[c];
+            }
+            d.nflag[lo + i] = (uint8_t)((f & 7u) | (kc < nb ? (uint32_t)(kc + 1) << 3 : 0u));
+            if (wr) {
+                double w = v[0];
+#pragma unroll
+                for (int c = 1; c < CB; c++) w = (c == nb - 1) ? v[c] : w;
+                d.s2[lo + i] = w;
+            }
+        }
+        ta = tb;
+        tb = tn;
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int c = 0; c < CB; c++) pxa[u][c] = pxb[u][c];
+    }
+#pragma unroll
+    for (int c = 0; c < CB; c++) {
+        rm[c] = wave_sum(cnt[c]);
+        vmx[c] = lane_reduce<1>(vmx[c], [](double a, double b) { return (b > a) ? b : a; });
+        maxState[c] = (vmx[c] == -INFINITY) ? DMIN : smax(DMIN, vmx[c]);
+    }
+    wave_mem_sync();
+#pragma unroll
+    for (int c = 0; c < CB; c++)
+        if (c < nb && vmx[c] == 0.0) f_leaf_pick<CB, PV_LDS>(d, bv, pool, c, maxState[c]);
+}
+
+template <int CB>
+__device__ __forceinline__ void f_leaf_scan(DD &d, BatchView &bv, const Pool &pool, int nb, int kS, uint32_t (&rm)[CB],
+                                            double (&maxState)[CB]) {
+    if (d.T - 2 < d.kg) f_leaf_scan_t<CB, true>(d, bv, pool, nb, kS, rm, maxState);
+    else f_leaf_scan_t<CB, false>(d, bv, pool, nb, kS, rm, maxState);
+}
+
 // getPathForNode (DD.cpp:3796-3820): walk up, first in-arc whose parent.state2 + weight
 // equals this node's state2; if none matches, continue through the first in-arc
 // without recording a decision.  Decisions land in d.walk (bottom-up); returns count.
@@ -1633,43 +1801,88 @@ __device__ __forceinline__ bool redo_cut(const NetDev &net, DD &d, BatchView &bv
 // nothing happened (the screen writes no DD state the exact phase reads).
 
 // leaf values of the nb screening cuts: run[i] = min(run[i], v_c(i)); returns the max over
-// alive leaves of run (DMIN when none is alive)
-template <int CB>
-__device__ __forceinline__ double screen_leaf(const DD &d, BatchView &bv, const Pool &pool, int nb, bool first,
-                                              GBL double *run) {
+// alive leaves of run (DMIN when none is alive).  Streaming as in sweep_tail_layer_t.
+template <int CB, bool PV_LDS>
+__device__ __forceinline__ double screen_leaf_t(const DD &d, BatchView &bv, const Pool &pool, int nb, bool first,
+                                                GBL double *run) {
+    constexpr int U = WideTopo<CB>::U;
+    constexpr uint32_t STEP = (uint32_t)U * kWave;
     const int last = d.T - 1;
     const uint32_t lo = uni(d.noff[last]), ln = uni(d.nn[last]);
     const int us = pool.ustride;
+    const ParentVals<CB, PV_LDS> pv = parent_vals<CB, PV_LDS>(d, bv, last - 1);
     double best = -INFINITY;
-    bool any = false;
-    for (uint32_t base = 0; base < ln; base += kWave) {
-        const uint32_t i = base + lane();
-        const bool ok = i < ln;
-        const uint32_t ic = ok ? i : 0u;
-        const uint32_t t = d.ntopo[lo + ic];
-        const uint32_t f = ok ? (uint32_t)d.nflag[lo + ic] : 0u;
-        const bool alive = (f & kAlive) != 0, inal = (f & kInAlive) != 0;
-        const uint32_t r = t >> kRankShift, p = alive ? (t & kParentMask) : 0u;
-        double m = first ? DMAX : run[(size_t)ic * CB];
+    auto load_topo = [&](uint32_t base, WideTopo<CB> &tp) {
 #pragma unroll
-        for (int c = 0; c < CB; c++) {
-            if (c < nb) {
-                const double px = batch_value<CB>(d, bv, last - 1, p, c);
-                const double cf = bv.coef[c * us + r];
-                const double v = !inal ? DMIN : ((r != 0) ? px + cf : px);
-                m = fmin(m, v);
+        for (int u = 0; u < U; u++) {
+            const uint32_t i = base + (uint32_t)u * kWave + lane();
+            const uint32_t ic = i < ln ? i : 0u;
+            tp.t[u] = d.ntopo[lo + ic];
+            tp.f[u] = i < ln ? (uint32_t)d.nflag[lo + ic] : 0u;
+        }
+    };
+    auto load_px = [&](uint32_t base, const WideTopo<CB> &tp, double (&px)[U][CB], double (&m)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t i = base + (uint32_t)u * kWave + lane();
+            const uint32_t ic = i < ln ? i : 0u;
+            pv.load((tp.f[u] & kAlive) ? (tp.t[u] & kParentMask) : 0u, px[u]);
+            m[u] = first ? DMAX : run[(size_t)ic * CB];
+        }
+    };
+    WideTopo<CB> ta, tb;
+    double pxa[U][CB], ma[U];
+    load_topo(0, ta);
+    load_px(0, ta, pxa, ma);
+    load_topo(STEP, tb);
+    for (uint32_t base = 0; base < ln; base += STEP) {
+        double pxb[U][CB], mb[U];
+        load_px(base + STEP, tb, pxb, mb);
+        WideTopo<CB> tn;
+        load_topo(base + 2 * STEP, tn);
+        double cf[U][CB];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int c = 0; c < CB; c++) cf[u][c] = bv.coef[c * us + (ta.t[u] >> kRankShift)];
+        sched_fence();
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t i = base + (uint32_t)u * kWave + lane();
+            const bool alive = (ta.f[u] & kAlive) != 0, inal = (ta.f[u] & kInAlive) != 0;
+            const uint32_t r = ta.t[u] >> kRankShift;
+            double m = ma[u];
+#pragma unroll
+            for (int c = 0; c < CB; c++) {
+                if (c < nb) {
+                    const double v = !inal ? DMIN : ((r != 0) ? pxa[u][c] + cf[u][c] : pxa[u][c]);
+                    m = fmin(m, v);
+                }
+            }
+            if (alive) {
+                run[(size_t)i * CB] = m;
+                best = (m > best) ? m : best;
             }
         }
-        if (alive) {
-            run[(size_t)i * CB] = m;
-            best = (m > best) ? m : best;
-            any = true;
+        ta = tb;
+        tb = tn;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            ma[u] = mb[u];
+#pragma unroll
+            for (int c = 0; c < CB; c++) pxa[u][c] = pxb[u][c];
         }
     }
     best = lane_reduce<1>(best, [](double a, double b) { return (b > a) ? b : a; });
-    any = wave_or((uint32_t)any) != 0;
     wave_mem_sync();
-    return any ? best : DMIN;
+    return best != -INFINITY ? best : DMIN;
+}
+
+template <int CB>
+__device__ __forceinline__ double screen_leaf(const DD &d, BatchView &bv, const Pool &pool, int nb, bool first,
+                                              GBL double *run) {
+    if (d.T - 2 < d.kg) return screen_leaf_t<CB, true>(d, bv, pool, nb, first, run);
+    return screen_leaf_t<CB, false>(d, bv, pool, nb, first, run);
 }
 
 // root fold (DD.cpp:3938-3949) of pool row `id` (lane-uniform or per lane)
@@ -1740,17 +1953,26 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
         st.stamp(2);
         int next = s + nb;
         if (feas) {
-            // feasibility cuts: last layer materialised, removal + cascade replayed per cut
-            sweep_tail_layer<CB>(net, d, bv, pool, last, nb, kS);
+            // feasibility cuts: one scan of the last layer (first removing cut per leaf),
+            // then removal + cascade replayed per cut
+            batch_coef_direct(net, d, bv, pool, last, nb);
+            uint32_t rm[CB];
+            double mstate[CB];
+            f_leaf_scan<CB>(d, bv, pool, nb, kS, rm, mstate);
             st.stamp(3);
-            const GBL double *lbase = bv.s2b + (size_t)(uni(d.noff[last]) - bv.gbase) * CB;
             for (int c = 0; c < nb; c++) {
                 const int seq = s + c;
                 const int id = uni(bv.ids[c]);
                 st.last_cut = id;
                 st.applied++;
-                double maxState;
-                if (!dd_remove_last(d, LastVals{lbase + c, CB}, maxState)) { st.status = kPrunedFeasibility; return; }
+                double maxState = DMIN;
+#pragma unroll
+                for (int cc = 0; cc < CB; cc++) maxState = (cc == c) ? mstate[cc] : maxState;
+                uint32_t rmc = 0;
+#pragma unroll
+                for (int cc = 0; cc < CB; cc++) rmc = (cc == c) ? rm[cc] : rmc;
+                if (rmc == uni(d.nalive[last])) { st.status = kPrunedFeasibility; return; }
+                if (rmc) dd_cascade(d, (uint32_t)c + 1u);
                 if (!d.exact && dd_prune_check<CB>(d, bv, c, 1, last, -0.01, maxState)) {
                     st.stamp(4);
                     if (!redo_cut<CB>(net, d, bv, pool, id, lane_get(rv, c), 1, last, -0.01, maxState)) {

@@ -41,12 +41,16 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 // Global-memory hand-off between lanes of the wave (stores complete, then loads).
 __device__ __forceinline__ void wave_mem_sync() { __syncthreads(); }
 
+// Inclusive prefix sum over the wave with DPP (no LDS crossbar round trips): row_shr 1, 2,
+// 4, 8 scan each 16-lane row, then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3)
+// carry the row totals.  Lanes whose DPP source is outside the row read old = 0.
 __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        uint32_t y = __shfl_up(x, d, kWave);
-        if (lane() >= d) x += y;
-    }
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);   // row_bcast:31
     return x;
 }
 // Butterfly partner exchange without the LDS path: DPP row rotations inside 16-lane
