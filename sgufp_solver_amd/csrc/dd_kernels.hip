@@ -125,6 +125,9 @@ constexpr uint16_t kMirParent = 127, kMirRankShift = 7, kMirAlive = 1u << 12, kM
 __device__ __forceinline__ void mir_node_clear(DD &d, uint32_t node, uint16_t bits) {
     if (d.stream && node < d.Nn) d.tmir[node] &= (uint16_t)~bits;
 }
+__device__ __forceinline__ void mir_arc_kill(DD &d, uint32_t a, uint32_t rank) {
+    if (d.stream) d.tmir[d.Nn + a] = (uint16_t)(kNarrowMax | ((rank & 31u) << kMirRankShift));
+}
 __device__ __forceinline__ void mir_arc_clear(DD &d, uint32_t a) {
     // dead: no alive bit, parent slot = the NaN sentinel of the narrow sweep
     if (d.stream) d.tmir[d.Nn + a] = (uint16_t)((d.tmir[d.Nn + a] & ~(kMirAlive | kMirParent)) | kNarrowMax);
@@ -132,7 +135,7 @@ __device__ __forceinline__ void mir_arc_clear(DD &d, uint32_t a) {
 
 struct LdsCarve {
     size_t bytes;
-    size_t o_lay, o_rslot, o_buf, o_coef, o_walk, o_bcoef, o_w1, o_ids, o_sm1, o_xm1, o_v1, o_gs, o_ring, o_tring;
+    size_t o_lay, o_rslot, o_buf, o_coef, o_walk, o_bcoef, o_w1, o_ids, o_sm1, o_xm1, o_v1, o_gs, o_ring, o_tring, o_wm;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -154,6 +157,7 @@ __host__ __device__ inline LdsCarve lds_carve(int Tcap, int Lcap, int cb, int us
     c.o_gs = o; o = align16(o + (cb > 1 ? (size_t)(Tcap + 1) * 2 : 0));
     c.o_ring = o; o = align16(o + (cb > 1 ? (size_t)2 * kStageEntries * 8 : 0));
     c.o_tring = o; o = align16(o + (cb > 1 ? (size_t)2 * kTopoEntries * 2 : 0));
+    c.o_wm = o; o = align16(o + (cb > 1 ? (size_t)2 * ((Tcap + 63) / 64) * 8 : 0));   // write mask + fire mask words
     c.o_sm1 = c.o_xm1 = c.o_v1 = 0;
     c.bytes = o;
     return c;
@@ -766,6 +770,9 @@ struct BatchView {
     LDS double *coef;      // [CB][ustride]
     LDS uint8_t *w1;       // [Tcap]: layer had one alive node when the batch started
     LDS int32_t *ids;      // [CB]: pool row of each batch cut
+    LDS uint64_t *wm;      // [ceil(Tcap/64)] layers whose state2 a sweep writes (exact redo), or null
+    LDS uint64_t *fm;      // [ceil(Tcap/64)] width-1 layers whose pruning fires (exact redo)
+    const LDS uint64_t *wsel;   // the write mask in force (null: the kS rule)
     GBL double *s2b;       // HBM [tail_cap][CB]: layers >= kg
     GBL double *sm, *xm;   // HBM [Tcap][CB]
     uint32_t gbase;    // noff[kg]
@@ -899,16 +906,22 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
     // LDS round trip per field; mmask: which of those layers are merged layers.
     uint32_t m_noff = 0, m_aoff = 0, m_pk = 0;
     uint64_t mmask = 0;
+    // bit 30 of the packed word: this layer's state2 (of the last batch cut) is written --
+    // what a path walk reads (merged layers and their parents, above the cutset layer kS)
+    // or, in an exact redo, the layers of the write mask
     auto load_meta = [&](int kw) {
         const int k = kw + lane();
         const bool ok = k < d.T;
         const int kk = ok ? k : 0;
         const uint32_t no = d.noff[kk], ao = d.aoff[kk], nn = d.nn[kk], ac = d.acnt[kk];
+        const uint32_t an = kk + 1 < d.T ? d.acnt[kk + 1] : 0u;
         const uint32_t w = bv.w1[kk];
+        const uint64_t wsw = bv.wsel ? bv.wsel[kk >> 6] : 0ull;
         sched_fence();
         m_noff = no;
         m_aoff = ao;
-        m_pk = (nn < 255u ? nn : 255u) | ((ac & 0xFFFu) << 8) | (w ? 0x80000000u : 0u);
+        const bool wrl = bv.wsel ? ((wsw >> (kk & 63)) & 1ull) != 0 : (k < kS && (kS >= d.T || ac != 0 || an != 0));
+        m_pk = (nn < 255u ? nn : 255u) | ((ac & 0xFFFu) << 8) | (wrl ? 0x40000000u : 0u) | (w ? 0x80000000u : 0u);
         mmask = __ballot(ok && ac != 0);
     };
     auto rl = [](uint32_t v, int l) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); };
@@ -940,7 +953,7 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
             nofs[s] = rl(m_noff, l0 + s);
             ebase[s] = nofs[s] - gn0_;
             w1s[s] = (rl(m_pk, l0 + s) >> 31) != 0;
-            wrs[s] = ka + s < kS && (kS >= d.T || ((mmask >> (l0 + s + 1)) & 1ull) != 0);
+            wrs[s] = ((rl(m_pk, l0 + s) >> 30) & 1u) != 0;
         }
         const uint32_t nlast = rl(m_pk, l0 + D - 1) & 255u;
         const bool wlane = c == nb - 1;   // the lane whose cut's state2 the path walks read
@@ -1032,7 +1045,7 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
         if (acnt) {
             // state2 of the last batch cut: only what a path walk reads (merged nodes and
             // their parents) unless every layer is asked for (kS = T: the exact redo)
-            const bool wr = k < kS;
+            const bool wr = ((pk >> 30) & 1u) != 0;
             const uint32_t aoff = rl(m_aoff, l);
             const uint32_t ebase = gnN + (aoff - ga0);   // ring entry of the layer's first arc
             auto word = [&](uint32_t e) -> uint32_t { return (uint32_t)tr[e]; };
@@ -1186,8 +1199,9 @@ __device__ __forceinline__ void sweep_tail_layer_t(const NetDev &net, DD &d, Bat
     batch_coef_direct(net, d, bv, pool, k, nb);
     const int us = pool.ustride;
     const uint32_t noff = uni(d.noff[k]), n = uni(d.nn[k]);
-    // state2 of tail layers is read only by the exact redo (kS = T); see sweep_narrow
-    const bool w1 = uni(bv.w1[k]) != 0, wr = kS >= d.T;
+    // state2 of tail layers is read only by the exact redo (its write mask, or kS = T)
+    const bool w1 = uni(bv.w1[k]) != 0;
+    const bool wr = bv.wsel ? ((bv.wsel[k >> 6] >> (k & 63)) & 1ull) != 0 : kS >= d.T;
     const ParentVals<CB, PV_LDS> pv = parent_vals<CB, PV_LDS>(d, bv, k - 1);
     GBL double *out = bv.s2b + (size_t)(noff - bv.gbase) * CB;
     auto load_topo = [&](uint32_t base, WideTopo<CB> &tp) {
@@ -1757,31 +1771,150 @@ __device__ __forceinline__ void cut_loop_single(const NetDev &net, DD &d, const 
     }
 }
 
-// Exact redo of one cut whose width-1 pruning fires: a batched sweep with this cut
-// alone (state2 of every layer below the last one), then the pruning of layers
-// [first, end) from its summaries (DD.cpp:3895-3928 / 3987-4021).  Returns false
+// Width-1 pruning of cut `id` over the layers of the fire mask fm (DD.cpp:3895-3928 /
+// 3987-4021): in each, every alive in-arc with parent.state2 + weight + gain <= thresh
+// goes, gain = maxState - state2 of the layer's single node.  Marks use the sweep's
+// state2 only and removing an arc of one layer changes nothing another layer reads, so
+// the layers are processed back to back with their loads batched and no hand-off in
+// between (removing them at once, as the reference's batchRemoveArcs, is the same).
+// Returns false when some layer would lose all of its incoming arcs.
+template <int CB>
+__device__ __forceinline__ bool prune_layers(const NetDev &net, DD &d, const BatchView &bv, const Pool &pool, int id, int first,
+                                             int end, double maxState, double thresh) {
+    constexpr int U = 4;
+    const int us = pool.ustride;
+    const GBL double *ct = pool.coefT + (size_t)id * ((size_t)net.L * us);
+    bool ok = true;
+    for (int wb = first & ~63; wb < end && ok; wb += kWave) {
+        uint64_t b = bv.fm[wb >> 6];
+        while (b && ok) {
+            const int k = wb + (int)(__ffsll((unsigned long long)b) - 1);
+            b &= b - 1;
+            const uint32_t pnoff = uni(d.noff[k - 1]), acnt = uni(d.acnt[k]);
+            const GBL double *ck = ct + (size_t)(d.g + k - 1) * us;
+            uint32_t total = 0, pruned = 0;
+            if (acnt) {
+                const uint32_t aoff = uni(d.aoff[k]);
+                const double gain = maxState - d.s2[uni(d.noff[k])];
+                for (uint32_t base = 0; base < acnt; base += U * kWave) {
+                    uint32_t fl[U], tp[U];
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        const uint32_t a = base + (uint32_t)u * kWave + lane();
+                        const uint32_t ac = a < acnt ? a : 0u;
+                        fl[u] = a < acnt ? (uint32_t)d.aflag[aoff + ac] : 0u;
+                        tp[u] = d.atopo[aoff + ac];
+                    }
+                    sched_fence();
+                    double px[U], w[U];
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        const uint32_t r = tp[u] >> kRankShift;
+                        px[u] = d.s2[pnoff + (tp[u] & kParentMask)];
+                        w[u] = r == 0 ? 0.0 : ck[r];
+                    }
+                    sched_fence();
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        const uint32_t a = base + (uint32_t)u * kWave + lane();
+                        const bool alive = (fl[u] & kAlive) != 0;
+                        const bool pr = alive && ((px[u] + w[u]) + gain) <= thresh;
+                        if (pr) {
+                            d.aflag[aoff + a] = 0;
+                            mir_arc_kill(d, aoff + a, tp[u] >> kRankShift);
+                            __hip_atomic_fetch_sub(&d.outcnt[pnoff + (tp[u] & kParentMask)], 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                        total += (uint32_t)__popcll(__ballot(alive));
+                        pruned += (uint32_t)__popcll(__ballot(pr));
+                    }
+                }
+            } else {
+                const uint32_t M = layer_single(d, k);
+                const uint32_t t = d.ntopo[M], f = d.nflag[M];
+                const uint32_t p = t & kParentMask, r = t >> kRankShift;
+                const double sM = d.s2[M], px = d.s2[pnoff + p], w = r == 0 ? 0.0 : ck[r];
+                if (f & kInAlive) {
+                    total = 1;
+                    if (((px + w) + (maxState - sM)) <= thresh) {
+                        pruned = 1;
+                        if (lane() == 0) {
+                            d.nflag[M] = (uint8_t)(f & ~kInAlive);
+                            mir_node_clear(d, M, kMirIn);
+                            d.outcnt[pnoff + p] -= 1u;
+                        }
+                    }
+                }
+            }
+            if (total == pruned) ok = false;
+        }
+    }
+    wave_mem_sync();
+    return ok;
+}
+
+// Fire mask of the batch cut c over [first, end) from the summaries sm/xm (stride CB) into
+// bv.fm; returns whether any layer fires.
+template <int CB>
+__device__ __forceinline__ bool fire_layers(const DD &d, BatchView &bv, int c, int first, int end, double thresh,
+                                            double maxState) {
+    const int nw = (d.T + 63) / 64;
+    for (int w = lane(); w < nw; w += kWave) bv.fm[w] = 0;
+    wave_lds_sync();
+    uint64_t any = 0;
+    for (int base = first; base < end; base += kWave) {
+        const uint64_t b = prune_fire(d, base, end, maxState, thresh, bv.sm + c, bv.xm + c, CB, bv.w1);
+        any |= b;
+        if (b && lane() == 0) {
+            // window [base, base + 64) may straddle two words
+            const int w0 = base >> 6, sh = base & 63;
+            bv.fm[w0] |= b << sh;
+            if (sh && w0 + 1 < nw) bv.fm[w0 + 1] |= b >> (64 - sh);
+        }
+    }
+    wave_lds_sync();
+    return any != 0;
+}
+
+// Exact redo of one cut whose width-1 pruning fires (batch cut c, pool row id): a sweep
+// with this cut alone, then the pruning (DD.cpp:3895-3928 / 3987-4021).  The pruning reads
+// state2 only in the firing layers and the layers above them; those are known before the
+// sweep from the batch summaries of cut c (same DD, same values), so the sweep writes
+// state2 of just those layers; the summaries the sweep recomputes must fire the same
+// layers (checked; otherwise the sweep is repeated writing every layer).  Returns false
 // when a width-1 layer would lose all of its incoming arcs.
 template <int CB>
-__device__ __forceinline__ bool redo_cut(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int id,
+__device__ __forceinline__ bool redo_cut(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int c, int id,
                                          double rv1, int first, int end, double thresh, double maxState) {
     const int last = d.T - 1;
+    const int nw = (d.T + 63) / 64;
+    fire_layers<CB>(d, bv, c, first, end, thresh, maxState);
+    for (int w = lane(); w < nw; w += kWave) {
+        const uint64_t f = bv.fm[w], fn = w + 1 < nw ? bv.fm[w + 1] : 0ull;
+        bv.wm[w] = f | (f >> 1) | (fn << 63);   // layer k fires -> write k and k - 1
+    }
     if (lane() == 0) bv.ids[0] = id;
     for (int k = lane(); k < d.T; k += kWave) bv.w1[k] = ((d.nalive[k]) == 1) ? 1 : 0;
     wave_lds_sync();
-    sweep_narrow<CB>(net, d, bv, pool, 1, rv1, d.T);
-    if (d.kg == 0 && lane() == 0) bv.s2b[0] = rv1;
-    for (int k = max(d.kg, 1); k < last; k++) sweep_tail_layer<CB>(net, d, bv, pool, k, 1, d.T);
-    wave_mem_sync();
-    const GBL double *row = pool.rows + (size_t)id * pool.stride;
-    for (int base = first; base < end; base += kWave) {
-        uint64_t b = prune_fire(d, base, end, maxState, thresh, bv.sm, bv.xm, CB, bv.w1);
-        while (b) {
-            int k = base + (int)(__ffsll((unsigned long long)b) - 1);
-            b &= b - 1;
-            if (!dd_prune_layer(net, d, row, k, maxState, thresh)) return false;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        bv.wsel = bv.wm;
+        sweep_narrow<CB>(net, d, bv, pool, 1, rv1, d.T);
+        if (d.kg == 0 && lane() == 0) bv.s2b[0] = rv1;
+        for (int k = max(d.kg, 1); k < last; k++) sweep_tail_layer<CB>(net, d, bv, pool, k, 1, d.T);
+        bv.wsel = nullptr;
+        wave_mem_sync();
+        // the fire mask of the fresh summaries must lie inside the write mask
+        bool covered = true;
+        fire_layers<CB>(d, bv, 0, first, end, thresh, maxState);
+        for (int w = 0; w < nw; w++) {
+            const uint64_t f = bv.fm[w], fn = w + 1 < nw ? bv.fm[w + 1] : 0ull;
+            if (((f | (f >> 1) | (fn << 63)) & ~bv.wm[w]) != 0) covered = false;
         }
+        if (covered) break;
+        for (int w = lane(); w < nw; w += kWave) bv.wm[w] = ~0ull;
+        wave_lds_sync();
     }
-    return true;
+    return prune_layers<CB>(net, d, bv, pool, id, first, end, maxState, thresh);
 }
 
 // CB cuts of one type per sweep, replayed in pool order (see "Multi-cut sweeps")
@@ -1975,7 +2108,7 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
                 if (rmc) dd_cascade(d, (uint32_t)c + 1u);
                 if (!d.exact && dd_prune_check<CB>(d, bv, c, 1, last, -0.01, maxState)) {
                     st.stamp(4);
-                    if (!redo_cut<CB>(net, d, bv, pool, id, lane_get(rv, c), 1, last, -0.01, maxState)) {
+                    if (!redo_cut<CB>(net, d, bv, pool, c, id, lane_get(rv, c), 1, last, -0.01, maxState)) {
                         st.status = kPrunedFeasibility;
                         return;
                     }
@@ -2030,7 +2163,7 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
                 const int c = redo;
                 const int id = uni(bv.ids[c]);
                 double v = redo_v;
-                if (!redo_cut<CB>(net, d, bv, pool, id, lane_get(rv, c), 3, last - 1, incumbent - 0.01, redo_ms))
+                if (!redo_cut<CB>(net, d, bv, pool, c, id, lane_get(rv, c), 3, last - 1, incumbent - 0.01, redo_ms))
                     v = DMIN;
                 st.applied++;
                 st.last_cut = id;
@@ -2116,6 +2249,9 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
         bv.coef = (LDS double *)(smem + cv.o_bcoef);
         bv.w1 = smem + cv.o_w1;
         bv.ids = (LDS int32_t *)(smem + cv.o_ids);
+        bv.wm = (LDS uint64_t *)(smem + cv.o_wm);
+        bv.fm = bv.wm + (sc.Tcap + 63) / 64;
+        bv.wsel = nullptr;
         bv.s2b = sc.s2b + (size_t)slot * sc.tail_cap * CB;
         bv.sm = sc.sm + (size_t)slot * sc.Tcap * CB;
         bv.xm = sc.xm + (size_t)slot * sc.Tcap * CB;
