@@ -871,27 +871,6 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
     if (d.ng == 0) return;
     double pf[PC] = {};
     uint32_t pt[PT] = {};
-    auto issue = [&](int j) {
-        if (j >= d.ng) return;
-        const int k0 = uni((int)d.gstart[j]), k1 = uni((int)d.gstart[j + 1]);
-        const uint32_t n0 = uni(d.noff[k0]), nN = uni(d.noff[k1]) - n0;
-        const uint32_t a0 = uni(d.aoff[k0]), nA = uni(d.aoff[k1]) - a0;
-#pragma unroll
-        for (int jj = 0; jj < PC; jj++) {
-            const int e = lane() + jj * kWave;
-            const int lo = e / per_layer, rem = e - lo * per_layer;
-            const int k = k0 + lo;
-            const int cc = rem / us, r = rem - cc * us;
-            const bool ok = k < k1;
-            pf[jj] = pool.coefT[ok ? (size_t)bv.ids[cc] * ltab + (size_t)(d.g + k - 1) * us + r : 0];
-        }
-#pragma unroll
-        for (int jj = 0; jj < PT; jj++) {
-            const uint32_t e = (uint32_t)(lane() + jj * kWave);
-            const uint32_t idx = e < nN ? n0 + e : (e < nN + nA ? d.Nn + a0 + (e - nN) : 0u);
-            pt[jj] = d.tmir[idx];
-        }
-    };
     auto commit = [&](int slot) {
         LDS double *ring = bv.cring + (size_t)slot * kStageEntries;
         LDS uint16_t *tr = bv.tring + (size_t)slot * kTopoEntries;
@@ -925,6 +904,37 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
         mmask = __ballot(ok && ac != 0);
     };
     auto rl = [](uint32_t v, int l) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); };
+
+    // ring entry e = lane + jj * 64 of a group stages the coefficient of layer k0 + lo, batch
+    // cut cc, rank r: the per-lane constants are computed once per sweep
+    int c_lo[PC];
+    uint32_t c_off[PC];
+#pragma unroll
+    for (int jj = 0; jj < PC; jj++) {
+        const int e = lane() + jj * kWave;
+        const int lo = e / per_layer, rem = e - lo * per_layer;
+        const int cc = rem / us, r = rem - cc * us;
+        c_lo[jj] = lo;
+        c_off[jj] = (uint32_t)(bv.ids[cc < nb ? cc : 0] * (int)ltab + r);
+    }
+    // prefetch of the group [k0g, k1g) into registers (layer offsets from the metadata
+    // window, which holds both ends)
+    auto issue = [&](int k0g, int k1g, int lw0) {
+        const uint32_t n0 = rl(m_noff, k0g - lw0), nN = rl(m_noff, k1g - lw0) - n0;
+        const uint32_t a0 = rl(m_aoff, k0g - lw0), nA = rl(m_aoff, k1g - lw0) - a0;
+#pragma unroll
+        for (int jj = 0; jj < PC; jj++) {
+            const int k = k0g + c_lo[jj];
+            const bool ok = k < k1g;
+            pf[jj] = pool.coefT[ok ? (size_t)c_off[jj] + (size_t)(d.g + k - 1) * us : 0];
+        }
+#pragma unroll
+        for (int jj = 0; jj < PT; jj++) {
+            const uint32_t e = (uint32_t)(lane() + jj * kWave);
+            const uint32_t idx = e < nN ? n0 + e : (e < nN + nA ? d.Nn + a0 + (e - nN) : 0u);
+            pt[jj] = d.tmir[idx];
+        }
+    };
 
     // Exact run [ka, kb] of odd depth D (see the call site).  Every node has one in-arc, so
     // a node's value is the fold of its ancestors' steps from layer ka - 1,
@@ -1011,12 +1021,12 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
             for (uint32_t base = 0; base < nlast; base += 2 * G) items(std::integral_constant<int, 2>{}, base);
     };
 
-    issue(0);
-    commit(0);
-    issue(1);
     int j = 0, slot = 0;
     int k0 = uni((int)d.gstart[0]), k1 = uni((int)d.gstart[1]);
     load_meta(k0);
+    issue(k0, k1, k0);
+    commit(0);
+    if (d.ng > 1) issue(k1, uni((int)d.gstart[2]), k0);
     uint32_t gn0 = rl(m_noff, 0), gnN = rl(m_noff, k1 - k0) - gn0, ga0 = rl(m_aoff, 0);
     wave_lds_sync();
     for (int k = 1; k < d.kg;) {
@@ -1025,10 +1035,10 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
             j++;
             slot ^= 1;
             commit(slot);
-            issue(j + 1);
             k0 = k1;
             k1 = uni((int)d.gstart[j + 1]);
             load_meta(k0);
+            if (j + 1 < d.ng) issue(k1, uni((int)d.gstart[j + 2]), k0);
             gn0 = rl(m_noff, 0);
             gnN = rl(m_noff, k1 - k0) - gn0;
             ga0 = rl(m_aoff, 0);
@@ -1053,12 +1063,13 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
             // words first, then all parent values / coefficients, so one step costs two LDS
             // round trips and a narrow layer runs no idle unrolled items.
             auto dispatch = [&](uint32_t count, auto &&step) {
-                const uint32_t per = (count + G - 1) / G;
-                if (per <= 1) step(std::integral_constant<int, 1>{}, 0u);
-                else if (per <= 2) step(std::integral_constant<int, 2>{}, 0u);
-                else if (per <= 4) step(std::integral_constant<int, 4>{}, 0u);
-                else
-                    for (uint32_t base = 0; base < count; base += G * 8) step(std::integral_constant<int, 8>{}, base);
+                uint32_t base = 0;
+                for (; count - base > (uint32_t)G * 8; base += G * 8) step(std::integral_constant<int, 8>{}, base);
+                const uint32_t per = (count - base + G - 1) / G;
+                if (per <= 1) step(std::integral_constant<int, 1>{}, base);
+                else if (per <= 2) step(std::integral_constant<int, 2>{}, base);
+                else if (per <= 4) step(std::integral_constant<int, 4>{}, base);
+                else step(std::integral_constant<int, 8>{}, base);
             };
             // Fast path: a plain max / min over the candidates parent + coefficient.  Dead
             // arcs carry parent slot 127 (kNarrowMax), whose value is a quiet NaN that
