@@ -232,9 +232,12 @@ __device__ inline uint32_t bf_pass(const SubNet &N, const SubLds &W, int nct, in
     auto arc = [&](uint32_t th, int64_t w, bool exists, bool forward) {
         const int t = (int)(th & 0xFFFFu), h = (int)(th >> 16);
         const int u = forward ? t : h, v = forward ? h : t;
+        // both end keys in one LDS round trip (fenced: the compiler would otherwise sink the
+        // second load under the first comparison and pay two)
         const int64_t ku = W.key[u], kv = W.key[v];
+        sched_fence();
         const int64_t nk = ku + w;
-        if (exists && ku < kInf && nk < kv) {
+        if (exists & (ku < kInf) & (nk < kv)) {
             __hip_atomic_fetch_min(&W.key[v], nk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             changed = 1;
         }
