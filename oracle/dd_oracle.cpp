@@ -13,6 +13,9 @@
 //   * node / arc deletion and updateTree .......... /root/reference/DD.cpp:4025-4177
 //   * getCutset ................................... /root/reference/DD.cpp:4179-4218
 //   * NodeExplorer::process (up to the first LP) .. /root/reference/NodeExplorer.cpp:915-986
+//   * RestrictedDDNew (compile, cut sweeps,
+//     getMaxPath, exact cutset) ................... /root/reference/DD.cpp:3090-3505
+//   * the restricted cut phases of processX3 ....... /root/reference/NodeExplorer.cpp:605-656
 // Data structures are plain index arrays (no hash maps).  Pinned against the
 // reference compiled from its own sources (oracle/_ref/ref_dd, see oracle/Makefile)
 // and the fixtures under tests/golden/.
@@ -20,6 +23,7 @@
 // Same CLI and text formats as oracle/ref_driver.cpp:
 //   dd_oracle relax <network> <cuts> <nodes> <incumbent> <out>
 //   dd_oracle time  <network> <cuts> <nodes> <incumbent> <threads> <seconds>
+//   dd_oracle restricted <network> <cuts> <nodes> <incumbent> <width> <out>
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -518,6 +522,179 @@ static void write_result(FILE *f, const Result &r) {
     for (auto &c : r.children) write_node(f, c);
 }
 
+// ------------------------------------------------------------------ restricted DD
+// RestrictedDDNew (DD.cpp:3090-3505): a tree.  Layers expand exactly -- each node's states
+// in reverse stored order, child states = parent minus the decision (-1 keeps all) --
+// until a layer would exceed `width` nodes: that layer keeps its first `width` children
+// and from then on every node gets one child, the decision its largest state
+// (buildRestrictedLayer, DD.cpp:3161-3220).  Only last-layer nodes are ever removed.
+struct RDD {
+    const Net *net = nullptr;
+    unsigned width = 128;
+    struct RNode { int parent = -1; int16_t dec = 0; int gl = 0; int layer = 0; std::vector<int16_t> states; double s2 = 0; };
+    std::vector<RNode> nodes;
+    std::vector<std::vector<int>> tree;      // node ids per layer (no terminal layer)
+    std::vector<int> term;                   // last-layer nodes with a terminal arc, in order
+    std::vector<double> tw;                  // terminal arc weight per node id (only leaves)
+    std::vector<int16_t> root_sol;
+    bool exact = true;
+    size_t exact_layer = 0;
+
+    void compile(const NodeRec &rec) {      // DD.cpp:3090-3159
+        nodes.clear(); tree.clear(); term.clear();
+        root_sol = rec.sol;
+        RNode root; root.gl = rec.gl; root.states = rec.states; root.layer = 0;
+        nodes.push_back(root);
+        tree.push_back({0});
+        exact = true;
+        exact_layer = 0;
+        for (int a = rec.gl; a < net->L; a++) {
+            std::vector<int> &cur = tree.back();
+            auto it = net->update.find(a);
+            if (it != net->update.end()) {
+                std::vector<int16_t> st(it->second.begin(), it->second.end());
+                for (int id : cur) nodes[id].states = st;
+            }
+            std::vector<int> nxt;
+            const std::vector<int> curc = cur;
+            if (exact) {
+                size_t count = 0;
+                bool stop = false;
+                for (int id : curc) {
+                    const std::vector<int16_t> st = nodes[id].states;
+                    for (size_t r = st.size(); r-- > 0;) {
+                        if (count >= width) { exact = false; stop = true; break; }
+                        RNode ch;
+                        ch.parent = id; ch.dec = st[r];
+                        ch.states = st;
+                        if (ch.dec != -1) ch.states.erase(std::find(ch.states.begin(), ch.states.end(), ch.dec));
+                        ch.gl = nodes[id].gl + 1; ch.layer = nodes[id].layer + 1;
+                        nodes.push_back(ch);
+                        nxt.push_back((int)nodes.size() - 1);
+                        count++;
+                    }
+                    if (stop) break;
+                }
+            } else {
+                for (int id : curc) {
+                    const std::vector<int16_t> &st = nodes[id].states;
+                    RNode ch;
+                    ch.parent = id;
+                    ch.dec = *std::max_element(st.begin(), st.end());
+                    ch.states = st;
+                    if (ch.dec != -1) ch.states.erase(std::find(ch.states.begin(), ch.states.end(), ch.dec));
+                    ch.gl = nodes[id].gl + 1; ch.layer = nodes[id].layer + 1;
+                    nodes.push_back(ch);
+                    nxt.push_back((int)nodes.size() - 1);
+                }
+            }
+            if (exact) exact_layer++;
+            tree.push_back(nxt);
+        }
+        term = tree.back();
+        tw.assign(nodes.size(), DMAX);
+    }
+
+    std::vector<int16_t> path_of(int id) const {   // getPathForNode (DD.cpp:3262-3277)
+        std::vector<int16_t> rev;
+        while (nodes[id].layer) { rev.push_back(nodes[id].dec); id = nodes[id].parent; }
+        std::vector<int16_t> sol(root_sol.begin(), root_sol.end());
+        sol.insert(sol.end(), rev.rbegin(), rev.rend());
+        return sol;
+    }
+
+    std::vector<NodeRec> cutset() const {          // getExactCutSet (DD.cpp:3279-3288)
+        std::vector<NodeRec> out;
+        for (int id : tree[exact_layer]) {
+            NodeRec r;
+            r.gl = nodes[id].gl; r.lb = DMIN; r.ub = DMIN;
+            r.states = nodes[id].states;
+            r.sol = path_of(id);
+            out.push_back(r);
+        }
+        return out;
+    }
+
+    double coef_for(const Cut &cut, size_t layer_idx, int16_t dec) const {
+        int na = net->order_arc[layer_idx];
+        uint64_t i = (uint64_t)net->tail[na], q = (uint64_t)net->head[na];
+        return cut.get(key_of(q, i, (uint64_t)net->head[dec]));
+    }
+
+    void sweep(const Cut &cut) {                   // DD.cpp:3346-3374 / 3431-3461
+        size_t i = 0;
+        double v = cut.rhs;
+        for (int16_t d : root_sol) {
+            if (d == -1) { i++; continue; }
+            v = v + coef_for(cut, i, d);
+            i++;
+        }
+        nodes[0].s2 = v;
+        for (size_t layer = 1; layer < tree.size(); layer++) {
+            size_t li = i++;
+            const std::vector<int> &ids = (layer + 1 == tree.size()) ? term : tree[layer];
+            for (int id : ids) {
+                RNode &nd = nodes[id];
+                const double ps = nodes[nd.parent].s2;
+                nd.s2 = nd.dec != -1 ? coef_for(cut, li, nd.dec) + ps : ps;
+            }
+        }
+    }
+
+    bool apply_feasibility(const Cut &cut) {      // DD.cpp:3340-3423
+        sweep(cut);
+        if (term.empty()) return false;
+        std::vector<int> keep;
+        for (int id : term)
+            if (!(nodes[id].s2 < -0.5)) keep.push_back(id);
+        term = keep;
+        return !term.empty();
+    }
+
+    double apply_optimality(const Cut &cut) {     // DD.cpp:3425-3505
+        sweep(cut);
+        double t = DMIN;
+        for (int id : term) {
+            tw[id] = smin(tw[id], nodes[id].s2);
+            t = smax(t, tw[id]);
+        }
+        return t;
+    }
+
+    std::vector<int16_t> max_path() const {        // getMaxPath (DD.cpp:3290-3305)
+        int best = 0;
+        double bw = DMIN;
+        for (int id : term)
+            if (tw[id] > bw) { bw = tw[id]; best = id; }
+        return path_of(best);
+    }
+};
+
+static void restricted(FILE *f, const Net &net, const NodeRec &nd, double optimalLB, const std::vector<Cut> &cuts,
+                       unsigned width) {
+    RDD dd; dd.net = &net; dd.width = width;
+    dd.compile(nd);
+    double lowerBound = nd.lb;
+    int status = 0;
+    for (size_t k = cuts.size(); k-- > 0 && status == 0;)
+        if (cuts[k].type == 1 && !dd.apply_feasibility(cuts[k])) status = 1;
+    for (size_t k = cuts.size(); k-- > 0 && status == 0;) {
+        if (cuts[k].type != 0) continue;
+        lowerBound = dd.apply_optimality(cuts[k]);
+        if (lowerBound <= optimalLB) status = 2;
+    }
+    std::vector<int16_t> path;
+    if (status == 0) path = dd.max_path();
+    std::vector<NodeRec> cs;
+    if (!dd.exact) cs = dd.cutset();
+    std::fprintf(f, "Q %d %d %a %zu %zu\n", status, dd.exact ? 1 : 0, lowerBound, cs.size(), path.size());
+    if (!path.empty()) {
+        for (size_t k = 0; k < path.size(); k++) std::fprintf(f, "%s%d", k ? " " : "", (int)path[k]);
+        std::fprintf(f, "\n");
+    }
+    for (auto &c : cs) write_node(f, c);
+}
+
 }  // namespace oracle
 
 int main(int argc, char **argv) {
@@ -538,6 +715,19 @@ int main(int argc, char **argv) {
             }
             std::printf("\n");
         }
+        return 0;
+    }
+    if (mode == "restricted" && argc == 8) {
+        Net net;
+        if (!load_network(argv[2], net)) return 2;
+        auto cuts = read_cuts(argv[3]);
+        auto nodes = read_nodes(argv[4]);
+        double inc = std::strtod(argv[5], nullptr);
+        unsigned width = (unsigned)std::strtoul(argv[6], nullptr, 10);
+        FILE *f = std::fopen(argv[7], "w");
+        std::fprintf(f, "%zu\n", nodes.size());
+        for (auto &nd : nodes) restricted(f, net, nd, inc, cuts, width);
+        std::fclose(f);
         return 0;
     }
     if (mode == "refine" && argc == 8) {

@@ -17,6 +17,9 @@
 //   ref_dd bfs    <network> <cuts> <incumbent-hex> <max-nodes> <out-nodes>
 //   ref_dd time   <network> <cuts> <nodes> <incumbent-hex> <threads> <seconds>
 //   ref_dd apply  <network> <cuts> <nodes> <out>     (per-cut trace, exact/non-exact alike)
+//   ref_dd restricted <network> <cuts> <nodes> <incumbent-hex> <width> <out>
+//                  (Inavap::RestrictedDDNew, DD.cpp:3090-3505, under the cut phases of
+//                   NodeExplorer::processX3, NodeExplorer.cpp:605-656)
 //
 // File formats (text; doubles as C99 hex floats, "%a"):
 //   cuts : <ncuts>\n then per cut "<type 0=opt 1=feas> <rhs> <nnz>\n" and nnz lines "<i> <q> <j> <val>"
@@ -34,6 +37,7 @@
 #include <deque>
 #include <fstream>
 #include <iostream>
+#include <memory>
 #include <sstream>
 #include <string>
 #include <thread>
@@ -159,6 +163,39 @@ static void write_result(FILE *f, const Result &r) {
     for (auto &c : r.children) write_node(f, c);
 }
 
+// The restricted-DD half of NodeExplorer::processX3 (NodeExplorer.cpp:605-656): compile a
+// width-limited restricted DD (RestrictedDDNew::compile, DD.cpp:3090-3159), apply the pool's
+// feasibility cuts then its optimality cuts (each list newest first; the first false /
+// the first bound <= optimalLB ends the node), then the max path (getSolution ->
+// getMaxPath, DD.cpp:3290-3305).  status 0 = ok, 1 = infeasible, 2 = bound <= optimalLB.
+static void restricted(FILE *f, const std::shared_ptr<Network> &np, const Inavap::Node &nd, double optimalLB,
+                       const std::vector<PoolCut> &cuts, unsigned width) {
+    Inavap::RestrictedDDNew dd{np, width};
+    auto cs = dd.compile(nd);
+    int exact = dd.isTreeExact() ? 1 : 0;
+    double lowerBound = nd.lb;
+    int status = 0;
+    for (size_t k = cuts.size(); k-- > 0 && status == 0;) {
+        if (cuts[k].type != 1) continue;
+        if (!dd.applyFeasibilityCut(cuts[k].cut)) status = 1;
+    }
+    for (size_t k = cuts.size(); k-- > 0 && status == 0;) {
+        if (cuts[k].type != 0) continue;
+        lowerBound = dd.applyOptimalityCut(cuts[k].cut);
+        if (lowerBound <= optimalLB) status = 2;
+    }
+    std::vector<int16_t> path;
+    if (status == 0) path = dd.getSolution();
+    size_t nc = cs ? cs->size() : 0;
+    std::fprintf(f, "Q %d %d %a %zu %zu\n", status, exact, lowerBound, nc, path.size());
+    if (!path.empty()) {
+        for (size_t k = 0; k < path.size(); k++) std::fprintf(f, "%s%d", k ? " " : "", (int)path[k]);
+        std::fprintf(f, "\n");
+    }
+    if (cs)
+        for (auto &c : *cs) write_node(f, c);
+}
+
 int main(int argc, char **argv) {
     if (argc < 2) { std::cerr << "usage: see header\n"; return 2; }
     std::string mode = argv[1];
@@ -261,6 +298,18 @@ int main(int argc, char **argv) {
             }
             write_result(f, r);
         }
+        std::fclose(f);
+        return 0;
+    }
+    if (mode == "restricted" && argc == 8) {
+        auto np = std::make_shared<Network>(argv[2]);
+        auto cuts = read_cuts(argv[3]);
+        auto nodes = read_nodes(argv[4]);
+        double inc = parse_double(argv[5]);
+        unsigned width = (unsigned)std::strtoul(argv[6], nullptr, 10);
+        FILE *f = std::fopen(argv[7], "w");
+        std::fprintf(f, "%zu\n", nodes.size());
+        for (auto &nd : nodes) restricted(f, np, nd, inc, cuts, width);
         std::fclose(f);
         return 0;
     }

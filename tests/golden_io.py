@@ -81,3 +81,45 @@ def refine_manifest():
         return {}
     with open(p) as fh:
         return json.load(fh)
+
+
+# ---------------------------------------------------------------- restricted DD fixtures
+RESTRICTED = os.path.join(GOLDEN, "restricted")
+
+
+def restricted_manifest():
+    with open(os.path.join(GOLDEN, "restricted_manifest.json")) as fh:
+        return json.load(fh)
+
+
+def restricted_dir(name: str) -> str:
+    return os.path.join(RESTRICTED, name)
+
+
+def read_restricted(name: str, fname: str) -> str:
+    with gzip.open(os.path.join(restricted_dir(name), fname), "rb") as fh:
+        return fh.read().decode()
+
+
+def parse_restricted_text(text: str):
+    """Per node: (status, exact, lb, path, children) from "Q status exact lb nchildren npath"
+    blocks (oracle/ref_driver.cpp "restricted")."""
+    lines = text.splitlines()
+    out, k = [], 1
+    while k < len(lines):
+        q = lines[k].split()
+        k += 1
+        st, ex, lb, nc, np_ = int(q[1]), int(q[2]), float.fromhex(q[3]), int(q[4]), int(q[5])
+        path = [int(x) for x in lines[k].split()] if np_ else []
+        k += 1 if np_ else 0
+        kids = []
+        for _ in range(nc):
+            t = lines[k].split()
+            k += 1
+            gl, ns = int(t[0]), int(t[3])
+            states = [int(x) for x in t[4:4 + ns]]
+            nsol = int(t[4 + ns])
+            sol = [int(x) for x in t[5 + ns:5 + ns + nsol]]
+            kids.append(pools.NodeRecord(gl, float.fromhex(t[1]), float.fromhex(t[2]), states, sol))
+        out.append((st, ex, lb, path, kids))
+    return out
