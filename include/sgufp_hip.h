@@ -198,6 +198,27 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
  * e.g. to all-gather the cuts a round produced to the other frontier shards. */
 int sgufp_cuts_rows(sgufp_ctx *ctx, int is_feasibility, int first, int count, double *rhs, double *rows);
 
+/* -- restricted decision diagram (replaces Inavap::RestrictedDDNew, DD.h:653-730 /
+ *    DD.cpp:3090-3505, driven as in NodeExplorer::processX3, NodeExplorer.cpp:605-656) --
+ * For every staged node (sgufp_batch_upload): RestrictedDDNew{net, width}.compile(node)
+ * (width <= 128), then the pool's feasibility cuts and then its optimality cuts, each list
+ * newest first (applyFeasibilityCut / applyOptimalityCut); the first false ends the node
+ * with status 1, the first bound <= optimal_lb with status 2. */
+int sgufp_restricted_relax(sgufp_ctx *ctx, int width, double optimal_lb);
+/* Per staged node: status (0, 1, 2; 16 = record not representable), isTreeExact(), the
+ * bound of the last optimality cut applied (node.lb when none), the length of the max path
+ * (getSolution, status 0 only, else 0) and the number of exact-cutset records compile()
+ * returned (0 for an exact tree).  Any pointer may be NULL. */
+int sgufp_restricted_results(sgufp_ctx *ctx, int32_t *status, uint8_t *exact, double *lb, int32_t *path_len,
+                             int32_t *cutset_n);
+/* Max paths (path_off has n+1 entries). */
+int sgufp_restricted_paths(sgufp_ctx *ctx, int64_t *path_off, int16_t *paths);
+/* The exact cutsets as Inavap::Node records (getExactCutSet, DD.cpp:3279-3288: states,
+ * solution, lb = ub = DOUBLE_MIN, globalLayer); node k's are [rec_off[k], rec_off[k+1]). */
+int sgufp_restricted_cutset_size(sgufp_ctx *ctx, int64_t *n_records, int64_t *n_states, int64_t *n_sol);
+int sgufp_restricted_cutset(sgufp_ctx *ctx, int64_t *rec_off, uint16_t *gl, double *lb, double *ub,
+                            int64_t *states_off, int16_t *states, int64_t *sol_off, int16_t *sol);
+
 /* -- timing (hipEvents on the ctx stream around each kernel of the last relax) -- */
 int sgufp_set_timing(sgufp_ctx *ctx, int enabled);
 int sgufp_last_timing(const sgufp_ctx *ctx, float *ms_relax, float *ms_emit);

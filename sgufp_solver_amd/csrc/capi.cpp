@@ -334,6 +334,22 @@ void sgufp_ctx::encode_records(int n, const uint16_t *gl, const int64_t *states_
     }
 }
 
+bool sgufp_ctx::rdd_init() {
+    if (rdd_ready) return true;
+    const size_t B = (size_t)max_batch;
+    rio.Tcap = sc.Tcap;
+    rio.Lcap = sc.Lcap;
+    if (rdd_lds_bytes(rio.Tcap, rio.Lcap, ustride) > 64 * 1024) { err = "too many layers for the restricted DD"; return false; }
+    if (!alloc(rio.topo, B * rio.Tcap * kRddMax, "restricted") || !alloc(rio.cmask, B * kRddMax, "restricted") ||
+        !alloc(rio.csm, B * kRddMax, "restricted") || !alloc(rio.csdec, B * kRddMax * rio.Tcap, "restricted") ||
+        !alloc(rio.status, B, "restricted") || !alloc(rio.exact, B, "restricted") || !alloc(rio.lb, B, "restricted") ||
+        !alloc(rio.path, B * rio.Lcap, "restricted") || !alloc(rio.path_len, B, "restricted") ||
+        !alloc(rio.cs_n, B, "restricted") || !alloc(rio.cs_gl, B, "restricted"))
+        return false;
+    rdd_ready = true;
+    return true;
+}
+
 extern "C" {
 
 
@@ -870,6 +886,134 @@ int sgufp_batch_debug(sgufp_ctx *ctx, int64_t *ticks, int32_t *redo) {
         if (ticks) ticks[k] = (int64_t)t[k];
         if (redo) redo[k] = (int32_t)r[k];
     }
+    return SGUFP_OK;
+}
+
+int sgufp_restricted_relax(sgufp_ctx *ctx, int width, double optimal_lb) {
+    if (!ctx || width < 1 || width > kRddMax) return SGUFP_ERR_ARG;
+    if (!ctx->push_orders() || !ctx->rdd_init()) return SGUFP_ERR_HIP;
+    ctx->rio.width = width;
+    ctx->restricted_done = false;
+    const BatchIn in = ctx->staged();
+    if (!ctx->hip_ok(launch_restrict(ctx->nd, in, ctx->pool(), ctx->rio, optimal_lb, ctx->stream), "k_restrict") ||
+        !ctx->sync())
+        return SGUFP_ERR_HIP;
+    ctx->restricted_done = true;
+    return SGUFP_OK;
+}
+
+int sgufp_restricted_results(sgufp_ctx *ctx, int32_t *status, uint8_t *exact, double *lb, int32_t *path_len,
+                             int32_t *cutset_n) {
+    if (!ctx || !ctx->restricted_done) return ctx ? SGUFP_ERR_STATE : SGUFP_ERR_ARG;
+    const int n = ctx->n;
+    std::vector<uint16_t> pl(n);
+    std::vector<uint32_t> cn(n);
+    if ((status && !ctx->download(status, ctx->rio.status, n)) || (exact && !ctx->download(exact, ctx->rio.exact, n)) ||
+        (lb && !ctx->download(lb, ctx->rio.lb, n)) || !ctx->download(pl.data(), ctx->rio.path_len, n) ||
+        !ctx->download(cn.data(), ctx->rio.cs_n, n) || !ctx->sync())
+        return SGUFP_ERR_HIP;
+    for (int k = 0; k < n; k++) {
+        if (path_len) path_len[k] = pl[k];
+        if (cutset_n) cutset_n[k] = (int32_t)cn[k];
+    }
+    return SGUFP_OK;
+}
+
+int sgufp_restricted_paths(sgufp_ctx *ctx, int64_t *path_off, int16_t *paths) {
+    if (!ctx || !ctx->restricted_done || !path_off) return ctx ? SGUFP_ERR_STATE : SGUFP_ERR_ARG;
+    const int n = ctx->n;
+    const int Lcap = ctx->sc.Lcap;
+    std::vector<uint16_t> pl(n);
+    std::vector<int16_t> all((size_t)n * Lcap);
+    if (!ctx->download(pl.data(), ctx->rio.path_len, n) || !ctx->download(all.data(), ctx->rio.path, all.size()) ||
+        !ctx->sync())
+        return SGUFP_ERR_HIP;
+    int64_t o = 0;
+    for (int k = 0; k < n; k++) {
+        path_off[k] = o;
+        if (paths) std::memcpy(paths + o, all.data() + (size_t)k * Lcap, pl[k] * sizeof(int16_t));
+        o += pl[k];
+    }
+    path_off[n] = o;
+    return SGUFP_OK;
+}
+
+// host copies of what the cutset records need: counts, layers, masks, decisions, root solutions
+struct RddCutset {
+    std::vector<uint32_t> n, mask;
+    std::vector<uint16_t> gl, sl, rg;   // cutset layer, root solution length, record layer
+    std::vector<int64_t> so;
+    std::vector<int16_t> dec, sol;
+};
+
+static bool rdd_cutset_download(sgufp_ctx *ctx, RddCutset &c) {
+    const int n = ctx->n, T = ctx->rio.Tcap;
+    c.n.resize(n); c.gl.resize(n); c.sl.resize(n); c.so.resize(n); c.rg.resize(n);
+    c.mask.resize((size_t)n * kRddMax);
+    c.dec.resize((size_t)n * kRddMax * T);
+    if (!ctx->download(c.n.data(), ctx->rio.cs_n, n) || !ctx->download(c.gl.data(), ctx->rio.cs_gl, n) ||
+        !ctx->download(c.sl.data(), ctx->d_sollen, n) || !ctx->download(c.so.data(), ctx->d_soloff, n) ||
+        !ctx->download(c.rg.data(), ctx->d_gl, n) ||
+        !ctx->download(c.mask.data(), ctx->rio.csm, c.mask.size()) ||
+        !ctx->download(c.dec.data(), ctx->rio.csdec, c.dec.size()) || !ctx->sync())
+        return false;
+    size_t tot = 0;
+    for (int k = 0; k < n; k++) tot = std::max(tot, (size_t)(c.so[k] + c.sl[k]));
+    c.sol.resize(tot);
+    return ctx->download(c.sol.data(), ctx->d_sol, tot) && ctx->sync();
+}
+
+int sgufp_restricted_cutset_size(sgufp_ctx *ctx, int64_t *n_records, int64_t *n_states, int64_t *n_sol) {
+    if (!ctx || !ctx->restricted_done) return ctx ? SGUFP_ERR_STATE : SGUFP_ERR_ARG;
+    RddCutset c;
+    if (!rdd_cutset_download(ctx, c)) return SGUFP_ERR_HIP;
+    int64_t nr = 0, ns = 0, nsol = 0;
+    for (int k = 0; k < ctx->n; k++) {
+        nr += c.n[k];
+        const int E = (int)c.gl[k] - (int)c.rg[k];
+        for (uint32_t j = 0; j < c.n[k]; j++) {
+            ns += __builtin_popcount(c.mask[(size_t)k * kRddMax + j]);
+            nsol += c.sl[k] + E;
+        }
+    }
+    if (n_records) *n_records = nr;
+    if (n_states) *n_states = ns;
+    if (n_sol) *n_sol = nsol;
+    return SGUFP_OK;
+}
+
+int sgufp_restricted_cutset(sgufp_ctx *ctx, int64_t *rec_off, uint16_t *gl, double *lb, double *ub,
+                            int64_t *states_off, int16_t *states, int64_t *sol_off, int16_t *sol) {
+    if (!ctx || !ctx->restricted_done) return ctx ? SGUFP_ERR_STATE : SGUFP_ERR_ARG;
+    RddCutset c;
+    if (!rdd_cutset_download(ctx, c)) return SGUFP_ERR_HIP;
+    const Network &net = ctx->net;
+    const int T = ctx->rio.Tcap;
+    int64_t r = 0, ss = 0, so = 0;
+    for (int k = 0; k < ctx->n; k++) {
+        if (rec_off) rec_off[k] = r;
+        const int E = (int)c.gl[k] - (int)c.rg[k];
+        const int u = net.layer_universe[c.gl[k]];
+        for (uint32_t j = 0; j < c.n[k]; j++, r++) {
+            if (gl) gl[r] = c.gl[k];
+            if (lb) lb[r] = -__DBL_MAX__;
+            if (ub) ub[r] = -__DBL_MAX__;
+            if (states_off) states_off[r] = ss;
+            for (uint32_t m = c.mask[(size_t)k * kRddMax + j]; m; m &= m - 1) {
+                if (states) states[ss] = net.sets[u][__builtin_ctz(m)];
+                ss++;
+            }
+            if (sol_off) sol_off[r] = so;
+            if (sol) {
+                std::memcpy(sol + so, c.sol.data() + c.so[k], c.sl[k] * sizeof(int16_t));
+                std::memcpy(sol + so + c.sl[k], c.dec.data() + ((size_t)k * kRddMax + j) * T, (size_t)E * sizeof(int16_t));
+            }
+            so += c.sl[k] + E;
+        }
+    }
+    if (rec_off) rec_off[ctx->n] = r;
+    if (states_off) states_off[r] = ss;
+    if (sol_off) sol_off[r] = so;
     return SGUFP_OK;
 }
 

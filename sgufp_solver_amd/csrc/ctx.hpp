@@ -18,6 +18,7 @@
 #include "dd_device.hpp"
 #include "network.hpp"
 #include "sub_device.hpp"
+#include "rdd_device.hpp"
 
 namespace sgufp {
 // dd_kernels.hip
@@ -35,6 +36,9 @@ hipError_t launch_gather_paths(const BatchOut &, int Lcap, const int32_t *idx, c
                                int16_t *dst, hipStream_t);
 hipError_t launch_push_children(const ChildOut &, const BatchOut &, const int32_t *parents, const int64_t *dst_child,
                                 const int64_t *dst_sol, int n, const FrontierDev &, hipStream_t);
+// rdd_kernels.hip
+size_t rdd_lds_bytes(int Tcap, int Lcap, int us);
+hipError_t launch_restrict(const NetDev &, const BatchIn &, const Pool &, const RddIO &, double, hipStream_t);
 }  // namespace sgufp
 
 using namespace sgufp;
@@ -146,6 +150,12 @@ struct sgufp_ctx {
     bool sub_init();
     bool sub_grow(int n, size_t total);
     bool append_rows(int is_feasibility, int n_cuts, const double *rhs, const std::vector<double> &rows);
+
+    // restricted DD (built on first use)
+    bool rdd_ready = false;
+    bool restricted_done = false;
+    RddIO rio{};
+    bool rdd_init();
 
     bool timing = false;
     hipEvent_t ev[4] = {};

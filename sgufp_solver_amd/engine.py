@@ -30,6 +30,8 @@ EXPORTS = [
     "sgufp_batch_phases", "sgufp_subproblem", "sgufp_subproblem_detail", "sgufp_slot_keys",
     "sgufp_cuts_append_rows", "sgufp_frontier_clear", "sgufp_frontier_size", "sgufp_frontier_push",
     "sgufp_frontier_take_size", "sgufp_frontier_take", "sgufp_bnb_step", "sgufp_cuts_rows",
+    "sgufp_restricted_relax", "sgufp_restricted_results", "sgufp_restricted_paths", "sgufp_restricted_cutset_size",
+    "sgufp_restricted_cutset",
 ]
 
 
@@ -101,6 +103,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.sgufp_frontier_take.argtypes = [P, C.c_int, C.c_int, P, P, P, P, P, P, P]
     lib.sgufp_bnb_step.argtypes = [P, C.c_int, P, P]
     lib.sgufp_cuts_rows.argtypes = [P, C.c_int, C.c_int, C.c_int, P, P]
+    lib.sgufp_restricted_relax.argtypes = [P, C.c_int, C.c_double]
+    lib.sgufp_restricted_results.argtypes = [P, P, P, P, P, P]
+    lib.sgufp_restricted_paths.argtypes = [P, P, P]
+    lib.sgufp_restricted_cutset_size.argtypes = [P, P, P, P]
+    lib.sgufp_restricted_cutset.argtypes = [P, P, P, P, P, P, P, P, P]
     _lib = lib
     return lib
 
@@ -360,6 +367,46 @@ class Engine:
         keys = np.zeros(max(self.info.n_slots, 1), dtype=np.uint64)
         self._check(self.lib.sgufp_slot_keys(self.ctx, _ptr(keys)))
         return keys[:self.info.n_slots]
+
+    def restricted(self, nodes, incumbent: float, width: int = 128):
+        """Inavap::RestrictedDDNew{net, width} for each record under the pool (restricted
+        cut phases of NodeExplorer::processX3, NodeExplorer.cpp:605-656), on the device.
+        Returns per record (status, exact, lb, max path, exact cutset records)."""
+        self.upload(nodes)
+        self._check(self.lib.sgufp_restricted_relax(self.ctx, int(width), C.c_double(incumbent)))
+        n = len(nodes) if not isinstance(nodes, BatchArrays) else nodes.n
+        st = np.zeros(max(n, 1), dtype=np.int32)
+        ex = np.zeros(max(n, 1), dtype=np.uint8)
+        lb = np.zeros(max(n, 1), dtype=np.float64)
+        pl = np.zeros(max(n, 1), dtype=np.int32)
+        cn = np.zeros(max(n, 1), dtype=np.int32)
+        self._check(self.lib.sgufp_restricted_results(self.ctx, _ptr(st), _ptr(ex), _ptr(lb), _ptr(pl), _ptr(cn)))
+        off = np.zeros(n + 1, dtype=np.int64)
+        self._check(self.lib.sgufp_restricted_paths(self.ctx, _ptr(off), None))
+        buf = np.zeros(max(int(off[n]), 1), dtype=np.int16)
+        self._check(self.lib.sgufp_restricted_paths(self.ctx, _ptr(off), _ptr(buf)))
+        nr, ns, nsol = C.c_int64(0), C.c_int64(0), C.c_int64(0)
+        self._check(self.lib.sgufp_restricted_cutset_size(self.ctx, C.byref(nr), C.byref(ns), C.byref(nsol)))
+        R = nr.value
+        roff = np.zeros(n + 1, dtype=np.int64)
+        gl = np.zeros(max(R, 1), dtype=np.uint16)
+        clb = np.zeros(max(R, 1), dtype=np.float64)
+        cub = np.zeros(max(R, 1), dtype=np.float64)
+        soff = np.zeros(R + 1, dtype=np.int64)
+        states = np.zeros(max(ns.value, 1), dtype=np.int16)
+        poff = np.zeros(R + 1, dtype=np.int64)
+        sol = np.zeros(max(nsol.value, 1), dtype=np.int16)
+        self._check(self.lib.sgufp_restricted_cutset(self.ctx, _ptr(roff), _ptr(gl), _ptr(clb), _ptr(cub), _ptr(soff),
+                                                     _ptr(states), _ptr(poff), _ptr(sol)))
+        out = []
+        for k in range(n):
+            kids = []
+            for r in range(int(roff[k]), int(roff[k + 1])):
+                kids.append(NodeRecord(int(gl[r]), float(clb[r]), float(cub[r]),
+                                       [int(x) for x in states[soff[r]:soff[r + 1]]],
+                                       [int(x) for x in sol[poff[r]:poff[r + 1]]]))
+            out.append((int(st[k]), int(ex[k]), float(lb[k]), [int(x) for x in buf[off[k]:off[k + 1]]], kids))
+        return out
 
     def subproblem(self, paths: Sequence[Sequence[int]]):
         """GuroSolver::solveSubProblem for each path on the device.
