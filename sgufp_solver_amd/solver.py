@@ -42,7 +42,8 @@ STEAL_SHARE = 0.4   # PROPORTION_OF_SHARE (DDSolver.h:22-38)
 class DDSolver:
     def __init__(self, network_path: Optional[str] = None, n_workers: int = 1, device: int = 0,
                  max_batch: int = 4096, batch_nodes: int = 0, engine=None, group=None, verbose: bool = True,
-                 progress: float = 0.0, max_rounds: int = 0, dive_batch: int = 64, time_budget: float = 0.0):
+                 progress: float = 0.0, max_rounds: int = 0, dive_batch: int = 64, time_budget: float = 0.0,
+                 restricted_width: int = 0):
         """n_workers is accepted for API compatibility with the reference (threads there);
         the parallelism here is the batch of ``batch_nodes`` (<= max_batch) records per
         round and one rank per GPU."""
@@ -65,6 +66,11 @@ class DDSolver:
         # stop after this many seconds (0: none) with complete = False -- for throughput
         # measurements of searches that would run for hours
         self.time_budget = time_budget
+        # primal heuristic (0: off): before the search, the restricted-DD half of
+        # NodeExplorer::processX3 (NodeExplorer.cpp:605-796) on the root record seeds the
+        # incumbent with the value of the routing its refinement loop converges to
+        self.restricted_width = restricted_width
+        self.heuristic_incumbent = None
         self.complete = False
         self.counters = {}
         self.rounds = 0
@@ -140,6 +146,11 @@ class DDSolver:
         if rank == 0:
             eng.frontier_push([NodeRecord(0, DOUBLE_MIN, DOUBLE_MAX, [], [])])
         z = float(known_optimal)
+        if self.restricted_width > 0 and rank == 0:
+            from .restricted import RestrictedExplorer
+            h = RestrictedExplorer(eng, self.restricted_width).incumbent([NodeRecord(0, DOUBLE_MIN, DOUBLE_MAX, [], [])], z)
+            self.heuristic_incumbent = h
+            z = max(z, h)
         marks = {1: eng.cuts_count(1), 0: eng.cuts_count(0)}
         keys = ("popped", "relaxed", "pruned_bound", "pruned_feasibility", "pruned_optimality", "exact",
                 "exact_closed", "subproblems", "new_feasibility_cuts", "new_optimality_cuts", "children", "pushed")

@@ -69,3 +69,42 @@ def test_restricted_matches_reference(name, run):
                 bad.append(f"node {k}: cutset record differs: {a} vs {b}")
                 break
     assert not bad, "\n".join(bad[:10])
+
+
+# ------------------------------------------------------------------ primal heuristic (GPU)
+HEUR = [("T1", 2, 3), ("T2", 1, 1), ("T3", 2, 3), ("T4", 3, 3)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,seed,S", HEUR, ids=[f"{c}-{s}-{S}" for c, s, S in HEUR])
+def test_restricted_heuristic_incumbent_is_a_feasible_value(cfg, seed, S):
+    """processX3's restricted refinement on the root record: a converged bound is the value
+    of its routing (the subproblem's mean objective at the final path, 1e-9 relative), never
+    above the extensive-form optimum (1e-5, main.cpp:43,76), and seeding the DDSolver with it
+    leaves the optimum unchanged."""
+    import tempfile
+    from oracle import extensive_form as ef
+    from sgufp_solver_amd import engine as E
+    from sgufp_solver_amd import instance
+    from sgufp_solver_amd.pools import DOUBLE_MAX, DOUBLE_MIN, NodeRecord
+    from sgufp_solver_amd.restricted import RestrictedExplorer
+    from sgufp_solver_amd.solver import DDSolver
+    inst = instance.generate(instance.CONFIGS[cfg], seed, scenarios=S)
+    inst.lb[:] = 0
+    d = tempfile.mkdtemp(prefix="sgufp_rh_")
+    path = os.path.join(d, "net.txt")
+    inst.write(path)
+    opt = ef.solve(inst)
+    eng = E.Engine(path, 0, 64)
+    res = RestrictedExplorer(eng, 128).explore([NodeRecord(0, DOUBLE_MIN, DOUBLE_MAX, [], [])], DOUBLE_MIN)[0]
+    assert res.status == 0 and res.converged, (res.status, res.iterations)
+    typ, rhs, rows, obj_mean = eng.subproblem([res.path])
+    eng.close()
+    assert typ[0] == 0
+    assert abs(res.lb - obj_mean[0]) <= 1e-9 * max(1.0, abs(obj_mean[0])), (res.lb, obj_mean[0])
+    assert res.lb <= opt + 1e-5 * max(1.0, abs(opt)), (res.lb, opt)
+    solver = DDSolver(path, max_batch=1024, max_rounds=20000, verbose=False, restricted_width=128)
+    sol, _ = solver.start(DOUBLE_MIN)
+    solver.eng.close()
+    assert solver.heuristic_incumbent == res.lb
+    assert abs(sol - opt) <= 1e-5 * max(1.0, abs(opt)), (sol, opt)
