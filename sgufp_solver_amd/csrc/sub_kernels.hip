@@ -218,9 +218,12 @@ __device__ __forceinline__ void load_chain_regs(const SubLds &W, int n, int nct,
 // previous group's atomic minima (a pass that changes nothing read only settled keys, so
 // convergence never depends on that ordering).  The fixed point -- the shortest (cost,
 // hops) keys -- is unique, so the order changes only how many passes it takes; the caller
-// iterates until a pass changes nothing.
-__device__ inline uint32_t bf_pass(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M,
-                                   const ChainRegs &C) {
+// iterates until a forward and a backward sweep in a row (either order) change nothing:
+// then every residual arc is settled on the same keys.  `forward` picks the half: the Z
+// arcs out of Z_out / Z and the forward residual arcs, then the arcs into Z_in / Z; or the
+// backward residual arcs.
+__device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M,
+                                    const ChainRegs &C, bool forward) {
     uint32_t changed = 0;
     auto relax = [&](int v, int64_t nk) {
         if (nk < W.key[v]) {
@@ -243,6 +246,22 @@ __device__ inline uint32_t bf_pass(const SubNet &N, const SubLds &W, int nct, in
         }
     };
     const int n = N.n;
+    const int G = (nct + kWave - 1) / kWave;
+    if (!forward) {
+        for (int g = G - 1; g >= kRegGroups; g--) {
+            const int k = g * kWave + lane();
+            uint64_t ca = 0, cb = 0;
+            if (k < nct) { ca = W.cta[k]; cb = W.ctb[k]; }
+            const ChainArcs c = chain_arcs(ca, cb, k < nct, n, mode, M);
+            arc(c.th, c.wb, c.bwd, false);
+        }
+#pragma unroll
+        for (int g = kRegGroups - 1; g >= 0; g--) {
+            if (g >= G) continue;
+            arc(C.th[g], C.wb[g], (C.bmask >> g) & 1u, false);
+        }
+        return changed;
+    }
     // Z_out -> sources (SSP) / Z -> every free node (potentials), cost 0
     {
         const int64_t kz = W.key[n];
@@ -253,7 +272,6 @@ __device__ inline uint32_t bf_pass(const SubNet &N, const SubLds &W, int nct, in
             }
     }
     wave_lds_sync();
-    const int G = (nct + kWave - 1) / kWave;
 #pragma unroll
     for (int g = 0; g < kRegGroups; g++) {
         if (g >= G) break;
@@ -275,20 +293,25 @@ __device__ inline uint32_t bf_pass(const SubNet &N, const SubLds &W, int nct, in
         if (mode == kSsp) { if ((e >> 29) & 1u) relax(n + 1, kv + 1); }
         else relax(n, kv + 1);
     }
-    wave_lds_sync();
-    for (int g = G - 1; g >= kRegGroups; g--) {
-        const int k = g * kWave + lane();
-        uint64_t ca = 0, cb = 0;
-        if (k < nct) { ca = W.cta[k]; cb = W.ctb[k]; }
-        const ChainArcs c = chain_arcs(ca, cb, k < nct, n, mode, M);
-        arc(c.th, c.wb, c.bwd, false);
-    }
-#pragma unroll
-    for (int g = kRegGroups - 1; g >= 0; g--) {
-        if (g >= G) continue;
-        arc(C.th[g], C.wb[g], (C.bmask >> g) & 1u, false);
-    }
     return changed;
+}
+
+// Iterate sweeps, forward and backward alternating, to the fixed point (false: not within
+// the pass bound).
+__device__ inline bool bf_converge(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M,
+                                   const ChainRegs &C) {
+    bool prev_quiet = false;   // the sweep before the current one changed nothing
+    for (int it = 0; it < 2 * (N.n + 4); it++) {
+#ifdef SGUFP_SUB_TRACE
+        if (lane() == 0 && !(it & 1)) W.misc[5]++;
+#endif
+        const uint32_t changed = bf_sweep(N, W, nct, nz, mode, M, C, !(it & 1));
+        wave_lds_sync();
+        const bool quiet = !wave_or(changed);
+        if (quiet && prev_quiet) return true;
+        prev_quiet = quiet;
+    }
+    return false;
 }
 
 // Predecessors of the SSP labels: the smallest arc code among the residual arcs into each
@@ -316,15 +339,7 @@ __device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, i
     ChainRegs C;
     load_chain_regs(W, N.n, nct, mode, M, C);
     wave_lds_sync();
-    bool converged = false;
-    for (int it = 0; it < nn + 2; it++) {
-#ifdef SGUFP_SUB_TRACE
-        if (lane() == 0) W.misc[5]++;
-#endif
-        const uint32_t changed = bf_pass(N, W, nct, nz, mode, M, C);
-        wave_lds_sync();
-        if (!wave_or(changed)) { converged = true; break; }
-    }
+    const bool converged = bf_converge(N, W, nct, nz, mode, M, C);
     if (mode != kSsp || !converged) return converged;
 #ifdef SGUFP_SUB_VERIFY
     // Debug build: the labels a warm start converged to must equal those of a cold
@@ -335,12 +350,7 @@ __device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, i
             W.key[v] = (v == N.n) ? 0 : kInf;
         }
         wave_lds_sync();
-        bool cold_ok = false;
-        for (int it = 0; it < nn + 2; it++) {
-            const uint32_t changed = bf_pass(N, W, nct, nz, mode, M, C);
-            wave_lds_sync();
-            if (!wave_or(changed)) { cold_ok = true; break; }
-        }
+        const bool cold_ok = bf_converge(N, W, nct, nz, mode, M, C);
         uint32_t diff = cold_ok ? 0u : 1u;
         for (int v = lane(); v < nn; v += kWave) diff |= (W.vkey[v] != W.key[v]) ? 1u : 0u;
         if (wave_or(diff) && lane() == 0) W.misc[6] = 1;
