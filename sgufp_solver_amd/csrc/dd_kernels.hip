@@ -122,6 +122,19 @@ constexpr uint16_t kMirParent = 127, kMirRankShift = 7, kMirAlive = 1u << 12, kM
 // layers are two contiguous segments that the narrow sweep stages into LDS ahead of use.
 // ntopo / nflag / atopo / aflag stay the master copy; every edit of a narrow node / arc
 // flag is applied to both.
+// Parent slot / rank field of a packed topology word as single bit-field instructions (the
+// compiler's shift-then-mask canonical form costs a third instruction per address).
+static_assert(kMirParent == 127 && kMirRankShift == 7, "mir_parent / mir_rank encode the field positions");
+__device__ __forceinline__ uint32_t mir_parent(uint32_t w) {
+    uint32_t r;
+    asm("v_and_b32 %0, 0x7f, %1" : "=v"(r) : "v"(w));
+    return r;
+}
+__device__ __forceinline__ uint32_t mir_rank(uint32_t w) {
+    uint32_t r;
+    asm("v_bfe_u32 %0, %1, 7, 5" : "=v"(r) : "v"(w));
+    return r;
+}
 __device__ __forceinline__ void mir_node_clear(DD &d, uint32_t node, uint16_t bits) {
     if (d.stream && node < d.Nn) d.tmir[node] &= (uint16_t)~bits;
 }
@@ -922,11 +935,11 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
     auto issue = [&](int k0g, int k1g, int lw0) {
         const uint32_t n0 = rl(m_noff, k0g - lw0), nN = rl(m_noff, k1g - lw0) - n0;
         const uint32_t a0 = rl(m_aoff, k0g - lw0), nA = rl(m_aoff, k1g - lw0) - a0;
+        // entries past the group load the group's last layer again (never read): no branch
 #pragma unroll
         for (int jj = 0; jj < PC; jj++) {
-            const int k = k0g + c_lo[jj];
-            const bool ok = k < k1g;
-            pf[jj] = pool.coefT[ok ? (size_t)c_off[jj] + (size_t)(d.g + k - 1) * us : 0];
+            const int k = min(k0g + c_lo[jj], k1g - 1);
+            pf[jj] = pool.coefT[(size_t)c_off[jj] + (size_t)(uint32_t)((d.g + k - 1) * us)];
         }
 #pragma unroll
         for (int jj = 0; jj < PT; jj++) {
@@ -948,24 +961,24 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
     // layer kb (the deletion cascade removes childless parents), so the width-1 summaries
     // and walk state2 of the inner layers are written on the way (lanes that share an
     // ancestor write the same value; items past the layer repeat its last node).
-    auto fold_run = [&](auto Dc, int ka, int slot_, int k0_, uint32_t gn0_) {
+    auto fold_run = [&](auto Dc, int ka, int slot_, int k0_, int kw_, uint32_t gn0_) {
         constexpr int D = decltype(Dc)::value;
         const int kb = ka + D - 1;
         const LDS uint16_t *tr = bv.tring + (size_t)slot_ * kTopoEntries;
-        const LDS double *ring = bv.cring + (size_t)slot_ * kStageEntries;
+        const LDS double *ring_c = bv.cring + (size_t)slot_ * kStageEntries + c * us;
         const LDS double *pb = bv.vb + (size_t)((ka - 1) & 1) * kLdsBatchWidth * CB;
         LDS double *ob = bv.vb + (size_t)(kb & 1) * kLdsBatchWidth * CB;
-        const int l0 = ka - k0_;
+        const int l0 = ka - k0_, lw = ka - kw_;   // ring / metadata-window positions
         uint32_t ebase[D], nofs[D];
         bool w1s[D], wrs[D];
 #pragma unroll
         for (int s = 0; s < D; s++) {
-            nofs[s] = rl(m_noff, l0 + s);
+            nofs[s] = rl(m_noff, lw + s);
             ebase[s] = nofs[s] - gn0_;
-            w1s[s] = (rl(m_pk, l0 + s) >> 31) != 0;
-            wrs[s] = ((rl(m_pk, l0 + s) >> 30) & 1u) != 0;
+            w1s[s] = (rl(m_pk, lw + s) >> 31) != 0;
+            wrs[s] = ((rl(m_pk, lw + s) >> 30) & 1u) != 0;
         }
-        const uint32_t nlast = rl(m_pk, l0 + D - 1) & 255u;
+        const uint32_t nlast = rl(m_pk, lw + D - 1) & 255u;
         const bool wlane = c == nb - 1;   // the lane whose cut's state2 the path walks read
         auto items = [&](auto Uc, uint32_t base) {
             constexpr int U = decltype(Uc)::value;
@@ -984,7 +997,7 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     wl[u][s] = w[u] | (cur[u] << 16);
-                    cur[u] = w[u] & kMirParent;
+                    cur[u] = mir_parent(w[u]);
                 }
             }
             double x[U], cf[U][D];
@@ -993,7 +1006,7 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
                 x[u] = pb[cur[u] * CB + c];
 #pragma unroll
                 for (int s = 0; s < D; s++)
-                    cf[u][s] = ring[(size_t)(l0 + s) * per_layer + c * us + ((wl[u][s] >> kMirRankShift) & 31u)];
+                    cf[u][s] = ring_c[(size_t)(l0 + s) * per_layer + mir_rank(wl[u][s])];
             }
             sched_fence();
 #pragma unroll
@@ -1021,55 +1034,77 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
             for (uint32_t base = 0; base < nlast; base += 2 * G) items(std::integral_constant<int, 2>{}, base);
     };
 
+    // the metadata window (base kw) is reloaded only when the next group's prefetch would
+    // leave it (groups are a few layers, the window 64)
     int j = 0, slot = 0;
     int k0 = uni((int)d.gstart[0]), k1 = uni((int)d.gstart[1]);
-    load_meta(k0);
-    issue(k0, k1, k0);
+    int kw = k0;
+    load_meta(kw);
+    issue(k0, k1, kw);
     commit(0);
-    if (d.ng > 1) issue(k1, uni((int)d.gstart[2]), k0);
-    uint32_t gn0 = rl(m_noff, 0), gnN = rl(m_noff, k1 - k0) - gn0, ga0 = rl(m_aoff, 0);
+    if (d.ng > 1) issue(k1, uni((int)d.gstart[2]), kw);
+    uint32_t gn0 = rl(m_noff, 0), gnN = rl(m_noff, k1 - kw) - gn0, ga0 = rl(m_aoff, 0);
     wave_lds_sync();
     for (int k = 1; k < d.kg;) {
         if (k == k1) {
+#ifdef SGUFP_PROF
+            const uint64_t t_sw = wall_clock64();
+#endif
             // next group: its words and coefficients were issued one group ago
             j++;
             slot ^= 1;
             commit(slot);
+#ifdef SGUFP_PROF_COMMIT
+            bv.prof[1] += wall_clock64() - t_sw;
+#endif
             k0 = k1;
             k1 = uni((int)d.gstart[j + 1]);
-            load_meta(k0);
-            if (j + 1 < d.ng) issue(k1, uni((int)d.gstart[j + 2]), k0);
-            gn0 = rl(m_noff, 0);
-            gnN = rl(m_noff, k1 - k0) - gn0;
-            ga0 = rl(m_aoff, 0);
+            const int k2 = j + 1 < d.ng ? uni((int)d.gstart[j + 2]) : k1;
+            if (k2 - kw >= kWave) {
+                kw = k0;
+                load_meta(kw);
+            }
+            if (j + 1 < d.ng) issue(k1, k2, kw);
+            gn0 = rl(m_noff, k0 - kw);
+            gnN = rl(m_noff, k1 - kw) - gn0;
+            ga0 = rl(m_aoff, k0 - kw);
             wave_lds_sync();
+#ifdef SGUFP_PROF
+            bv.prof[0] += wall_clock64() - t_sw;
+#endif
         }
-        const int l = k - k0;
+        const int l = k - k0, lm = k - kw;
         const LDS double *coefk = bv.cring + (size_t)slot * kStageEntries + (size_t)l * per_layer;
         const LDS uint16_t *tr = bv.tring + (size_t)slot * kTopoEntries;
-        const uint32_t pk = rl(m_pk, l);
-        const uint32_t noff = rl(m_noff, l), acnt = (pk >> 8) & 0xFFFu;
+        const uint32_t pk = rl(m_pk, lm);
+        const uint32_t noff = rl(m_noff, lm), acnt = (pk >> 8) & 0xFFFu;
         const LDS double *pbuf = bv.vb + (size_t)((k - 1) & 1) * kLdsBatchWidth * CB;
         LDS double *cbuf = bv.vb + (size_t)(k & 1) * kLdsBatchWidth * CB;
         const bool w1 = (pk >> 31) != 0;
         if (acnt) {
+#ifdef SGUFP_PROF
+            const uint64_t t_m = wall_clock64();
+#endif
             // state2 of the last batch cut: only what a path walk reads (merged nodes and
             // their parents) unless every layer is asked for (kS = T: the exact redo)
             const bool wr = ((pk >> 30) & 1u) != 0;
-            const uint32_t aoff = rl(m_aoff, l);
+            const uint32_t aoff = rl(m_aoff, lm);
             const uint32_t ebase = gnN + (aoff - ga0);   // ring entry of the layer's first arc
             auto word = [&](uint32_t e) -> uint32_t { return (uint32_t)tr[e]; };
             // U independent items per lane per step (U sized to the layer): all topology
             // words first, then all parent values / coefficients, so one step costs two LDS
             // round trips and a narrow layer runs no idle unrolled items.
+            // Full steps (every item inside the layer) index the ring with immediate offsets;
+            // only the last step clamps.
             auto dispatch = [&](uint32_t count, auto &&step) {
                 uint32_t base = 0;
-                for (; count - base > (uint32_t)G * 8; base += G * 8) step(std::integral_constant<int, 8>{}, base);
+                for (; count - base > (uint32_t)G * 8; base += G * 8)
+                    step(std::integral_constant<int, 8>{}, std::false_type{}, base);
                 const uint32_t per = (count - base + G - 1) / G;
-                if (per <= 1) step(std::integral_constant<int, 1>{}, base);
-                else if (per <= 2) step(std::integral_constant<int, 2>{}, base);
-                else if (per <= 4) step(std::integral_constant<int, 4>{}, base);
-                else step(std::integral_constant<int, 8>{}, base);
+                if (per <= 1) step(std::integral_constant<int, 1>{}, std::true_type{}, base);
+                else if (per <= 2) step(std::integral_constant<int, 2>{}, std::true_type{}, base);
+                else if (per <= 4) step(std::integral_constant<int, 4>{}, std::true_type{}, base);
+                else step(std::integral_constant<int, 8>{}, std::true_type{}, base);
             };
             // Fast path: a plain max / min over the candidates parent + coefficient.  Dead
             // arcs carry parent slot 127 (kNarrowMax), whose value is a quiet NaN that
@@ -1081,20 +1116,27 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
             // with the exact pick below.
             double mx = -INFINITY, xmin = INFINITY;
             const uint32_t alast = acnt - 1u;
-            dispatch(acnt, [&](auto Uc, uint32_t base) {
+            const LDS double *pbc = pbuf + c, *cfc = coefk + c * us;
+            dispatch(acnt, [&](auto Uc, auto Cc, uint32_t base) {
                 constexpr int U = decltype(Uc)::value;
+                constexpr bool CLAMP = decltype(Cc)::value;
                 uint32_t wd[U];
+                const LDS uint16_t *tw = tr + ebase + base + grp;
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    const uint32_t a = base + (uint32_t)(u * G + grp);
-                    wd[u] = word(ebase + (a < alast ? a : alast));
+                    if (CLAMP) {
+                        const uint32_t a = base + (uint32_t)(u * G + grp);
+                        wd[u] = word(ebase + (a < alast ? a : alast));
+                    } else {
+                        wd[u] = (uint32_t)tw[u * G];
+                    }
                 }
                 sched_fence();
                 double px[U], cf[U];
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    px[u] = pbuf[(wd[u] & kMirParent) * CB + c];
-                    cf[u] = coefk[c * us + ((wd[u] >> kMirRankShift) & 31u)];
+                    px[u] = pbc[mir_parent(wd[u]) * CB];
+                    cf[u] = cfc[mir_rank(wd[u])];
                 }
                 sched_fence();
 #pragma unroll
@@ -1111,7 +1153,7 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
             VP best{mx, any ? 0 : INT_MIN};
             if (__ballot(mx == 0.0) != 0) {
                 best = VP{0.0, INT_MIN};
-                dispatch(acnt, [&](auto Uc, uint32_t base) {
+                dispatch(acnt, [&](auto Uc, auto, uint32_t base) {
                     constexpr int U = decltype(Uc)::value;
 #pragma unroll
                     for (int u = 0; u < U; u++) {
@@ -1141,6 +1183,9 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
                 }
             }
             wave_lds_sync();
+#ifdef SGUFP_PROF
+            bv.prof[1] += wall_clock64() - t_m;
+#endif
             k++;
             continue;
         }
@@ -1149,14 +1194,14 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
         int kb = min(min(k1, d.kg) - 1, k + kMaxRun - 1);
         {
             const int span = kb - k + 1;
-            const uint64_t b = (mmask >> l) & ((1ull << span) - 1ull);
+            const uint64_t b = (mmask >> lm) & ((1ull << span) - 1ull);
             if (b) kb = k + (int)(__ffsll((unsigned long long)b) - 1) - 1;
             if (((kb - k) & 1) != 0) kb--;
         }
         switch (kb - k) {
-            case 0: fold_run(std::integral_constant<int, 1>{}, k, slot, k0, gn0); break;
-            case 2: fold_run(std::integral_constant<int, 3>{}, k, slot, k0, gn0); break;
-            default: fold_run(std::integral_constant<int, 5>{}, k, slot, k0, gn0); break;
+            case 0: fold_run(std::integral_constant<int, 1>{}, k, slot, k0, kw, gn0); break;
+            case 2: fold_run(std::integral_constant<int, 3>{}, k, slot, k0, kw, gn0); break;
+            default: fold_run(std::integral_constant<int, 5>{}, k, slot, k0, kw, gn0); break;
         }
         wave_lds_sync();
         k = kb + 1;

@@ -9,7 +9,7 @@ OUT=sgufp_solver_amd/lib_var/$NAME
 mkdir -p $OUT/obj
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Iinclude -Isgufp_solver_amd/csrc $*"
 /opt/rocm/bin/hipcc $FLAGS -x hip -c $SRC -o $OUT/obj/dd.o
-for f in sub_kernels.hip bnb_kernels.hip capi.cpp bnb.cpp network.cpp; do
+for f in sub_kernels.hip bnb_kernels.hip rdd_kernels.hip capi.cpp bnb.cpp network.cpp; do
   cp sgufp_solver_amd/lib/obj/$f.o $OUT/obj/$f.o
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libsgufp_hip.so $OUT/obj/*.o
