@@ -1012,20 +1012,32 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const bool alive = (wl[u][D - 1] & kMirAlive) != 0;
-                double xv = x[u];
+                double xv = x[u], xs[D], xms[D];
 #pragma unroll
                 for (int s = 0; s < D; s++) {
                     const uint32_t w = wl[u][s];
                     const bool in = (w & kMirIn) != 0, reg = (w & (31u << kMirRankShift)) != 0;
                     const double xn = !in ? DMIN : (reg ? xv + cf[u][s] : xv);
-                    if (alive && w1s[s] && cv) {
-                        bv.sm[(size_t)(ka + s) * CB + c] = xn;
-                        bv.xm[(size_t)(ka + s) * CB + c] = !in ? DMAX : (reg ? xn : xv + 0.0);
-                    }
-                    xv = xn;
-                    if (alive && wrs[s] && wlane) d.s2[nofs[s] + (w >> 16)] = xv;
+                    xms[s] = !in ? DMAX : (reg ? xn : xv + 0.0);
+                    xs[s] = xv = xn;
                 }
                 ob[(wl[u][D - 1] >> 16) * CB + c] = xv;
+                // the summaries / walk values of the run's layers: one divergent branch per
+                // item (the per-layer conditions are wave-uniform)
+                if (alive && cv) {
+#pragma unroll
+                    for (int s = 0; s < D; s++) {
+                        if (w1s[s]) {
+                            bv.sm[(size_t)(ka + s) * CB + c] = xs[s];
+                            bv.xm[(size_t)(ka + s) * CB + c] = xms[s];
+                        }
+                    }
+                    if (wlane) {
+#pragma unroll
+                        for (int s = 0; s < D; s++)
+                            if (wrs[s]) d.s2[nofs[s] + (wl[u][s] >> 16)] = xs[s];
+                    }
+                }
             }
         };
         const uint32_t per = (nlast + G - 1) / G;
