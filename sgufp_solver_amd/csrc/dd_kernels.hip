@@ -866,7 +866,7 @@ __device__ __forceinline__ void batch_coef_direct(const NetDev &net, const DD &d
 // read no state2.
 template <int CB>
 __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int nb,
-                                             double rv, int kS) {
+                                             double rv, int kS, int kend = INT_MAX) {
     constexpr int G = kWave / CB;
     constexpr int PC = kStageEntries / kWave, PT = kTopoEntries / kWave;
     const int c = lane() % CB, grp = lane() / CB;
@@ -1057,7 +1057,8 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
     if (d.ng > 1) issue(k1, uni((int)d.gstart[2]), kw);
     uint32_t gn0 = rl(m_noff, 0), gnN = rl(m_noff, k1 - kw) - gn0, ga0 = rl(m_aoff, 0);
     wave_lds_sync();
-    for (int k = 1; k < d.kg;) {
+    const int ke = min(d.kg, kend);   // layers >= kend are not needed (exact redo)
+    for (int k = 1; k < ke;) {
         if (k == k1) {
 #ifdef SGUFP_PROF
             const uint64_t t_sw = wall_clock64();
@@ -1203,7 +1204,7 @@ __device__ __forceinline__ void sweep_narrow(const NetDev &net, DD &d, BatchView
         }
         // A run of exact (tree) layers [k, kb] inside the staging group, ended by the next
         // merged layer; odd depth (see fold_run).
-        int kb = min(min(k1, d.kg) - 1, k + kMaxRun - 1);
+        int kb = min(min(k1, ke) - 1, k + kMaxRun - 1);
         {
             const int span = kb - k + 1;
             const uint64_t b = (mmask >> lm) & ((1ull << span) - 1ull);
@@ -1953,7 +1954,8 @@ __device__ __forceinline__ bool fire_layers(const DD &d, BatchView &bv, int c, i
 // when a width-1 layer would lose all of its incoming arcs.
 template <int CB>
 __device__ __forceinline__ bool redo_cut(const NetDev &net, DD &d, BatchView &bv, const Pool &pool, int c, int id,
-                                         double rv1, int first, int end, double thresh, double maxState) {
+                                         double rv1, int first, int end, double thresh, double maxState,
+                                         bool unchanged) {
     const int last = d.T - 1;
     const int nw = (d.T + 63) / 64;
     fire_layers<CB>(d, bv, c, first, end, thresh, maxState);
@@ -1964,6 +1966,22 @@ __device__ __forceinline__ bool redo_cut(const NetDev &net, DD &d, BatchView &bv
     if (lane() == 0) bv.ids[0] = id;
     for (int k = lane(); k < d.T; k += kWave) bv.w1[k] = ((d.nalive[k]) == 1) ? 1 : 0;
     wave_lds_sync();
+    if (unchanged) {
+        // no edit since the batch sweep: the fresh summaries equal the batch ones, so the
+        // fire mask stands and the sweep stops after the last layer it writes
+        int kend = 0;
+        for (int w = 0; w < nw; w++) {
+            const uint64_t m = bv.wm[w];
+            if (m) kend = w * 64 + 64 - (int)__clzll((long long)m);
+        }
+        bv.wsel = bv.wm;
+        sweep_narrow<CB>(net, d, bv, pool, 1, rv1, d.T, kend);
+        if (d.kg == 0 && lane() == 0) bv.s2b[0] = rv1;
+        for (int k = max(d.kg, 1); k < min(last, kend); k++) sweep_tail_layer<CB>(net, d, bv, pool, k, 1, d.T);
+        bv.wsel = nullptr;
+        wave_mem_sync();
+        return prune_layers<CB>(net, d, bv, pool, id, first, end, maxState, thresh);
+    }
     for (int attempt = 0; attempt < 2; attempt++) {
         bv.wsel = bv.wm;
         sweep_narrow<CB>(net, d, bv, pool, 1, rv1, d.T);
@@ -2161,6 +2179,7 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
             double mstate[CB];
             f_leaf_scan<CB>(d, bv, pool, nb, kS, rm, mstate);
             st.stamp(3);
+            bool removed = false;   // some batch cut so far removed leaves (the DD changed)
             for (int c = 0; c < nb; c++) {
                 const int seq = s + c;
                 const int id = uni(bv.ids[c]);
@@ -2173,10 +2192,10 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
 #pragma unroll
                 for (int cc = 0; cc < CB; cc++) rmc = (cc == c) ? rm[cc] : rmc;
                 if (rmc == uni(d.nalive[last])) { st.status = kPrunedFeasibility; return; }
-                if (rmc) dd_cascade(d, (uint32_t)c + 1u);
+                if (rmc) { dd_cascade(d, (uint32_t)c + 1u); removed = true; }
                 if (!d.exact && dd_prune_check<CB>(d, bv, c, 1, last, -0.01, maxState)) {
                     st.stamp(4);
-                    if (!redo_cut<CB>(net, d, bv, pool, c, id, lane_get(rv, c), 1, last, -0.01, maxState)) {
+                    if (!redo_cut<CB>(net, d, bv, pool, c, id, lane_get(rv, c), 1, last, -0.01, maxState, !removed)) {
                         st.status = kPrunedFeasibility;
                         return;
                     }
@@ -2231,7 +2250,7 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
                 const int c = redo;
                 const int id = uni(bv.ids[c]);
                 double v = redo_v;
-                if (!redo_cut<CB>(net, d, bv, pool, c, id, lane_get(rv, c), 3, last - 1, incumbent - 0.01, redo_ms))
+                if (!redo_cut<CB>(net, d, bv, pool, c, id, lane_get(rv, c), 3, last - 1, incumbent - 0.01, redo_ms, true))
                     v = DMIN;
                 st.applied++;
                 st.last_cut = id;
