@@ -309,6 +309,10 @@ def main():
             # is limited by instruction issue and LDS latency, not by HBM
             "bound": "hbm",
             "limiter": "latency/issue (measured HBM traffic is a fraction of the algorithmic bytes)",
+            # SURVEY 8(d)'s byte model streams every (arc, cut) operand from HBM; the kernel
+            # serves most of them from LDS / L2 (topology staged once per cut batch), so the
+            # model's rate can pass the HBM peak -- frac_traffic is the measured utilisation
+            "byte_model": "SURVEY 8(d): 6A + sum over applied cuts (14A + 8N) + records; not HBM traffic",
             "kernel": "k_relax",
             "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBPS,
