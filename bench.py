@@ -78,11 +78,16 @@ def lib_sha256() -> str:
 FETCH_CORRECTION = 2.0
 
 
-def pmc_traffic(tag: str, kernel: str = "k_relax"):
+def workload_key(args) -> str:
+    """The bench workload a PMC profile belongs to (profiles/<tag>_pmc_*/workload.txt)."""
+    return f"{args.config}:seed{args.seed}:nodes{args.nodes}:pool{args.n_feas}F+{args.n_opt}O"
+
+
+def pmc_traffic(tag: str, workload: str, kernel: str = "k_relax"):
     """(HBM bytes per launch of `kernel`, source) from the rocprofv3 --pmc CSVs of the same
     bench command (profiles/<tag>_pmc_fetch/*counter_collection.csv, profiles/<tag>_pmc_write/...),
-    only when they were collected with this very library (lib.sha256 next to the CSVs);
-    otherwise (None, reason).  FETCH_SIZE x FETCH_CORRECTION + WRITE_SIZE; both count the
+    only when they were collected with this very library (lib.sha256 next to the CSVs) on
+    this very workload (workload.txt); otherwise (None, reason).  FETCH_SIZE x FETCH_CORRECTION + WRITE_SIZE; both count the
     L2's fabric-side requests (Infinity-Cache hits included), so this is L2-miss traffic."""
     want = lib_sha256()
     for sub in ("pmc_fetch", "pmc_write"):
@@ -92,6 +97,12 @@ def pmc_traffic(tag: str, kernel: str = "k_relax"):
         with open(shafile) as fh:
             if fh.read().strip() != want:
                 return None, f"profiles/{tag}_{sub} was collected with another build of libsgufp_hip.so"
+        wfile = os.path.join(ROOT, "profiles", f"{tag}_{sub}", "workload.txt")
+        if not os.path.exists(wfile):
+            return None, f"profiles/{tag}_{sub}/workload.txt missing"
+        with open(wfile) as fh:
+            if fh.read().strip() != workload:
+                return None, f"profiles/{tag}_{sub} was collected on another workload"
     def load(pattern, counter):
         # only the bench launches (largest grid): the 1024-node probe launch is excluded
         rows = []
@@ -275,7 +286,7 @@ def main():
     r_out = float(np.sum(2 * ch.gl.astype(np.float64) + 2 * np.diff(ch.states_off) + 24)) if ch.n else 0.0
     t_relax = float(np.mean(relax_ms)) / 1e3
     achieved = bytes_relax / t_relax / 1e9
-    traffic, traffic_src = pmc_traffic(args.profile_tag)
+    traffic, traffic_src = pmc_traffic(args.profile_tag, workload_key(args))
 
     total_nodes = mine.n * world
     value = total_nodes * args.steps / elapsed
