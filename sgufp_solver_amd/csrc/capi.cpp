@@ -581,6 +581,14 @@ bool sgufp_ctx::sub_init() {
         !sync())
         return false;
     sn.n = n; sn.m = m; sn.S = S; sn.L = N.L; sn.n_slots = N.n_slots; sn.nz = nz; sn.zlist = d_z; sn.arc_topo = d_topo;
+    {
+        // every arc sits in one chain, so M = 1 + sum_chains 2 |R| (U + 1) (k_sub_scenario)
+        // is at most 1 + 2 sum_a |r_a| (max u + 1); residual costs are below R + M <= 2 M
+        int64_t sr = 0, umax = 0;
+        for (int a = 0; a < m; a++) sr += std::abs((int64_t)rew[a]);
+        for (size_t i = 0; i < ub.size(); i++) umax = std::max<int64_t>(umax, ub[i]);
+        sn.cost_bound = 2 * (1 + 2 * sr * (umax + 1));
+    }
     sn.tail = d_tail; sn.head = d_head; sn.vbar = d_vb; sn.inner = d_inner; sn.arc_layer = d_layer;
     sn.lb = d_lb; sn.ub = d_ub; sn.reward = d_rew;
     sn.in_off = d_ioff; sn.in_list = d_il; sn.out_off = d_ooff; sn.out_list = d_ol;

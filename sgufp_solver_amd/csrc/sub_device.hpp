@@ -17,6 +17,8 @@ enum SubStatus : int32_t {
 
 struct SubNet {
     int n, m, S, L, n_slots, nz;
+    int64_t cost_bound;                  // bound on |residual costs| incl. big-M: 2 M with
+                                         // M <= 1 + 2 sum_a |r_a| (max u + 1) (host)
     const int32_t SGUFP_GBL *tail;       // [m]
     const int32_t SGUFP_GBL *head;       // [m]
     const uint8_t SGUFP_GBL *vbar;       // [n]

@@ -162,12 +162,16 @@ __device__ inline void for_residual(const SubNet &N, const SubLds &W, int nct, i
 // The residual arcs of chain group g (chains g*64 .. g*64+63, one per lane) for one
 // Bellman-Ford: ends packed tail | head << 16, forward / backward key increments
 // ((cost << 16) + 1) and which of the two arcs exist.  Flows only change between
-// Bellman-Fords, so the first kRegGroups groups live in registers for all its passes.
-constexpr int kRegGroups = 16;
+// Bellman-Fords, so the first RG groups live in registers for all its passes: 16 groups
+// (80 VGPRs) on the 1k-arc networks, whose small LDS footprint runs 9 waves per CU; 64 on
+// the large ones, where the LDS allows one wave per CU anyway and the registers are free.
+// The groups beyond them are read from LDS one group ahead of their use.
+constexpr int kRegGroupsSmall = 16, kRegGroupsLarge = 40;
 
 struct ChainArcs {
     uint32_t th;
-    int64_t wf, wb;
+    int64_t wf, wb;     // key increments (cost << 16) + 1
+    int64_t cf, cbk;    // the costs
     bool fwd, bwd;
 };
 
@@ -180,6 +184,8 @@ __device__ __forceinline__ ChainArcs chain_arcs(uint64_t ca, uint64_t cb, bool i
     const int64_t R = ch_R(ca);
     const int64_t w_f = (mode == kPotPlain) ? -R : -(R + (x < L ? M : 0));
     const int64_t w_b = (mode == kPotPlain) ? R : R + (x <= L ? M : 0);
+    c.cf = w_f;
+    c.cbk = w_b;
     c.wf = (w_f << kHopBits) + 1;
     c.wb = (w_b << kHopBits) + 1;
     c.fwd = ok && x < U;
@@ -187,26 +193,35 @@ __device__ __forceinline__ ChainArcs chain_arcs(uint64_t ca, uint64_t cb, bool i
     return c;
 }
 
+// WT: the type the costs are kept in (int32_t for the large variant, whose host check bounds
+// the big-M costs below 2^30; the key increment (cost << 16) + 1 is formed at use)
+template <int RG, typename WT>
 struct ChainRegs {
-    uint32_t th[kRegGroups];
-    int64_t wf[kRegGroups], wb[kRegGroups];
-    uint32_t fmask, bmask;
+    uint32_t th[RG];
+    WT wf[RG], wb[RG];
+    uint64_t fmask, bmask;
 };
 
-__device__ __forceinline__ void load_chain_regs(const SubLds &W, int n, int nct, int mode, int64_t M, ChainRegs &C) {
+template <int RG, typename WT>
+__device__ __forceinline__ void load_chain_regs(const SubLds &W, int n, int nct, int mode, int64_t M, ChainRegs<RG, WT> &C) {
     C.fmask = 0;
     C.bmask = 0;
 #pragma unroll
-    for (int g = 0; g < kRegGroups; g++) {
+    for (int g = 0; g < RG; g++) {
         const int k = g * kWave + lane();
         uint64_t ca = 0, cb = 0;
         if (k < nct) { ca = W.cta[k]; cb = W.ctb[k]; }
         const ChainArcs c = chain_arcs(ca, cb, k < nct, n, mode, M);
         C.th[g] = c.th;
-        C.wf[g] = c.wf;
-        C.wb[g] = c.wb;
-        C.fmask |= (c.fwd ? 1u : 0u) << g;
-        C.bmask |= (c.bwd ? 1u : 0u) << g;
+        if constexpr (sizeof(WT) == 8) {   // key increments, formed once
+            C.wf[g] = c.wf;
+            C.wb[g] = c.wb;
+        } else {                           // costs, the increment formed at use
+            C.wf[g] = (WT)c.cf;
+            C.wb[g] = (WT)c.cbk;
+        }
+        C.fmask |= (c.fwd ? 1ull : 0ull) << g;
+        C.bmask |= (c.bwd ? 1ull : 0ull) << g;
     }
 }
 
@@ -222,8 +237,9 @@ __device__ __forceinline__ void load_chain_regs(const SubLds &W, int n, int nct,
 // then every residual arc is settled on the same keys.  `forward` picks the half: the Z
 // arcs out of Z_out / Z and the forward residual arcs, then the arcs into Z_in / Z; or the
 // backward residual arcs.
+template <int RG, typename WT>
 __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M,
-                                    const ChainRegs &C, bool forward) {
+                                    const ChainRegs<RG, WT> &C, bool forward) {
     uint32_t changed = 0;
     auto relax = [&](int v, int64_t nk) {
         if (nk < W.key[v]) {
@@ -247,18 +263,37 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
     };
     const int n = N.n;
     const int G = (nct + kWave - 1) / kWave;
+    // chains of group g from LDS (groups past the register-resident ones)
+    auto fetch = [&](int g, uint64_t &ca, uint64_t &cb) {
+        const int k = g * kWave + lane();
+        ca = 0;
+        cb = 0;
+        if (k < nct) { ca = W.cta[k]; cb = W.ctb[k]; }
+    };
+    constexpr bool kPrefetch = RG >= kRegGroupsLarge;
     if (!forward) {
-        for (int g = G - 1; g >= kRegGroups; g--) {
-            const int k = g * kWave + lane();
-            uint64_t ca = 0, cb = 0;
-            if (k < nct) { ca = W.cta[k]; cb = W.ctb[k]; }
-            const ChainArcs c = chain_arcs(ca, cb, k < nct, n, mode, M);
-            arc(c.th, c.wb, c.bwd, false);
+        if (!kPrefetch) {
+            for (int g = G - 1; g >= RG; g--) {
+                uint64_t ca, cb;
+                fetch(g, ca, cb);
+                const ChainArcs c = chain_arcs(ca, cb, g * kWave + lane() < nct, n, mode, M);
+                arc(c.th, c.wb, c.bwd, false);
+            }
+        } else if (G > RG) {
+            uint64_t na, nb;
+            fetch(G - 1, na, nb);
+            for (int g = G - 1; g >= RG; g--) {
+                const uint64_t ca = na, cb = nb;
+                if (g > RG) fetch(g - 1, na, nb);   // next group's chains load under this group's keys
+                const ChainArcs c = chain_arcs(ca, cb, g * kWave + lane() < nct, n, mode, M);
+                arc(c.th, c.wb, c.bwd, false);
+            }
         }
 #pragma unroll
-        for (int g = kRegGroups - 1; g >= 0; g--) {
+        for (int g = RG - 1; g >= 0; g--) {
             if (g >= G) continue;
-            arc(C.th[g], C.wb[g], (C.bmask >> g) & 1u, false);
+            arc(C.th[g], sizeof(WT) == 8 ? (int64_t)C.wb[g] : ((int64_t)C.wb[g] << kHopBits) + 1, (C.bmask >> g) & 1ull,
+                false);
         }
         return changed;
     }
@@ -273,16 +308,27 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
     }
     wave_lds_sync();
 #pragma unroll
-    for (int g = 0; g < kRegGroups; g++) {
+    for (int g = 0; g < RG; g++) {
         if (g >= G) break;
-        arc(C.th[g], C.wf[g], (C.fmask >> g) & 1u, true);
+        arc(C.th[g], sizeof(WT) == 8 ? (int64_t)C.wf[g] : ((int64_t)C.wf[g] << kHopBits) + 1, (C.fmask >> g) & 1ull,
+            true);
     }
-    for (int g = kRegGroups; g < G; g++) {
-        const int k = g * kWave + lane();
-        uint64_t ca = 0, cb = 0;
-        if (k < nct) { ca = W.cta[k]; cb = W.ctb[k]; }
-        const ChainArcs c = chain_arcs(ca, cb, k < nct, n, mode, M);
-        arc(c.th, c.wf, c.fwd, true);
+    if (!kPrefetch) {
+        for (int g = RG; g < G; g++) {
+            uint64_t ca, cb;
+            fetch(g, ca, cb);
+            const ChainArcs c = chain_arcs(ca, cb, g * kWave + lane() < nct, n, mode, M);
+            arc(c.th, c.wf, c.fwd, true);
+        }
+    } else if (G > RG) {
+        uint64_t na, nb;
+        fetch(RG, na, nb);
+        for (int g = RG; g < G; g++) {
+            const uint64_t ca = na, cb = nb;
+            if (g + 1 < G) fetch(g + 1, na, nb);
+            const ChainArcs c = chain_arcs(ca, cb, g * kWave + lane() < nct, n, mode, M);
+            arc(c.th, c.wf, c.fwd, true);
+        }
     }
     // sinks -> Z_in (SSP) / free nodes -> Z (potentials), cost 0
     for (int i = lane(); i < nz; i += kWave) {
@@ -298,8 +344,9 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
 
 // Iterate sweeps, forward and backward alternating, to the fixed point (false: not within
 // the pass bound).
+template <int RG, typename WT>
 __device__ inline bool bf_converge(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M,
-                                   const ChainRegs &C) {
+                                   const ChainRegs<RG, WT> &C) {
     bool prev_quiet = false;   // the sweep before the current one changed nothing
     for (int it = 0; it < 2 * (N.n + 4); it++) {
 #ifdef SGUFP_SUB_TRACE
@@ -329,6 +376,7 @@ __device__ inline void ssp_preds(const SubNet &N, const SubLds &W, int nct, int 
 
 // warm: keep the keys (exact or infinite, see invalidate_subtrees) instead of starting from
 // Z_out alone -- Bellman-Ford from any upper bounds of the shortest keys reaches them.
+template <int RG, typename WT>
 __device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M,
                                     bool warm = false) {
     const int nn = N.n + 2;
@@ -336,8 +384,8 @@ __device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, i
         if (!warm) W.key[v] = (mode == kSsp) ? (v == N.n ? 0 : kInf) : 0;
         W.pred[v] = kNoPred;
     }
-    ChainRegs C;
-    load_chain_regs(W, N.n, nct, mode, M, C);
+    ChainRegs<RG, WT> C;
+    load_chain_regs<RG, WT>(W, N.n, nct, mode, M, C);
     wave_lds_sync();
     const bool converged = bf_converge(N, W, nct, nz, mode, M, C);
     if (mode != kSsp || !converged) return converged;
@@ -556,6 +604,7 @@ __device__ ChainOut assemble_chain(const SubNet &N, const SubLds &W, const SubIO
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
+template <int RG, typename WT>
 __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
@@ -716,7 +765,7 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
         bool warm = false;
         for (; status == kSubOptimal; iters++) {
             SUB_T0();
-            if (!bellman_ford(N, W, nct, nz, kSsp, M, warm)) { status = kSubError; break; }
+            if (!bellman_ford<RG, WT>(N, W, nct, nz, kSsp, M, warm)) { status = kSubError; break; }
             SUB_T1(t_bf);
 #ifdef SGUFP_SUB_VERIFY
             if (W.misc[6]) { status = kSubError; break; }
@@ -791,7 +840,7 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
             //    costs (their M-multiple is a dual ray, case (iii))
             const int mode = unmet ? kPotBigM : kPotPlain;
             if (unmet) status = kSubInfeasible;
-            if (!bellman_ford(N, W, nct, nz, mode, M)) status = kSubError;
+            if (!bellman_ford<RG, WT>(N, W, nct, nz, mode, M)) status = kSubError;
             const int64_t dz = key_cost(W.key[n]);
             for (int v = lane(); v < n; v += kWave) {
                 int64_t d = key_cost(W.key[v]) - dz;
@@ -904,7 +953,15 @@ hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st) {
 #ifdef SGUFP_SUB_LDS_MIN
     if (lds < SGUFP_SUB_LDS_MIN) lds = SGUFP_SUB_LDS_MIN;   // occupancy experiments
 #endif
-    hipLaunchKernelGGL(k_sub_scenario, dim3((unsigned)io.n_paths * N.S), dim3(kWave), lds, st, N, io);
+    // register-resident chain groups: the large variant once the LDS footprint allows at
+    // most two waves per CU (its registers would cost the small networks their occupancy)
+    // and the big-M costs fit 32 bits (N.cost_bound, host)
+    if (lds > 64 * 1024 && io.nct_cap > kRegGroupsSmall * kWave && N.cost_bound < ((int64_t)1 << 30))
+        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsLarge, int32_t>), dim3((unsigned)io.n_paths * N.S), dim3(kWave), lds, st,
+                           N, io);
+    else
+        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsSmall, int64_t>), dim3((unsigned)io.n_paths * N.S), dim3(kWave), lds,
+                           st, N, io);
     hipLaunchKernelGGL(k_sub_reduce, dim3((unsigned)io.n_paths), dim3(256), 0, st, N, io);
     return hipGetLastError();
 }
