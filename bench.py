@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--profile-tag", default="r02")
     ap.add_argument("--sub-paths", type=int, default=32, help="subproblem leg: random full-matching paths (0: skip)")
     ap.add_argument("--cpu-sub-seconds", type=float, default=8.0)
+    ap.add_argument("--c5-nodes", type=int, default=1024,
+                    help="config-5 leg (5k arcs, 512 scenarios): open nodes relaxed per step (0: skip)")
+    ap.add_argument("--c5-paths", type=int, default=4, help="config-5 leg: subproblem paths x 512 scenarios")
     ap.add_argument("--mode", choices=["relax", "bnb"], default="relax",
                     help="relax: the headline batch relaxation; bnb: the device B&B (config C3) for --bnb-seconds")
     ap.add_argument("--bnb-config", default="C3")
@@ -349,11 +352,71 @@ def main():
     if sub is not None:
         sub.pop("_paths", None)
         sub.pop("_inst0", None)
+    eng.close()
+    if rank == 0 and world == 1 and args.config == "C4" and args.c5_nodes > 0:
+        line["config5"] = config5_leg(args, work)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    eng.close()
     if dist:
         dist.destroy_process_group()
+
+
+def config5_leg(args, work):
+    """BASELINE configs[4]: the 5k-arc, 512-scenario instance with cut generation in the loop.
+    Relaxation rate of a BFS frontier of --c5-nodes records under a 16F + 64O pool (same
+    timing as the headline, k_relax on the library's stream), and the scenario subproblem
+    (k_sub_scenario + k_sub_reduce) on --c5-paths random full matchings x 512 scenarios with
+    lower bounds 0 (every scenario optimal: full max-reward flows, optimality cuts)."""
+    from sgufp_solver_amd import engine as E
+    from sgufp_solver_amd import frontier, instance, pools
+    cfg = instance.CONFIGS["C5"]
+    inst = instance.generate(cfg, args.seed)
+    inst.lb[:] = 0
+    net = os.path.join(work, "net_c5.txt")
+    inst.write(net)
+    pool = pools.synthetic_pool(inst, args.n_feas, args.n_opt, args.seed)
+    n = args.c5_nodes
+    eng = E.Engine(net, 0, n)
+    fr = frontier.bfs_frontier(eng, n)
+    eng.add_cuts(pool)
+    eng.upload(fr)
+    eng.relax_async(pools.DOUBLE_MIN)
+    eng.sync()
+    st, ex, lb, ub, nc = eng.results_arrays()
+    fin = ub[(st == 0) | (st == 3)]
+    inc = float(np.percentile(fin, 40)) if fin.size else 0.0
+    eng.set_timing(True)
+    eng.relax_async(inc)
+    eng.sync()
+    steps = 5
+    ms = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.relax_async(inc)
+        eng.sync()
+        ms.append(eng.last_timing()[0])
+    wall = time.perf_counter() - t0
+    st, ex, lb, ub, nc = eng.results_arrays()
+    dn, da, dl, sw = eng.stats()
+    out = {"workload": f"C5: {cfg.n_arcs}-arc layered network, {inst.scenarios} scenarios, {args.n_feas}F+{args.n_opt}O "
+                       f"pool, BFS frontier of {fr.n} open nodes", "instance_seed": args.seed, "incumbent": inc,
+           "relaxations_per_s": round(fr.n * steps / wall, 2), "k_relax_ms": round(float(np.mean(ms)), 4),
+           "status_counts": {str(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
+           "avg_dd_nodes": float(np.mean(dn)), "avg_sweeps": float(np.mean(sw))}
+    if args.c5_paths > 0:
+        _, la, _ = E.probe_network(net)
+        rng = np.random.default_rng(args.seed + 7)
+        paths = [instance.random_matching_path(inst, la, rng) for _ in range(args.c5_paths)]
+        eng.subproblem(paths)                                  # warm-up
+        t0 = time.perf_counter()
+        typ, _, _, _ = eng.subproblem(paths)
+        t = time.perf_counter() - t0
+        out["subproblem"] = {"kernel": "k_sub_scenario", "paths": len(paths), "scenarios": int(inst.scenarios),
+                             "lower_bounds": 0, "ms_per_call": round(t * 1e3, 2),
+                             "scenario_lps_per_s": round(len(paths) * inst.scenarios / t, 1),
+                             "cut_types": {str(k): int(v) for k, v in zip(*np.unique(typ, return_counts=True))}}
+    eng.close()
+    return out
 
 
 def subproblem_leg(eng, inst, net, args):

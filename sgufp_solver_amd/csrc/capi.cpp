@@ -541,7 +541,7 @@ bool sgufp_ctx::sub_init() {
         for (int a = 0; a < m; a++) arc_topo[a] = a;
         std::stable_sort(arc_topo.begin(), arc_topo.end(), [&](int a, int b) { return rank[N.tail[a]] < rank[N.tail[b]]; });
     }
-    if (sub_lds_bytes(n, m, m, nz) > 160 * 1024) { err = "network too large for the LDS subproblem"; return false; }
+    if (sub_lds_bytes(n, m, m, nz, 4) > 160 * 1024) { err = "network too large for the LDS subproblem"; return false; }
     std::vector<int32_t> inner(n), arc_layer(m, -1), lb((size_t)S * m), ub((size_t)S * m), rew(m);
     std::vector<uint8_t> vb(n), in8(n);
     std::vector<int32_t> in_off(n + 1, 0), out_off(n + 1, 0), in_list, out_list;

@@ -35,6 +35,7 @@
 #include <cstdint>
 
 #include "sub_device.hpp"
+#define SGUFP_MULTI_WAVE_TU   // k_sub_scenario runs 1 or 4 waves per workgroup
 #include "wave.hpp"
 
 namespace sgufp {
@@ -65,6 +66,8 @@ struct SubLds {
     double GBL *coef;       // [n_slots] this (path, scenario)'s row of SubIO::coef (phase 5)
     LDS int32_t *zlist;     // [nz] free-supply / free-demand nodes: v | src << 30 | snk << 29
     LDS int32_t *misc;      // [8] flags
+    LDS int64_t *red;       // [8] cross-wave reduction slots (multi-wave workgroups)
+    LDS uint16_t *anc2;     // [n+2] second ancestor buffer of invalidate_subtrees (multi-wave)
 #ifdef SGUFP_SUB_VERIFY
     LDS int64_t *vkey;      // [n+2] warm Bellman-Ford keys, compared with a cold run
 #endif
@@ -72,9 +75,43 @@ struct SubLds {
 
 __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+// One scenario per workgroup of NW waves.  NW = 1 on the 1k-arc networks (a single wave;
+// nine of them share a CU's LDS); NW = 4 on the large ones, whose LDS holds one scenario per
+// CU: the waves then share every per-chain / per-node loop, and a Bellman-Ford step relaxes
+// NW chain groups at once (see bf_sweep).
+template <int NW>
+struct Blk {
+    static constexpr int T = NW * kWave;
+    __device__ static __forceinline__ int tid() { return (int)threadIdx.x; }
+    __device__ static __forceinline__ int wid() { return NW == 1 ? 0 : (int)threadIdx.x / kWave; }
+    __device__ static __forceinline__ void sync() {
+        if constexpr (NW == 1) wave_lds_sync();
+        else __syncthreads();
+    }
+    // all-reduce over the workgroup (associative, commutative op)
+    template <typename V, typename Op>
+    __device__ static __forceinline__ V all(V x, Op op, LDS int64_t *red) {
+        x = lane_reduce<1>(x, op);
+        if constexpr (NW == 1) {
+            return x;
+        } else {
+            if (lane() == 0) red[wid()] = (int64_t)x;
+            __syncthreads();
+            V r = (V)red[0];
+            for (int w = 1; w < NW; w++) r = op(r, (V)red[w]);
+            __syncthreads();
+            return r;
+        }
+    }
+    __device__ static __forceinline__ uint32_t any(uint32_t x, LDS int64_t *red) {
+        return all(x, [](uint32_t a, uint32_t b) { return a | b; }, red);
+    }
+};
+
 // LDS: chains, then a union -- phases 1-2: chosen and dec (int16 [m] each);
 // phases 3-5: key (alpha), pred, plist -- then the free-node list and flags.
-__host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int nz, size_t *off) {
+constexpr int kSubLdsParts = 12;
+__host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int nz, int nw, size_t *off) {
     size_t o = 0;
     off[1] = o; o = a16(o + (size_t)nct_cap * 8);
     off[2] = o; o = a16(o + (size_t)nct_cap * 8);
@@ -82,11 +119,13 @@ __host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int 
     off[3] = o; o = a16(o + (size_t)(n + 2) * 8);   // key | chosen
     off[4] = o; o = a16(o + (size_t)(n + 2) * 4);   // pred
     off[8] = o; o = a16(o + (size_t)(n + 2) * 2);   // plist
+    off[11] = o; o = a16(o + (nw > 1 ? (size_t)(n + 2) * 2 : 0));   // anc2
     off[0] = a16(u0 + (size_t)m * 2);               // dec, after chosen
     if (o < a16(off[0] + (size_t)m * 2)) o = a16(off[0] + (size_t)m * 2);
     off[5] = o;
     off[6] = o; o = a16(o + (size_t)nz * 4);
     off[7] = o; o = a16(o + 8 * 4);
+    off[10] = o; o = a16(o + (nw > 1 ? 8 * 8 : 0));   // red
 #ifdef SGUFP_SUB_VERIFY
     off[9] = o; o = a16(o + (size_t)(n + 2) * 8);
 #endif
@@ -128,10 +167,11 @@ __device__ inline int slot_of(const SubNet &N, int layer, int j) {
 //             BIGM selects the big-M costs (dual ray) or the plain ones (optimal duals).
 enum BfMode { kSsp = 0, kPotPlain = 1, kPotBigM = 2 };
 
-template <typename F>
+template <int NW, typename F>
 __device__ inline void for_residual(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M, F visit) {
+    using B = Blk<NW>;
     // contracted arcs: code 2k (forward), 2k+1 (backward)
-    for (int k = lane(); k < nct; k += kWave) {
+    for (int k = B::tid(); k < nct; k += B::T) {
         const uint64_t ca = W.cta[k], cb = W.ctb[k];
         const int t = ch_t(ca), h = ch_h(ca);
         if (t < 0 || h < 0) continue;
@@ -145,7 +185,7 @@ __device__ inline void for_residual(const SubNet &N, const SubLds &W, int nct, i
         }
     }
     // Z arcs: code 2m + 2v (+1), from the LDS list of non-inner nodes
-    for (int i = lane(); i < nz; i += kWave) {
+    for (int i = B::tid(); i < nz; i += B::T) {
         const uint32_t e = (uint32_t)W.zlist[i];
         const int v = (int)(e & 0x1FFFFFFFu);
         const bool src = (e >> 30) & 1u, snk = (e >> 29) & 1u;
@@ -162,11 +202,11 @@ __device__ inline void for_residual(const SubNet &N, const SubLds &W, int nct, i
 // The residual arcs of chain group g (chains g*64 .. g*64+63, one per lane) for one
 // Bellman-Ford: ends packed tail | head << 16, forward / backward key increments
 // ((cost << 16) + 1) and which of the two arcs exist.  Flows only change between
-// Bellman-Fords, so the first RG groups live in registers for all its passes: 16 groups
-// (80 VGPRs) on the 1k-arc networks, whose small LDS footprint runs 9 waves per CU; 64 on
-// the large ones, where the LDS allows one wave per CU anyway and the registers are free.
-// The groups beyond them are read from LDS one group ahead of their use.
-constexpr int kRegGroupsSmall = 16, kRegGroupsLarge = 40;
+// Bellman-Fords, so the first RG groups of each wave live in registers for all its passes:
+// 16 groups (80 VGPRs) on the 1k-arc networks, whose small LDS footprint runs 9 waves per CU;
+// on the large ones (one scenario per CU, NW = 4 waves) 20 groups per wave with 32-bit
+// costs.  Groups beyond them are read from LDS (one group ahead of their use with one wave).
+constexpr int kRegGroupsSmall = 16, kRegGroupsLarge = 20, kLargeWaves = 4;
 
 struct ChainArcs {
     uint32_t th;
@@ -202,13 +242,14 @@ struct ChainRegs {
     uint64_t fmask, bmask;
 };
 
-template <int RG, typename WT>
+// register slot j of wave w holds chain group j * NW + w
+template <int RG, typename WT, int NW>
 __device__ __forceinline__ void load_chain_regs(const SubLds &W, int n, int nct, int mode, int64_t M, ChainRegs<RG, WT> &C) {
     C.fmask = 0;
     C.bmask = 0;
 #pragma unroll
     for (int g = 0; g < RG; g++) {
-        const int k = g * kWave + lane();
+        const int k = (g * NW + Blk<NW>::wid()) * kWave + lane();
         uint64_t ca = 0, cb = 0;
         if (k < nct) { ca = W.cta[k]; cb = W.ctb[k]; }
         const ChainArcs c = chain_arcs(ca, cb, k < nct, n, mode, M);
@@ -237,7 +278,11 @@ __device__ __forceinline__ void load_chain_regs(const SubLds &W, int n, int nct,
 // then every residual arc is settled on the same keys.  `forward` picks the half: the Z
 // arcs out of Z_out / Z and the forward residual arcs, then the arcs into Z_in / Z; or the
 // backward residual arcs.
-template <int RG, typename WT>
+// With NW waves, step j of a sweep relaxes groups j * NW .. j * NW + NW - 1 at once (one per
+// wave) and a barrier closes the step: the groups of one step are consecutive chains, almost
+// always tails of one layer of the network, so the in-order propagation along runs of arcs
+// is kept.
+template <int RG, typename WT, int NW>
 __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M,
                                     const ChainRegs<RG, WT> &C, bool forward) {
     uint32_t changed = 0;
@@ -270,7 +315,65 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
         cb = 0;
         if (k < nct) { ca = W.cta[k]; cb = W.ctb[k]; }
     };
-    constexpr bool kPrefetch = RG >= kRegGroupsLarge;
+    auto reg_w = [&](WT w) -> int64_t { return sizeof(WT) == 8 ? (int64_t)w : ((int64_t)w << kHopBits) + 1; };
+    if constexpr (NW > 1) {
+        using B = Blk<NW>;
+        const int S = (G + NW - 1) / NW, wv = B::wid();
+        if (!forward) {
+            for (int j = S - 1; j >= RG; j--) {
+                const int g = j * NW + wv;
+                if (g < G) {
+                    uint64_t ca, cb;
+                    fetch(g, ca, cb);
+                    const ChainArcs c = chain_arcs(ca, cb, g * kWave + lane() < nct, n, mode, M);
+                    arc(c.th, c.wb, c.bwd, false);
+                }
+                __syncthreads();
+            }
+#pragma unroll
+            for (int j = RG - 1; j >= 0; j--) {
+                if (j >= S) continue;
+                if (j * NW + wv < G) arc(C.th[j], reg_w(C.wb[j]), (C.bmask >> j) & 1ull, false);
+                __syncthreads();
+            }
+            return changed;
+        }
+        {
+            const int64_t kz = W.key[n];
+            if (kz < kInf)
+                for (int i = B::tid(); i < nz; i += B::T) {
+                    const uint32_t e = (uint32_t)W.zlist[i];
+                    if (mode != kSsp || ((e >> 30) & 1u)) relax((int)(e & 0x1FFFFFFFu), kz + 1);
+                }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < RG; j++) {
+            if (j >= S) break;
+            if (j * NW + wv < G) arc(C.th[j], reg_w(C.wf[j]), (C.fmask >> j) & 1ull, true);
+            __syncthreads();
+        }
+        for (int j = RG; j < S; j++) {
+            const int g = j * NW + wv;
+            if (g < G) {
+                uint64_t ca, cb;
+                fetch(g, ca, cb);
+                const ChainArcs c = chain_arcs(ca, cb, g * kWave + lane() < nct, n, mode, M);
+                arc(c.th, c.wf, c.fwd, true);
+            }
+            __syncthreads();
+        }
+        for (int i = B::tid(); i < nz; i += B::T) {
+            const uint32_t e = (uint32_t)W.zlist[i];
+            const int v = (int)(e & 0x1FFFFFFFu);
+            const int64_t kv = W.key[v];
+            if (kv >= kInf) continue;
+            if (mode == kSsp) { if ((e >> 29) & 1u) relax(n + 1, kv + 1); }
+            else relax(n, kv + 1);
+        }
+        return changed;
+    }
+    constexpr bool kPrefetch = RG >= 32;
     if (!forward) {
         if (!kPrefetch) {
             for (int g = G - 1; g >= RG; g--) {
@@ -292,8 +395,7 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
 #pragma unroll
         for (int g = RG - 1; g >= 0; g--) {
             if (g >= G) continue;
-            arc(C.th[g], sizeof(WT) == 8 ? (int64_t)C.wb[g] : ((int64_t)C.wb[g] << kHopBits) + 1, (C.bmask >> g) & 1ull,
-                false);
+            arc(C.th[g], reg_w(C.wb[g]), (C.bmask >> g) & 1ull, false);
         }
         return changed;
     }
@@ -310,8 +412,7 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
 #pragma unroll
     for (int g = 0; g < RG; g++) {
         if (g >= G) break;
-        arc(C.th[g], sizeof(WT) == 8 ? (int64_t)C.wf[g] : ((int64_t)C.wf[g] << kHopBits) + 1, (C.fmask >> g) & 1ull,
-            true);
+        arc(C.th[g], reg_w(C.wf[g]), (C.fmask >> g) & 1ull, true);
     }
     if (!kPrefetch) {
         for (int g = RG; g < G; g++) {
@@ -344,17 +445,18 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
 
 // Iterate sweeps, forward and backward alternating, to the fixed point (false: not within
 // the pass bound).
-template <int RG, typename WT>
+template <int RG, typename WT, int NW>
 __device__ inline bool bf_converge(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M,
                                    const ChainRegs<RG, WT> &C) {
+    using B = Blk<NW>;
     bool prev_quiet = false;   // the sweep before the current one changed nothing
     for (int it = 0; it < 2 * (N.n + 4); it++) {
 #ifdef SGUFP_SUB_TRACE
-        if (lane() == 0 && !(it & 1)) W.misc[5]++;
+        if (B::tid() == 0 && !(it & 1)) W.misc[5]++;
 #endif
-        const uint32_t changed = bf_sweep(N, W, nct, nz, mode, M, C, !(it & 1));
-        wave_lds_sync();
-        const bool quiet = !wave_or(changed);
+        const uint32_t changed = bf_sweep<RG, WT, NW>(N, W, nct, nz, mode, M, C, !(it & 1));
+        B::sync();
+        const bool quiet = !B::any(changed, W.red);
         if (quiet && prev_quiet) return true;
         prev_quiet = quiet;
     }
@@ -364,48 +466,50 @@ __device__ inline bool bf_converge(const SubNet &N, const SubLds &W, int nct, in
 // Predecessors of the SSP labels: the smallest arc code among the residual arcs into each
 // node that are tight in (cost, hops).  Hops grow by one along such arcs, so the
 // predecessor graph has no cycle and the walk from Z_in ends at Z_out.
+template <int NW>
 __device__ inline void ssp_preds(const SubNet &N, const SubLds &W, int nct, int nz, int64_t M) {
-    for_residual(N, W, nct, nz, kSsp, M, [&](int u, int v, int64_t w, int code) {
+    for_residual<NW>(N, W, nct, nz, kSsp, M, [&](int u, int v, int64_t w, int code) {
         const int64_t ku = W.key[u];
         if (ku >= kInf) return;
         if (ku + (w << kHopBits) + 1 == W.key[v])
             __hip_atomic_fetch_min(&W.pred[v], code << 15 | u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     });
-    wave_lds_sync();
+    Blk<NW>::sync();
 }
 
 // warm: keep the keys (exact or infinite, see invalidate_subtrees) instead of starting from
 // Z_out alone -- Bellman-Ford from any upper bounds of the shortest keys reaches them.
-template <int RG, typename WT>
+template <int RG, typename WT, int NW>
 __device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M,
                                     bool warm = false) {
+    using B = Blk<NW>;
     const int nn = N.n + 2;
-    for (int v = lane(); v < nn; v += kWave) {
+    for (int v = B::tid(); v < nn; v += B::T) {
         if (!warm) W.key[v] = (mode == kSsp) ? (v == N.n ? 0 : kInf) : 0;
         W.pred[v] = kNoPred;
     }
     ChainRegs<RG, WT> C;
-    load_chain_regs<RG, WT>(W, N.n, nct, mode, M, C);
-    wave_lds_sync();
-    const bool converged = bf_converge(N, W, nct, nz, mode, M, C);
+    load_chain_regs<RG, WT, NW>(W, N.n, nct, mode, M, C);
+    B::sync();
+    const bool converged = bf_converge<RG, WT, NW>(N, W, nct, nz, mode, M, C);
     if (mode != kSsp || !converged) return converged;
 #ifdef SGUFP_SUB_VERIFY
     // Debug build: the labels a warm start converged to must equal those of a cold
     // Bellman-Ford from Z_out alone (invalidate_subtrees' exactness argument, checked).
     if (warm) {
-        for (int v = lane(); v < nn; v += kWave) {
+        for (int v = B::tid(); v < nn; v += B::T) {
             W.vkey[v] = W.key[v];
             W.key[v] = (v == N.n) ? 0 : kInf;
         }
-        wave_lds_sync();
-        const bool cold_ok = bf_converge(N, W, nct, nz, mode, M, C);
+        B::sync();
+        const bool cold_ok = bf_converge<RG, WT, NW>(N, W, nct, nz, mode, M, C);
         uint32_t diff = cold_ok ? 0u : 1u;
-        for (int v = lane(); v < nn; v += kWave) diff |= (W.vkey[v] != W.key[v]) ? 1u : 0u;
-        if (wave_or(diff) && lane() == 0) W.misc[6] = 1;
-        wave_lds_sync();
+        for (int v = B::tid(); v < nn; v += B::T) diff |= (W.vkey[v] != W.key[v]) ? 1u : 0u;
+        if (B::any(diff, W.red) && B::tid() == 0) W.misc[6] = 1;
+        B::sync();
     }
 #endif
-    ssp_preds(N, W, nct, nz, M);
+    ssp_preds<NW>(N, W, nct, nz, M);
     return true;
 }
 
@@ -420,8 +524,36 @@ __device__ inline int64_t key_cost(int64_t k) { return k >> kHopBits; }
 // at equal cost with more hops.  Pointer jumping over the tree (ancestor in the path list's
 // space, dead = infinite key): a wave reads one group's entries before it writes them, and
 // later groups read after earlier ones wrote, so no lane sees a half-updated pair.
+// With several waves the rounds are double-buffered (every pointer of a round is read from
+// the previous round's buffer); a node killed in the same round as a descendant reads it is
+// caught one round later through the very ancestor that killed it.
+template <int NW>
 __device__ inline void invalidate_subtrees(const SubNet &N, const SubLds &W) {
     const int nn = N.n + 2;
+    if constexpr (NW > 1) {
+        using B = Blk<NW>;
+        LDS uint16_t *a_in = W.plist, *a_out = W.anc2;
+        for (int v = B::tid(); v < nn; v += B::T) {
+            const int32_t pr = W.pred[v];
+            a_in[v] = (uint16_t)(pr == kNoPred ? v : (pr & 0x7FFF));
+        }
+        __syncthreads();
+        for (int r = 0; r < 32; r++) {
+            uint32_t moved = 0;
+            for (int v = B::tid(); v < nn; v += B::T) {
+                const int a = a_in[v];
+                const int aa = a_in[a];
+                if (W.key[a] >= kInf && W.key[v] < kInf) W.key[v] = kInf;
+                a_out[v] = (uint16_t)aa;
+                moved |= (aa != a) ? 1u : 0u;
+            }
+            LDS uint16_t *t = a_in;
+            a_in = a_out;
+            a_out = t;
+            if (!B::any(moved, W.red)) break;
+        }
+        return;
+    }
     LDS uint16_t *anc = W.plist;
     for (int v = lane(); v < nn; v += kWave) {
         const int32_t pr = W.pred[v];
@@ -604,15 +736,18 @@ __device__ ChainOut assemble_chain(const SubNet &N, const SubLds &W, const SubIO
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
-template <int RG, typename WT>
-__global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
+template <int RG, typename WT, int NW>
+__global__ void __launch_bounds__(kWave * NW) k_sub_scenario(SubNet N, SubIO io) {
+    using B = Blk<NW>;
+    const int tid = B::tid();
+    constexpr int T = B::T;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
     const int S = N.S;
     const int p = blockIdx.x / S, s = blockIdx.x - p * S;
     if (p >= io.n_paths) return;
-    size_t off[10];
-    sub_lds_layout(N.n, N.m, io.nct_cap, N.nz, off);
+    size_t off[kSubLdsParts];
+    sub_lds_layout(N.n, N.m, io.nct_cap, N.nz, NW, off);
     SubLds W;
     W.dec = (LDS int16_t *)(smem + off[0]);
     W.cta = (LDS uint64_t *)(smem + off[1]);
@@ -625,6 +760,8 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     W.coef = io.coef + ((size_t)p * S + s) * N.n_slots;
     W.zlist = (LDS int32_t *)(smem + off[6]);
     W.misc = (LDS int32_t *)(smem + off[7]);
+    W.red = (LDS int64_t *)(smem + off[10]);
+    W.anc2 = (LDS uint16_t *)(smem + off[11]);
 #ifdef SGUFP_SUB_VERIFY
     W.vkey = (LDS int64_t *)(smem + off[9]);
 #endif
@@ -634,44 +771,59 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     const size_t b = (size_t)p * S + s;
 
     // 1. decisions and matching
-    if (lane() < 8) W.misc[lane()] = 0;
-    for (int a = lane(); a < m; a += kWave) {
+    if (tid < 8) W.misc[tid] = 0;
+    for (int a = tid; a < m; a += T) {
         W.chosen[a] = -1;
         W.dec[a] = (int16_t)dec_of(N, io, poff, plen, a);
     }
-    wave_lds_sync();
-    for (int a = lane(); a < m; a += kWave) {
+    B::sync();
+    for (int a = tid; a < m; a += T) {
         const int d = W.dec[a];
         if (d == -3) W.misc[0] = 1;
         if (d >= 0) W.chosen[d] = (int16_t)a;   // one of several writers wins ...
     }
-    wave_lds_sync();
-    for (int a = lane(); a < m; a += kWave) {
+    B::sync();
+    for (int a = tid; a < m; a += T) {
         const int d = W.dec[a];
         if (d >= 0 && W.chosen[d] != a) W.misc[0] = 1;   // ... the others: two in-arcs chose one
     }                                                    // out-arc, not a path of an exact DD
-    wave_lds_sync();
+    B::sync();
 
     // 2. chains, numbered in the topological order of their first arc's tail
     int nct = 0;
-    for (int base = 0; base < m; base += kWave) {
-        const int a = base + lane() < m ? N.arc_topo[base + lane()] : -1;
+    for (int base = 0; base < m; base += T) {
+        const int a = base + tid < m ? N.arc_topo[base + tid] : -1;
         bool st = false;
         if (a >= 0) st = !N.vbar[N.tail[a]] || W.chosen[a] < 0;
         const uint32_t incl = wave_scan_incl(st ? 1u : 0u);
-        if (st && nct + (int)incl - 1 < io.nct_cap) W.ctb[nct + (int)incl - 1] = pack_b(0, 0, 0, a);
-        nct += (int)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+        uint32_t woff = 0, tot;
+        if constexpr (NW == 1) {
+            tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+        } else {
+            if (lane() == kWave - 1) W.red[B::wid()] = (int64_t)incl;
+            __syncthreads();
+            tot = 0;
+            for (int w = 0; w < NW; w++) {
+                const uint32_t c = (uint32_t)W.red[w];
+                woff += w < B::wid() ? c : 0u;
+                tot += c;
+            }
+            __syncthreads();
+        }
+        const int pos = nct + (int)(woff + incl) - 1;
+        if (st && pos < io.nct_cap) W.ctb[pos] = pack_b(0, 0, 0, a);
+        nct += (int)tot;
     }
     if (nct > io.nct_cap) {   // more chains than the host counted: not a valid path
-        if (lane() == 0) W.misc[0] = 1;
+        if (tid == 0) W.misc[0] = 1;
         nct = io.nct_cap;
     }
-    wave_lds_sync();
+    B::sync();
     // free-supply / free-demand nodes (structural, from the host; read by every pass)
     const int nz = N.nz;
-    for (int i = lane(); i < nz; i += kWave) W.zlist[i] = N.zlist[i];
+    for (int i = tid; i < nz; i += T) W.zlist[i] = N.zlist[i];
     int first_bad = INT_MAX;   // first chain (rank) that makes the scenario infeasible up front
-    for (int k = lane(); k < nct; k += kWave) {
+    for (int k = tid; k < nct; k += T) {
         int a = ch_first(W.ctb[k]);
         const int first = a;
         const int t0 = N.tail[a];
@@ -694,21 +846,21 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
         const bool complete = t >= 0 && h >= 0;
         if ((complete && L > U) || (!complete && L > 0)) first_bad = min(first_bad, k);
     }
-    first_bad = lane_reduce<1>(first_bad, [](int x, int y) { return x < y ? x : y; });
-    wave_lds_sync();
+    first_bad = B::all(first_bad, [](int x, int y) { return x < y ? x : y; }, W.red);
+    B::sync();
     // chosen is dead from here: its space holds keys / predecessors
-    for (int v = lane(); v < N.n_slots; v += kWave) W.coef[v] = 0.0;
+    for (int v = tid; v < N.n_slots; v += T) W.coef[v] = 0.0;
     __threadfence();   // zeros stored before any lane's atomic adds of phase 5
-    wave_lds_sync();
+    B::sync();
     if (W.misc[0]) {
-        if (lane() == 0) { io.status[b] = kSubError; io.obj[b] = 0; io.dual[b] = 0; io.rhs[b] = 0; }
-        for (int v = lane(); v < N.n_slots; v += kWave) io.coef[b * N.n_slots + v] = 0.0;
+        if (tid == 0) { io.status[b] = kSubError; io.obj[b] = 0; io.dual[b] = 0; io.rhs[b] = 0; }
+        for (int v = tid; v < N.n_slots; v += T) io.coef[b * N.n_slots + v] = 0.0;
         return;
     }
 
     int status = kSubOptimal;
-    int64_t M = 1, max_aug = 0;
-    for (int k = lane(); k < nct; k += kWave) {
+    int64_t M = 0, max_aug = 0;
+    for (int k = tid; k < nct; k += T) {
         const uint64_t ca = W.cta[k];
         if (ch_t(ca) >= 0 && ch_h(ca) >= 0) {
             const int64_t R = ch_R(ca), U = ch_U(W.ctb[k]);
@@ -716,11 +868,11 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
             max_aug += U > 0 ? U : 0;
         }
     }
-    M = lane_reduce<1>(M, [](int64_t x, int64_t y) { return x + y; }) - (kWave - 1);
+    M = 1 + B::all(M, [](int64_t x, int64_t y) { return x + y; }, W.red);
     // Every augmentation moves delta >= 1 more units from Z_out to Z_in, and that flow
     // crosses at least one complete chain, so the number of augmentations is at most the
     // sum of the chains' capacities (min u): the loop below stops after that many.
-    max_aug = lane_reduce<1>(max_aug, [](int64_t x, int64_t y) { return x + y; });
+    max_aug = B::all(max_aug, [](int64_t x, int64_t y) { return x + y; }, W.red);
     int ray_chain = -1, ray_p = -1, ray_q = -1;
     int64_t primal = 0;
 
@@ -742,8 +894,9 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
         }
         if (complete) { ray_p = bp; ray_q = bq; }
         else { ray_p = bp; ray_q = -1; }
-        for (int v = lane(); v <= n; v += kWave) W.alpha[v] = 0;
-        wave_lds_sync();
+        B::sync();   // every wave has walked its chain over dec before alpha (aliasing it) is zeroed
+        for (int v = tid; v <= n; v += T) W.alpha[v] = 0;
+        B::sync();
     } else {
         // 3. successive shortest paths (max reward) from the sources to the sinks
 #ifdef SGUFP_SUB_TRACE
@@ -765,7 +918,7 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
         bool warm = false;
         for (; status == kSubOptimal; iters++) {
             SUB_T0();
-            if (!bellman_ford<RG, WT>(N, W, nct, nz, kSsp, M, warm)) { status = kSubError; break; }
+            if (!bellman_ford<RG, WT, NW>(N, W, nct, nz, kSsp, M, warm)) { status = kSubError; break; }
             SUB_T1(t_bf);
 #ifdef SGUFP_SUB_VERIFY
             if (W.misc[6]) { status = kSubError; break; }
@@ -777,7 +930,7 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
             // round trip per arc: the entry holds the tail), then the wave takes the
             // bottleneck and augments (a simple path uses each chain once)
             SUB_T0();
-            if (lane() == 0) {
+            if (tid == 0) {
                 int v = n + 1, len = 0;
                 while (v != n && len < n + 2) {
                     const int32_t pr = W.pred[v];
@@ -787,10 +940,10 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
                 }
                 W.misc[3] = (v == n) ? len : -1;
             }
-            wave_lds_sync();
+            B::sync();
             const int plen = W.misc[3];
             int64_t delta = kInf;
-            for (int i = lane(); i < plen; i += kWave) {
+            for (int i = tid; i < plen; i += T) {
                 const int code = W.plist[i];
                 if (code >= 2 * m) continue;   // Z arcs: uncapacitated
                 const uint64_t cb = W.ctb[code >> 1];
@@ -798,9 +951,9 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
                 const int64_t cap = (code & 1) ? (x > L ? x - L : x) : (x < L ? L - x : U - x);
                 delta = cap < delta ? cap : delta;
             }
-            delta = lane_reduce<1>(delta, [](int64_t p, int64_t q) { return p < q ? p : q; });
+            delta = B::all(delta, [](int64_t p, int64_t q) { return p < q ? p : q; }, W.red);
             if (plen < 0 || delta <= 0 || delta >= kInf) { status = kSubError; break; }
-            for (int i = lane(); i < plen; i += kWave) {
+            for (int i = tid; i < plen; i += T) {
                 const int code = W.plist[i];
                 if (code >= 2 * m) continue;
                 const int k = code >> 1;
@@ -810,8 +963,8 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
                 *ch_xp(W, k) += (int16_t)((code & 1) ? -delta : delta);
                 if (cap == delta) W.key[(code & 1) ? ch_t(ca) : ch_h(ca)] = kInf;   // segment used up
             }
-            wave_lds_sync();
-            invalidate_subtrees(N, W);
+            B::sync();
+            invalidate_subtrees<NW>(N, W);
             warm = true;
             SUB_T1(t_walk);
 #ifdef SGUFP_SUB_TRACE
@@ -819,30 +972,31 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
 #endif
         }
 #ifdef SGUFP_SUB_TRACE
-        if (blockIdx.x % 997 == 0 && lane() == 0)
+        if (blockIdx.x % 997 == 0 && tid == 0)
             printf("SUB blk=%d nct=%d nz=%d aug=%d bf=%d passes=%d ticks=%llu t_bf=%llu t_pred=%llu t_walk=%llu\n",
                    (int)blockIdx.x, nct, nz, iters, nbf, W.misc[5], (unsigned long long)(wall_clock64() - tr0),
                    (unsigned long long)t_bf, (unsigned long long)t_pred, (unsigned long long)t_walk);
 #endif
         // lower bounds met?
         int unmet = 0;
-        for (int k = lane(); k < nct; k += kWave) {
+        for (int k = tid; k < nct; k += T) {
             const uint64_t ca = W.cta[k], cb = W.ctb[k];
             if (ch_t(ca) >= 0 && ch_h(ca) >= 0) {
                 if (ch_x(cb) < ch_L(cb)) unmet = 1;
                 primal += (int64_t)ch_R(ca) * ch_x(cb);
             }
         }
-        primal = lane_reduce<1>(primal, [](int64_t x, int64_t y) { return x + y; });
-        unmet = (int)wave_or((uint32_t)unmet);
+        primal = B::all(primal, [](int64_t x, int64_t y) { return x + y; }, W.red);
+        unmet = (int)B::any((uint32_t)unmet, W.red);
         if (status == kSubOptimal) {
             // 4. potentials of the final residual: plain costs (optimal duals) or big-M
             //    costs (their M-multiple is a dual ray, case (iii))
             const int mode = unmet ? kPotBigM : kPotPlain;
             if (unmet) status = kSubInfeasible;
-            if (!bellman_ford<RG, WT>(N, W, nct, nz, mode, M)) status = kSubError;
+            if (!bellman_ford<RG, WT, NW>(N, W, nct, nz, mode, M)) status = kSubError;
             const int64_t dz = key_cost(W.key[n]);
-            for (int v = lane(); v < n; v += kWave) {
+            B::sync();   // every thread read Z's key before the alphas overwrite it in place
+            for (int v = tid; v < n; v += T) {
                 int64_t d = key_cost(W.key[v]) - dz;
                 int64_t al;
                 if (mode == kPotPlain) al = -d;
@@ -852,7 +1006,7 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
                 }
                 W.alpha[v] = (N.inner[v] && !N.vbar[v]) ? al : 0;
             }
-            wave_lds_sync();
+            B::sync();
         }
     }
 
@@ -861,16 +1015,16 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
     bool ok = true;
     if (status != kSubError) {
         const bool ray = status == kSubInfeasible;
-        for (int k = lane(); k < nct; k += kWave) {
+        for (int k = tid; k < nct; k += T) {
             if (ray && ray_chain >= 0 && k != ray_chain) continue;   // (i)/(ii): only the bad chain
             ChainOut c = assemble_chain(N, W, io, poff, plen, k, s, ray, (k == ray_chain) ? ray_p : -1,
                                         (k == ray_chain) ? ray_q : -1, ok);
             rhs += c.rhs;
             dual += c.obj;
         }
-        rhs = lane_reduce<1>(rhs, [](int64_t x, int64_t y) { return x + y; });
-        dual = lane_reduce<1>(dual, [](int64_t x, int64_t y) { return x + y; });
-        ok = wave_or(ok ? 0u : 1u) == 0;
+        rhs = B::all(rhs, [](int64_t x, int64_t y) { return x + y; }, W.red);
+        dual = B::all(dual, [](int64_t x, int64_t y) { return x + y; }, W.red);
+        ok = B::any(ok ? 0u : 1u, W.red) == 0;
         if (ray && ray_chain >= 0 && ray_p >= 0 && ray_p == ray_q) {
             // single arc with l > u: beta = gamma = 1 on it
             const int64_t d0 = (int64_t)N.ub[so + ray_p] - N.lb[so + ray_p];
@@ -879,8 +1033,8 @@ __global__ void __launch_bounds__(kWave) k_sub_scenario(SubNet N, SubIO io) {
         }
         if (!ok || (ray ? dual >= 0 : dual != primal)) status = kSubError;
     }
-    wave_lds_sync();
-    if (lane() == 0) {
+    B::sync();
+    if (tid == 0) {
         io.status[b] = status;
         io.obj[b] = (double)primal;
         io.dual[b] = (double)dual;
@@ -942,26 +1096,29 @@ __global__ void __launch_bounds__(256) k_sub_reduce(SubNet N, SubIO io) {
 }
 
 // ---------------------------------------------------------------------------------------
-size_t sub_lds_bytes(int n, int m, int nct_cap, int nz) {
-    size_t off[10];
-    return sub_lds_layout(n, m, nct_cap, nz, off);
+size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw) {
+    size_t off[kSubLdsParts];
+    return sub_lds_layout(n, m, nct_cap, nz, nw, off);
 }
 
 hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st) {
     if (io.n_paths <= 0) return hipSuccess;
-    size_t lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz);
+    size_t lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, 1);
 #ifdef SGUFP_SUB_LDS_MIN
     if (lds < SGUFP_SUB_LDS_MIN) lds = SGUFP_SUB_LDS_MIN;   // occupancy experiments
 #endif
-    // register-resident chain groups: the large variant once the LDS footprint allows at
-    // most two waves per CU (its registers would cost the small networks their occupancy)
-    // and the big-M costs fit 32 bits (N.cost_bound, host)
-    if (lds > 64 * 1024 && io.nct_cap > kRegGroupsSmall * kWave && N.cost_bound < ((int64_t)1 << 30))
-        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsLarge, int32_t>), dim3((unsigned)io.n_paths * N.S), dim3(kWave), lds, st,
-                           N, io);
-    else
-        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsSmall, int64_t>), dim3((unsigned)io.n_paths * N.S), dim3(kWave), lds,
-                           st, N, io);
+    // the large variant (kLargeWaves waves per scenario, 32-bit costs in registers) once the
+    // LDS allows at most two scenarios per CU and the big-M costs fit 32 bits (host bound)
+    const bool large = lds > 64 * 1024 && io.nct_cap > kRegGroupsSmall * kWave && N.cost_bound < ((int64_t)1 << 30);
+    const char *ev = getenv("SGUFP_SUB_WAVES");
+    if (large && !(ev && atoi(ev) == 1)) {
+        lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, kLargeWaves);
+        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsLarge, int32_t, kLargeWaves>), dim3((unsigned)io.n_paths * N.S),
+                           dim3(kWave * kLargeWaves), lds, st, N, io);
+    } else {
+        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsSmall, int64_t, 1>), dim3((unsigned)io.n_paths * N.S), dim3(kWave),
+                           lds, st, N, io);
+    }
     hipLaunchKernelGGL(k_sub_reduce, dim3((unsigned)io.n_paths), dim3(256), 0, st, N, io);
     return hipGetLastError();
 }

@@ -13,7 +13,13 @@ namespace sgufp {
 #define LDS __attribute__((address_space(3)))
 #define GBL SGUFP_GBL
 
+// lane within the wave; translation units with multi-wave workgroups (SGUFP_MULTI_WAVE_TU)
+// mask the thread id, the single-wave ones use it as is
+#ifdef SGUFP_MULTI_WAVE_TU
+__device__ __forceinline__ int lane() { return (int)(threadIdx.x & (kWave - 1)); }
+#else
 __device__ __forceinline__ int lane() { return (int)threadIdx.x; }
+#endif
 // a wave-uniform value read from LDS / memory, moved to an SGPR (scalar branches and
 // address arithmetic instead of per-lane ones)
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
