@@ -76,7 +76,7 @@ struct SubLds {
 __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // One scenario per workgroup of NW waves.  NW = 1 on the 1k-arc networks (a single wave;
-// nine of them share a CU's LDS); NW = 4 on the large ones, whose LDS holds one scenario per
+// nine of them share a CU's LDS); NW = 8 on the large ones, whose LDS holds one scenario per
 // CU: the waves then share every per-chain / per-node loop, and a Bellman-Ford step relaxes
 // NW chain groups at once (see bf_sweep).
 template <int NW>
@@ -204,9 +204,14 @@ __device__ inline void for_residual(const SubNet &N, const SubLds &W, int nct, i
 // ((cost << 16) + 1) and which of the two arcs exist.  Flows only change between
 // Bellman-Fords, so the first RG groups of each wave live in registers for all its passes:
 // 16 groups (80 VGPRs) on the 1k-arc networks, whose small LDS footprint runs 9 waves per CU;
-// on the large ones (one scenario per CU, NW = 4 waves) 20 groups per wave with 32-bit
-// costs.  Groups beyond them are read from LDS (one group ahead of their use with one wave).
-constexpr int kRegGroupsSmall = 16, kRegGroupsLarge = 20, kLargeWaves = 4;
+// on the large ones (one scenario per CU, NW = 8 waves; C5, 4 paths x 512 scenarios: 1 / 2 /
+// 4 / 8 waves 2408 / 1549 / 918 / 732 ms) 80 / NW groups per wave with 32-bit costs.  Groups
+// beyond them are read from LDS (one group ahead of their use with one wave).
+#ifndef SGUFP_LARGE_WAVES
+#define SGUFP_LARGE_WAVES 8
+#endif
+constexpr int kLargeWaves = SGUFP_LARGE_WAVES;
+constexpr int kRegGroupsSmall = 16, kRegGroupsLarge = (80 + kLargeWaves - 1) / kLargeWaves;
 
 struct ChainArcs {
     uint32_t th;
