@@ -969,9 +969,11 @@ __global__ void __launch_bounds__(kWave * NW) k_sub_scenario(SubNet N, SubIO io)
                 if (cap == delta) W.key[(code & 1) ? ch_t(ca) : ch_h(ca)] = kInf;   // segment used up
             }
             B::sync();
+            SUB_T1(t_walk);
+            SUB_T0();
             invalidate_subtrees<NW>(N, W);
             warm = true;
-            SUB_T1(t_walk);
+            SUB_T1(t_pred);
 #ifdef SGUFP_SUB_TRACE
             nbf++;
 #endif
