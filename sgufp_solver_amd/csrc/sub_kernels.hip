@@ -2,7 +2,8 @@
 // GuroSolver::solveSubProblem(path) (/root/reference/grb.cpp:139-360), which the reference
 // solves as one Gurobi LP per scenario (the dual of a flow problem, grb.cpp:42-136).
 //
-// One 64-lane wave per (path, scenario):
+// One workgroup per (path, scenario): a single 64-lane wave on the 1k-arc networks, eight
+// waves on the large ones whose LDS holds one scenario per CU (Blk<NW> below):
 //   1. y-bar from the path (grb.cpp:139-150): at every V-bar node q each incoming arc is
 //      matched to the out-arc its DD layer decided, or to nothing (-1).
 //   2. Contraction.  The primal of the reference's dual is max sum r x over the network
