@@ -180,6 +180,8 @@ typedef struct {
     int32_t refine_iters;
     int32_t improved;            /* 1 if *incumbent rose */
     double ms_relax;             /* k_relax time of the round (sgufp_set_timing) */
+    int64_t deferred;            /* records whose refinement loop hit the round's limit and
+                                    went back on top of the frontier (sgufp_bnb_set_limits) */
 } sgufp_bnb_stats;
 
 int sgufp_frontier_clear(sgufp_ctx *ctx);
@@ -194,6 +196,11 @@ int sgufp_frontier_take_size(sgufp_ctx *ctx, int n, int from_bottom, int64_t *n_
 int sgufp_frontier_take(sgufp_ctx *ctx, int n, int from_bottom, uint16_t *gl, double *lb, double *ub,
                         int64_t *states_off, int16_t *states, int64_t *sol_off, int16_t *sol);
 int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_stats *stats);
+/* Bound the exact-leaf refinement loops of one sgufp_bnb_step: at most max_refine_iters
+ * iterations (subproblem batches) and round_seconds of wall time (0: no limit).  Records
+ * still in their loop are pushed back on top of the frontier with the bound reached; popped
+ * again they rebuild, apply the pool (their own new cuts included) and resume the loop. */
+int sgufp_bnb_set_limits(sgufp_ctx *ctx, int max_refine_iters, double round_seconds);
 /* Read back pool cuts [first, first + count) of one list (insertion order) as dense rows,
  * e.g. to all-gather the cuts a round produced to the other frontier shards. */
 int sgufp_cuts_rows(sgufp_ctx *ctx, int is_feasibility, int first, int count, double *rhs, double *rows);

@@ -16,6 +16,7 @@
 // of the reference may.  Children of a parent keep the reference's cutset order; parents
 // keep their frontier order, so the top of the stack is the last parent's first child.
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <numeric>
@@ -75,7 +76,18 @@ bool sgufp_ctx::frontier_reserve(int64_t entries, size_t sol_entries) {
     return true;
 }
 
+static double seconds_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 extern "C" {
+
+int sgufp_bnb_set_limits(sgufp_ctx *ctx, int max_refine_iters, double round_seconds) {
+    if (!ctx || max_refine_iters < 0 || !(round_seconds >= 0.0)) return SGUFP_ERR_ARG;
+    ctx->bnb_max_iters = max_refine_iters;
+    ctx->bnb_seconds = round_seconds;
+    return SGUFP_OK;
+}
 
 int sgufp_frontier_clear(sgufp_ctx *ctx) {
     if (!ctx) return SGUFP_ERR_ARG;
@@ -214,6 +226,7 @@ int sgufp_cuts_rows(sgufp_ctx *ctx, int is_feasibility, int first, int count, do
 int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_stats *stats) {
     if (!ctx || !incumbent) return SGUFP_ERR_ARG;
     sgufp_bnb_stats S{};
+    const auto t_round = std::chrono::steady_clock::now();
     const double z = *incumbent;
     const int64_t T = ctx->fr_n;
     if (T == 0) {
@@ -229,6 +242,7 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
     // 1-3: relax the top of the stack in place
     ctx->n = b;
     ctx->cur = ctx->frontier_slice(base, b);
+    ctx->restricted_done = false;
     if (!ctx->relax_current(z)) return SGUFP_ERR_HIP;
     std::vector<int32_t> st(b);
     std::vector<double> ub(b), lbv(b, -__DBL_MAX__);
@@ -269,11 +283,23 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
     }
     S.exact = (int64_t)act.size();
 
-    // 4: refinement loop of the exact DDs (NodeExplorer.cpp:946-969)
+    // 4: refinement loop of the exact DDs (NodeExplorer.cpp:946-969).  The loop of one record
+    // is a chain of dependent subproblems (one new cut per iteration); a round stops it after
+    // ctx->bnb_max_iters iterations or ctx->bnb_seconds, and the records still in their loop
+    // go back on top of the frontier (deferred).  Popped again, such a record rebuilds its DD
+    // and applies the whole pool -- its own new cuts included, so its bound is where the loop
+    // left it -- and resumes the loop: the first path is the last one found (its cut is in
+    // the pool, so the repeat costs one subproblem and then stops the loop as a seen path).
     std::vector<std::vector<std::vector<int16_t>>> seen(b);
     std::vector<uint16_t> plen(b);
     const size_t stride = (size_t)ctx->net.n_slots + 1;
+    std::vector<int> deferred;
     while (!act.empty()) {
+        if ((ctx->bnb_max_iters > 0 && S.refine_iters >= ctx->bnb_max_iters) ||
+            (ctx->bnb_seconds > 0 && seconds_since(t_round) >= ctx->bnb_seconds)) {
+            deferred.swap(act);
+            break;
+        }
         S.refine_iters++;
         if (!ctx->download(plen.data(), o.path_len, b) || !ctx->sync()) return SGUFP_ERR_HIP;
         const int na = (int)act.size();
@@ -343,6 +369,33 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
         }
     }
 
+    // deferred records: saved before the children overwrite the popped slice
+    const int nd = (int)deferred.size();
+    std::vector<uint16_t> d_gl(nd), d_len(nd);
+    std::vector<double> d_lb(nd), d_ub(nd);
+    std::vector<uint32_t> d_mask(nd);
+    std::vector<uint8_t> d_valid(nd);
+    std::vector<int64_t> d_soff(nd);
+    std::vector<std::vector<int16_t>> d_sol(nd);
+    {
+        FrontierDev &f = ctx->fr;
+        for (int i = 0; i < nd; i++) {
+            const int64_t e = base + deferred[i];
+            if (!ctx->download(&d_gl[i], f.gl + e, 1) || !ctx->download(&d_lb[i], f.lb + e, 1) ||
+                !ctx->download(&d_mask[i], f.mask + e, 1) || !ctx->download(&d_valid[i], f.valid + e, 1) ||
+                !ctx->download(&d_len[i], f.sol_len + e, 1) || !ctx->download(&d_soff[i], f.sol_off + e, 1))
+                return SGUFP_ERR_HIP;
+            d_ub[i] = ub[deferred[i]];   // the bound the loop reached (every pool cut is valid)
+        }
+        if (nd && !ctx->sync()) return SGUFP_ERR_HIP;
+        for (int i = 0; i < nd; i++) {
+            d_sol[i].resize(d_len[i]);
+            if (!ctx->download(d_sol[i].data(), f.sol + d_soff[i], d_len[i])) return SGUFP_ERR_HIP;
+        }
+        if (nd && !ctx->sync()) return SGUFP_ERR_HIP;
+    }
+    S.deferred = nd;
+
     // 5: incumbent (DDSolver.cpp:723-731)
     double znew = z;
     for (int k = 0; k < b; k++)
@@ -381,6 +434,29 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
     }
     ctx->fr_n = base + nc;
     ctx->fr_sol_top = ctx->fr_n ? sol_start + ns : 0;
+    if (nd) {
+        // the deferred records on top, in their frontier order: popped first next round
+        int64_t stot = 0;
+        for (int i = 0; i < nd; i++) stot += d_len[i];
+        const int64_t e0 = ctx->fr_n, s0 = ctx->fr_sol_top;
+        if (!ctx->frontier_reserve(e0 + nd, (size_t)(s0 + stot))) return SGUFP_ERR_HIP;
+        std::vector<int64_t> so(nd);
+        std::vector<int16_t> flat;
+        flat.reserve((size_t)stot);
+        for (int i = 0; i < nd; i++) {
+            so[i] = s0 + (int64_t)flat.size();
+            flat.insert(flat.end(), d_sol[i].begin(), d_sol[i].end());
+        }
+        FrontierDev &f = ctx->fr;
+        if (!ctx->upload(f.gl + e0, d_gl.data(), nd) || !ctx->upload(f.lb + e0, d_lb.data(), nd) ||
+            !ctx->upload(f.ub + e0, d_ub.data(), nd) || !ctx->upload(f.mask + e0, d_mask.data(), nd) ||
+            !ctx->upload(f.valid + e0, d_valid.data(), nd) || !ctx->upload(f.sol_len + e0, d_len.data(), nd) ||
+            !ctx->upload(f.sol_off + e0, so.data(), nd) || !ctx->upload(f.sol + s0, flat.data(), flat.size()) ||
+            !ctx->sync())
+            return SGUFP_ERR_HIP;
+        ctx->fr_n = e0 + nd;
+        ctx->fr_sol_top = s0 + stot;
+    }
     S.pushed = nc;
     S.frontier = ctx->fr_n;
     if (stats) *stats = S;

@@ -726,6 +726,7 @@ int sgufp_batch_upload(sgufp_ctx *ctx, int n, const uint16_t *gl, const double *
         return SGUFP_ERR_HIP;
     ctx->cur = ctx->staged();
     ctx->relaxed = false;
+    ctx->restricted_done = false;   // sgufp_restricted_* results belong to the previous batch
     return SGUFP_OK;
 }
 

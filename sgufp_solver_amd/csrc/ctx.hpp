@@ -105,6 +105,8 @@ struct sgufp_ctx {
     int perm_n = -1;                          // batch size d_perm was drawn for
     int64_t *d_boff = nullptr, *d_bsol = nullptr;  // [max_batch + 1]
     int16_t *d_bpaths = nullptr;              // [max_batch * Lcap] gathered paths
+    int bnb_max_iters = 0;                    // refinement iterations per round (0: no limit)
+    double bnb_seconds = 0.0;                 // refinement-loop seconds per round (0: no limit)
     bool relax_current(double optimal_lb);
     bool relax_order(BatchIn &in);
     void encode_records(int n, const uint16_t *gl, const int64_t *states_off, const int16_t *states,

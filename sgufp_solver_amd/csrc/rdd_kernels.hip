@@ -249,8 +249,10 @@ __global__ void __launch_bounds__(kWave, 2) k_restrict(NetDev net, BatchIn in, P
             wave_lds_sync();
             for (int k = 1; k <= TR; k++) {
                 const uint32_t wk = uni((uint32_t)W.lw[k]) == 255 ? 256u : uni((uint32_t)W.lw[k]);
-                if (lane() < RCB * pool.ustride) {
-                    const int cc = lane() / pool.ustride, r = lane() - cc * pool.ustride;
+                // RCB * ustride entries: up to 4 x 32 (network.cpp admits 32 states per set),
+                // more than the wave's lanes
+                for (int e = lane(); e < RCB * pool.ustride; e += kWave) {
+                    const int cc = e / pool.ustride, r = e - cc * pool.ustride;
                     W.ct[cc * pool.ustride + r] = coef(W.ids[cc], k, (uint32_t)r);
                 }
                 wave_lds_sync();

@@ -36,7 +36,7 @@
 #include <cstdint>
 
 #include "sub_device.hpp"
-#define SGUFP_MULTI_WAVE_TU   // k_sub_scenario runs 1 or 4 waves per workgroup
+#define SGUFP_MULTI_WAVE_TU   // k_sub_scenario runs 1 or kLargeWaves (8) waves per workgroup
 #include "wave.hpp"
 
 namespace sgufp {
@@ -212,6 +212,8 @@ __device__ inline void for_residual(const SubNet &N, const SubLds &W, int nct, i
 #define SGUFP_LARGE_WAVES 8
 #endif
 constexpr int kLargeWaves = SGUFP_LARGE_WAVES;
+// Blk<NW>::all and the chain-numbering scan write one `red` slot per wave (8 in the layout)
+static_assert(kLargeWaves >= 1 && kLargeWaves <= 8, "the cross-wave reduction array holds 8 waves");
 constexpr int kRegGroupsSmall = 16, kRegGroupsLarge = (80 + kLargeWaves - 1) / kLargeWaves;
 
 struct ChainArcs {
@@ -336,11 +338,15 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
                 }
                 __syncthreads();
             }
+            // fixed trip count with uniform guards: a data-dependent exit would keep the
+            // loop rolled (it holds a barrier) and index the register arrays dynamically,
+            // i.e. from scratch memory
 #pragma unroll
             for (int j = RG - 1; j >= 0; j--) {
-                if (j >= S) continue;
-                if (j * NW + wv < G) arc(C.th[j], reg_w(C.wb[j]), (C.bmask >> j) & 1ull, false);
-                __syncthreads();
+                if (j < S) {
+                    if (j * NW + wv < G) arc(C.th[j], reg_w(C.wb[j]), (C.bmask >> j) & 1ull, false);
+                    __syncthreads();
+                }
             }
             return changed;
         }
@@ -355,9 +361,10 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < RG; j++) {
-            if (j >= S) break;
-            if (j * NW + wv < G) arc(C.th[j], reg_w(C.wf[j]), (C.fmask >> j) & 1ull, true);
-            __syncthreads();
+            if (j < S) {
+                if (j * NW + wv < G) arc(C.th[j], reg_w(C.wf[j]), (C.fmask >> j) & 1ull, true);
+                __syncthreads();
+            }
         }
         for (int j = RG; j < S; j++) {
             const int g = j * NW + wv;
@@ -400,8 +407,7 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
         }
 #pragma unroll
         for (int g = RG - 1; g >= 0; g--) {
-            if (g >= G) continue;
-            arc(C.th[g], reg_w(C.wb[g]), (C.bmask >> g) & 1ull, false);
+            if (g < G) arc(C.th[g], reg_w(C.wb[g]), (C.bmask >> g) & 1ull, false);
         }
         return changed;
     }
@@ -417,8 +423,7 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
     wave_lds_sync();
 #pragma unroll
     for (int g = 0; g < RG; g++) {
-        if (g >= G) break;
-        arc(C.th[g], reg_w(C.wf[g]), (C.fmask >> g) & 1ull, true);
+        if (g < G) arc(C.th[g], reg_w(C.wf[g]), (C.fmask >> g) & 1ull, true);
     }
     if (!kPrefetch) {
         for (int g = RG; g < G; g++) {
@@ -630,110 +635,110 @@ __device__ inline int dec_of(const SubNet &N, const SubIO &io, int64_t poff, int
     return d;
 }
 
-// ray_mode: r = 0; e_target[m] given for every arc (only used when ray_mode)
+// ray_mode: r = 0; prescribed targets (ray_p / ray_q) for the chain that certifies an
+// infeasibility up front.  The chain is walked from its first arc over the decisions, twice
+// and without per-arc arrays (a lane's chain of up to 63 arcs would otherwise live in scratch
+// memory): the first walk gets its length, reward sum, binding arcs and the transfer total
+// of a broken start; the second emits e, the transfers of the matched pairs and sigma / phi,
+// in the order of the closed forms below (all integers: any summation order is exact).
 __device__ ChainOut assemble_chain(const SubNet &N, const SubLds &W, const SubIO &io, int64_t poff, int64_t plen,
                                    int k, int s, bool ray_mode, int ray_p, int ray_q, bool &ok) {
     ChainOut o{0, 0};
-    int arcs[kMaxChain];
-    int len = 0;
     const uint64_t ca = W.cta[k], cb = W.ctb[k];
-    for (int a = ch_first(cb); a >= 0 && len < kMaxChain;) {
-        arcs[len++] = a;
-        if (!N.vbar[N.head[a]]) break;
-        a = dec_of(N, io, poff, plen, a);
-    }
-    if (len >= kMaxChain) { ok = false; return o; }
     const int t = ch_t(ca), h = ch_h(ca);
     const size_t so = (size_t)s * N.m;
     auto rew = [&](int a) -> int64_t { return ray_mode ? 0 : (int64_t)N.reward[a]; };
     auto cost = [&](int a, int64_t e) -> int64_t { return e >= 0 ? (int64_t)N.ub[so + a] * e : (int64_t)N.lb[so + a] * e; };
-    int64_t e[kMaxChain];
-    for (int i = 0; i < len; i++) e[i] = 0;
-    const bool complete = t >= 0 && h >= 0;
-    // prescribed targets: the chain that certifies infeasibility up front ((i) / (ii))
+    // the arc after a in the chain, -1 at its end (head not V-bar, or no / no valid decision)
+    auto next = [&](int a) -> int {
+        if (!N.vbar[N.head[a]]) return -1;
+        const int d = dec_of(N, io, poff, plen, a);
+        return d >= 0 ? d : -1;
+    };
+    // prescribed targets: beta = 1 on the max-l arc (e - 1), gamma = 1 on the min-u arc (e + 1)
     const bool prescribed = ray_mode && ray_p >= 0;
-    if (prescribed) {
-        for (int i = 0; i < len; i++) {
-            if (arcs[i] == ray_p) e[i] -= 1;   // beta = 1 on the max-l arc
-            if (arcs[i] == ray_q) e[i] += 1;   // gamma = 1 on the min-u arc
-        }
+    auto pres = [&](int a) -> int64_t { return prescribed ? (int64_t)(a == ray_q) - (int64_t)(a == ray_p) : 0; };
+    // matched pair (a, b) at q = head(a) with transfer tt: lambda = max(tt, 0), mu = max(-tt, 0)
+    auto pair = [&](int a, int b, int64_t tt) {
+        const int64_t lam = tt > 0 ? tt : 0, mu = tt < 0 ? -tt : 0;
+        const int64_t v = (int64_t)N.ub[so + a] * lam + (int64_t)N.ub[so + b] * mu;
+        o.rhs += v;
+        add_coef(N, W, N.arc_layer[a], N.head[b], -v);
+    };
+    const int first = ch_first(cb);
+    // walk 1: length, sum r, first min-u / first max-l arc, sum_{i >= 1} (e_i - r_i)
+    int len = 0, bmin = 0, bmax = 0;
+    int64_t sumr = 0, dsum = 0, umin = 0, lmax = 0;
+    for (int a = first; a >= 0; a = next(a)) {
+        const int64_t u = N.ub[so + a], l = N.lb[so + a];
+        if (len == 0 || u < umin) { umin = u; bmin = len; }
+        if (len == 0 || l > lmax) { lmax = l; bmax = len; }
+        sumr += rew(a);
+        if (len > 0) dsum += pres(a) - rew(a);
+        if (++len >= kMaxChain) { ok = false; return o; }
     }
-    int64_t pair_t[kMaxChain];
+    const bool complete = t >= 0 && h >= 0;
     if (complete) {
-        // E on the binding arc
-        int64_t E = -alpha_of(N, W, h) + alpha_of(N, W, t);
-        for (int i = 0; i < len; i++) E += rew(arcs[i]);
-        if (!prescribed) {
-            int bind = 0;
-            for (int i = 1; i < len; i++) {
-                const int64_t ui = N.ub[so + arcs[i]], ub = N.ub[so + arcs[bind]];
-                const int64_t li = N.lb[so + arcs[i]], lb = N.lb[so + arcs[bind]];
-                if (E > 0 ? ui < ub : li > lb) bind = i;
+        // all of E = sum r - alpha(h) + alpha(t) on the binding arc (min u if E > 0, max l if
+        // E < 0); transfers t_i = r_i - e_i + t_{i-1} from t_0 = r_0 + alpha(t) - e_0
+        const int64_t E = sumr - alpha_of(N, W, h) + alpha_of(N, W, t);
+        const int bind = E > 0 ? bmin : bmax;
+        int64_t tp = 0;
+        for (int a = first, i = 0; a >= 0; i++) {
+            const int b = next(a);
+            int64_t e = pres(a);
+            if (!prescribed && i == bind && E != 0) e = E;
+            o.obj += cost(a, e);
+            if (b >= 0) {
+                tp = (i == 0) ? rew(a) + alpha_of(N, W, t) - e : rew(a) - e + tp;
+                pair(a, b, tp);
             }
-            if (E != 0) e[bind] = E;
-        }
-        if (len == 1) {
-            o.obj += cost(arcs[0], e[0]);
-        } else {
-            int64_t tp = rew(arcs[0]) + alpha_of(N, W, t) - e[0];   // P_1 = -alpha(t)
-            pair_t[0] = tp;
-            for (int i = 1; i < len - 1; i++) {
-                tp = rew(arcs[i]) - e[i] + tp;
-                pair_t[i] = tp;
-            }
-            for (int i = 0; i < len; i++) o.obj += cost(arcs[i], e[i]);
+            a = b;
         }
     } else if (h < 0) {
-        // broken end: forward transfers, sigma at the unmatched in-arc absorbs (e <= 0)
+        // broken end: forward transfers, sigma at the unmatched last in-arc absorbs (e <= 0)
         int64_t tp = 0;
-        for (int i = 0; i < len; i++) {
-            const int a = arcs[i];
+        for (int a = first, i = 0; a >= 0; i++) {
+            const int b = next(a);
             const int64_t P = (i == 0) ? -alpha_of(N, W, t) : 0;
-            if (i < len - 1) {
-                tp = rew(a) - P - e[i] + tp;
-                pair_t[i] = tp;
+            int64_t e = pres(a);
+            if (b >= 0) {
+                tp = rew(a) - P - e + tp;
+                pair(a, b, tp);
             } else {
-                const int64_t prev = (len >= 2) ? pair_t[len - 2] : 0;
-                const int64_t free_e = rew(a) - P + prev;     // e with sigma = 0
+                const int64_t free_e = rew(a) - P + tp;     // e with sigma = 0
                 int64_t sig;
-                if (prescribed) sig = free_e - e[i];
-                else { sig = free_e > 0 ? free_e : 0; e[i] = free_e - sig; }
+                if (prescribed) sig = free_e - e;
+                else { sig = free_e > 0 ? free_e : 0; e = free_e - sig; }
                 if (sig < 0) ok = false;
                 add_sigma(N, W, a, sig, s);
             }
-            o.obj += cost(a, e[i]);
+            o.obj += cost(a, e);
+            a = b;
         }
     } else {
-        // broken start only: backward transfers, phi at the unchosen out-arc absorbs
-        int64_t tn = 0;   // transfer after the current arc
-        for (int i = len - 1; i >= 0; i--) {
-            const int a = arcs[i];
-            const int64_t P = (i == len - 1) ? alpha_of(N, W, h) : 0;
-            if (i > 0) {
-                // e_i = r_i - P_i - (-t_{i-1} + t_i)  ->  t_{i-1} = e_i - r_i + P_i + t_i
-                const int64_t tprev = e[i] - rew(a) + P + tn;
-                pair_t[i - 1] = tprev;
-                tn = tprev;
-            } else {
-                const int64_t t1 = (len >= 2) ? pair_t[0] : 0;
-                const int64_t free_e = rew(a) - P - t1;         // e with phi = 0
+        // broken start only: backward transfers t_{j} = sum_{i > j} (e_i - r_i) + alpha(h),
+        // i.e. T - sum_{1 <= i <= j} (e_i - r_i); phi at the unchosen first out-arc absorbs
+        const int64_t T = len >= 2 ? dsum + alpha_of(N, W, h) : 0;
+        int64_t pre = 0;
+        for (int a = first, i = 0; a >= 0; i++) {
+            const int b = next(a);
+            int64_t e = pres(a);
+            if (i == 0) {
+                const int64_t P0 = (len == 1) ? alpha_of(N, W, h) : 0;
+                const int64_t free_e = rew(a) - P0 - T;       // e with phi = 0
                 int64_t ph;
-                if (prescribed) ph = free_e - e[0];
-                else { ph = free_e > 0 ? free_e : 0; e[0] = free_e - ph; }
+                if (prescribed) ph = free_e - e;
+                else { ph = free_e > 0 ? free_e : 0; e = free_e - ph; }
                 if (ph < 0) ok = false;
                 add_phi(N, W, a, ph, s);
+            } else {
+                pre += e - rew(a);
             }
+            o.obj += cost(a, e);
+            if (b >= 0) pair(a, b, T - pre);
+            a = b;
         }
-        for (int i = 0; i < len; i++) o.obj += cost(arcs[i], e[i]);
-    }
-    // matched pairs (a_i, a_{i+1}) at q = head(a_i): lambda = max(t, 0), mu = max(-t, 0)
-    for (int i = 0; i + 1 < len; i++) {
-        const int a = arcs[i], b = arcs[i + 1];
-        const int64_t tt = pair_t[i];
-        const int64_t lam = tt > 0 ? tt : 0, mu = tt < 0 ? -tt : 0;
-        const int64_t ua = N.ub[so + a], ubb = N.ub[so + b];
-        o.rhs += ua * lam + ubb * mu;
-        add_coef(N, W, N.arc_layer[a], N.head[b], -(ua * lam + ubb * mu));
     }
     o.rhs += o.obj;
     return o;

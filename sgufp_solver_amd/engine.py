@@ -31,7 +31,7 @@ EXPORTS = [
     "sgufp_cuts_append_rows", "sgufp_frontier_clear", "sgufp_frontier_size", "sgufp_frontier_push",
     "sgufp_frontier_take_size", "sgufp_frontier_take", "sgufp_bnb_step", "sgufp_cuts_rows",
     "sgufp_restricted_relax", "sgufp_restricted_results", "sgufp_restricted_paths", "sgufp_restricted_cutset_size",
-    "sgufp_restricted_cutset",
+    "sgufp_restricted_cutset", "sgufp_bnb_set_limits",
 ]
 
 
@@ -41,7 +41,7 @@ class BnbStats(C.Structure):
         "popped", "relaxed", "pruned_bound", "pruned_feasibility", "pruned_optimality", "exact", "exact_closed",
         "subproblems", "new_feasibility_cuts", "new_optimality_cuts", "children", "pushed", "frontier",
         "dd_nodes", "dd_arcs", "sweeps")] + [("refine_iters", C.c_int32), ("improved", C.c_int32),
-                                             ("ms_relax", C.c_double)]
+                                             ("ms_relax", C.c_double), ("deferred", C.c_int64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -102,6 +102,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.sgufp_frontier_take_size.argtypes = [P, C.c_int, C.c_int, P, P]
     lib.sgufp_frontier_take.argtypes = [P, C.c_int, C.c_int, P, P, P, P, P, P, P]
     lib.sgufp_bnb_step.argtypes = [P, C.c_int, P, P]
+    lib.sgufp_bnb_set_limits.argtypes = [P, C.c_int, C.c_double]
     lib.sgufp_cuts_rows.argtypes = [P, C.c_int, C.c_int, C.c_int, P, P]
     lib.sgufp_restricted_relax.argtypes = [P, C.c_int, C.c_double]
     lib.sgufp_restricted_results.argtypes = [P, P, P, P, P, P]
@@ -489,6 +490,11 @@ class Engine:
         st = BnbStats()
         self._check(self.lib.sgufp_bnb_step(self.ctx, int(max_nodes), C.byref(z), C.byref(st)))
         return z.value, st
+
+    def bnb_set_limits(self, max_refine_iters: int = 0, round_seconds: float = 0.0):
+        """Bound the refinement loops of one bnb_step (0: no limit); unfinished exact
+        records go back on top of the frontier."""
+        self._check(self.lib.sgufp_bnb_set_limits(self.ctx, int(max_refine_iters), C.c_double(round_seconds)))
 
     # -- convenience: NodeExplorer::process for a list of nodes ----------------
     def relax(self, nodes: Sequence[NodeRecord], incumbent: float) -> List[RelaxResult]:

@@ -9,7 +9,11 @@ subproblem (GuroSolver::solveSubProblem; k_sub_scenario), the new cut joins the 
 (NodeExplorer.cpp:650-664 / 736-748).  A record that converges returns
 {lowerBound, ...}: the value of a feasible routing, which raises the incumbent
 (DDSolver.cpp:723-731).  A false feasibility sweep or a bound <= optimalLB ends the record
-(INVALID_OBJECT).  The restricted DD is re-swept from scratch with the grown pool each
+(INVALID_OBJECT).  What is reproduced is the value of the exact-tree refinement only: in
+processX3's non-exact branch (NodeExplorer.cpp:698-793) a restricted infeasibility or a
+bound <= optimalLB still returns SUCCESS with the cutset and the relaxed DD decides the
+pruning; the heuristic here drops such records instead (it only seeds the incumbent).
+A record the device cannot represent (status 16) raises.  The restricted DD is re-swept from scratch with the grown pool each
 iteration; the outcome equals applying only the new cut (removals are a union, terminal
 weights a running minimum).
 """
@@ -46,6 +50,8 @@ class RestrictedExplorer:
             res = eng.restricted([records[k] for k in active], optimal_lb, self.width)
             nxt, paths = [], []
             for k, (st, ex, lb, path, kids) in zip(active, res):
+                if st >= 16:
+                    raise RuntimeError(f"restricted heuristic: record {k} failed on the device (status {st})")
                 if st != 0:
                     out[k] = RestrictedResult(st, lb, path, it, False)       # INVALID_OBJECT
                     continue

@@ -43,7 +43,7 @@ class DDSolver:
     def __init__(self, network_path: Optional[str] = None, n_workers: int = 1, device: int = 0,
                  max_batch: int = 4096, batch_nodes: int = 0, engine=None, group=None, verbose: bool = True,
                  progress: float = 0.0, max_rounds: int = 0, dive_batch: int = 64, time_budget: float = 0.0,
-                 restricted_width: int = 0):
+                 restricted_width: int = 0, round_seconds: float = 0.0, round_iters: int = 0):
         """n_workers is accepted for API compatibility with the reference (threads there);
         the parallelism here is the batch of ``batch_nodes`` (<= max_batch) records per
         round and one rank per GPU."""
@@ -70,6 +70,9 @@ class DDSolver:
         # NodeExplorer::processX3 (NodeExplorer.cpp:605-796) on the root record seeds the
         # incumbent with the value of the routing its refinement loop converges to
         self.restricted_width = restricted_width
+        # bound of one round's exact-leaf refinement loops (0: none; see Engine.bnb_set_limits)
+        self.round_seconds = round_seconds
+        self.round_iters = round_iters
         self.heuristic_incumbent = None
         self.complete = False
         self.counters = {}
@@ -146,24 +149,36 @@ class DDSolver:
         if rank == 0:
             eng.frontier_push([NodeRecord(0, DOUBLE_MIN, DOUBLE_MAX, [], [])])
         z = float(known_optimal)
+        # rows already shared: the heuristic's cuts below are new, so the first exchange
+        # sends them to every shard (the global pool, DDSolver.h:415-416)
+        marks = {1: eng.cuts_count(1), 0: eng.cuts_count(0)}
         if self.restricted_width > 0 and rank == 0:
             from .restricted import RestrictedExplorer
             h = RestrictedExplorer(eng, self.restricted_width).incumbent([NodeRecord(0, DOUBLE_MIN, DOUBLE_MAX, [], [])], z)
             self.heuristic_incumbent = h
             z = max(z, h)
-        marks = {1: eng.cuts_count(1), 0: eng.cuts_count(0)}
         keys = ("popped", "relaxed", "pruned_bound", "pruned_feasibility", "pruned_optimality", "exact",
-                "exact_closed", "subproblems", "new_feasibility_cuts", "new_optimality_cuts", "children", "pushed")
+                "exact_closed", "subproblems", "new_feasibility_cuts", "new_optimality_cuts", "children", "pushed",
+                "deferred")
         self.counters = {k: 0 for k in keys}
         self.rounds = 0
         t_last = time.perf_counter()
         diving = self.dive_batch > 0
         self.complete = False
         t_start = time.perf_counter()
+        limits = hasattr(eng, "bnb_set_limits")
         while True:
             batch = self.batch_nodes
             if diving:
                 batch = self.dive_batch if not batch else min(batch, self.dive_batch)
+            if limits:
+                # a round's refinement loops stop at the budget (or round_seconds); the
+                # unfinished exact records go back on top of the frontier
+                left = self.time_budget - (time.perf_counter() - t_start) if self.time_budget > 0 else 0.0
+                secs = self.round_seconds
+                if self.time_budget > 0:
+                    secs = max(1e-3, min(left, secs) if secs > 0 else left)
+                eng.bnb_set_limits(self.round_iters, secs)
             z, st = eng.bnb_step(z, batch)
             if diving and int(getattr(st, "exact", 0) if not isinstance(st, dict) else st["exact"]) > 0:
                 diving = False   # the dive reached exact leaves: cuts exist from here on
@@ -176,7 +191,7 @@ class DDSolver:
             if self.max_rounds and self.rounds >= self.max_rounds:
                 raise RuntimeError(f"DDSolver: no termination within {self.max_rounds} rounds (z={z!r})")
             for k in keys:
-                self.counters[k] += int(getattr(st, k) if not isinstance(st, dict) else st[k])
+                self.counters[k] += int(getattr(st, k, 0) if not isinstance(st, dict) else st.get(k, 0))
             over = self.time_budget > 0 and time.perf_counter() - t_start > self.time_budget
             if dist is None:
                 if eng.frontier_size() == 0:
