@@ -182,6 +182,7 @@ typedef struct {
     double ms_relax;             /* k_relax time of the round (sgufp_set_timing) */
     int64_t deferred;            /* records whose refinement loop hit the round's limit and
                                     went back on top of the frontier (sgufp_bnb_set_limits) */
+    int64_t resumed;             /* deferred records whose loop this round resumed */
 } sgufp_bnb_stats;
 
 int sgufp_frontier_clear(sgufp_ctx *ctx);
@@ -199,7 +200,8 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
 /* Bound the exact-leaf refinement loops of one sgufp_bnb_step: at most max_refine_iters
  * iterations (subproblem batches) and round_seconds of wall time (0: no limit).  Records
  * still in their loop are pushed back on top of the frontier with the bound reached; popped
- * again they rebuild, apply the pool (their own new cuts included) and resume the loop. */
+ * again they rebuild, apply the pool (their own new cuts included) and resume the loop with
+ * the paths it had seen (kept by the context until then; sgufp_frontier_clear drops them). */
 int sgufp_bnb_set_limits(sgufp_ctx *ctx, int max_refine_iters, double round_seconds);
 /* Read back pool cuts [first, first + count) of one list (insertion order) as dense rows,
  * e.g. to all-gather the cuts a round produced to the other frontier shards. */

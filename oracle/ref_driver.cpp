@@ -16,6 +16,9 @@
 //   ref_dd relax  <network> <cuts> <nodes> <incumbent-hex> <out>
 //   ref_dd bfs    <network> <cuts> <incumbent-hex> <max-nodes> <out-nodes>
 //   ref_dd time   <network> <cuts> <nodes> <incumbent-hex> <threads> <seconds>
+//   ref_dd relaxp <network> <cuts> <nodes> <incumbent-hex> <threads> <out>
+//                  (every node, static work queue over threads; timing JSON on stdout,
+//                   results in node order as "relax" writes them: CPU baseline + parity)
 //   ref_dd apply  <network> <cuts> <nodes> <out>     (per-cut trace, exact/non-exact alike)
 //   ref_dd restricted <network> <cuts> <nodes> <incumbent-hex> <width> <out>
 //                  (Inavap::RestrictedDDNew, DD.cpp:3090-3505, under the cut phases of
@@ -29,6 +32,7 @@
 #include "Network.h"
 #include "Cut.h"
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -356,6 +360,35 @@ int main(int argc, char **argv) {
         for (auto &th : pool) th.join();
         double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         std::printf("{\"relaxations\": %zu, \"seconds\": %.6f, \"threads\": %d}\n", done.load(), el, threads);
+        return 0;
+    }
+    if (mode == "relaxp" && argc == 8) {
+        Network net{argv[2]};
+        auto cuts = read_cuts(argv[3]);
+        auto nodes = read_nodes(argv[4]);
+        double inc = parse_double(argv[5]);
+        int threads = std::max(1, std::atoi(argv[6]));
+        std::vector<Result> res(nodes.size());
+        std::atomic<size_t> next{0};
+        auto t0 = std::chrono::steady_clock::now();
+        std::vector<std::thread> pool;
+        for (int t = 0; t < threads; t++) {
+            pool.emplace_back([&]() {
+                Inavap::RelaxedDDNew dd{&net};
+                for (;;) {
+                    size_t k = next.fetch_add(1);
+                    if (k >= nodes.size()) break;
+                    res[k] = process(dd, nodes[k], inc, cuts);
+                }
+            });
+        }
+        for (auto &th : pool) th.join();
+        double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        FILE *f = std::fopen(argv[7], "w");
+        std::fprintf(f, "%zu\n", nodes.size());
+        for (auto &r : res) write_result(f, r);
+        std::fclose(f);
+        std::printf("{\"relaxations\": %zu, \"seconds\": %.6f, \"threads\": %d}\n", nodes.size(), el, threads);
         return 0;
     }
     if (mode == "apply" && argc == 6) {

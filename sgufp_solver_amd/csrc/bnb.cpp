@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstring>
 #include <numeric>
+#include <string>
 #include <vector>
 
 #include "ctx.hpp"
@@ -89,10 +90,31 @@ int sgufp_bnb_set_limits(sgufp_ctx *ctx, int max_refine_iters, double round_seco
     return SGUFP_OK;
 }
 
+void sgufp_ctx::make_record_key(uint16_t gl, uint32_t mask, const int16_t *sol, size_t len, std::string &key) {
+    key.resize(6 + 2 * len);
+    std::memcpy(&key[0], &gl, 2);
+    std::memcpy(&key[2], &mask, 4);
+    if (len) std::memcpy(&key[6], sol, 2 * len);
+}
+
+bool sgufp_ctx::record_key(int64_t e, std::string &key) {
+    uint16_t gl = 0, len = 0;
+    uint32_t mask = 0;
+    int64_t so = 0;
+    if (!download(&gl, fr.gl + e, 1) || !download(&mask, fr.mask + e, 1) || !download(&len, fr.sol_len + e, 1) ||
+        !download(&so, fr.sol_off + e, 1) || !sync())
+        return false;
+    std::vector<int16_t> sol(len);
+    if (len && (!download(sol.data(), fr.sol + so, len) || !sync())) return false;
+    make_record_key(gl, mask, sol.data(), len, key);
+    return true;
+}
+
 int sgufp_frontier_clear(sgufp_ctx *ctx) {
     if (!ctx) return SGUFP_ERR_ARG;
     ctx->fr_n = 0;
     ctx->fr_sol_top = 0;
+    ctx->deferred_seen.clear();
     return SGUFP_OK;
 }
 
@@ -286,21 +308,27 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
     // 4: refinement loop of the exact DDs (NodeExplorer.cpp:946-969).  The loop of one record
     // is a chain of dependent subproblems (one new cut per iteration); a round stops it after
     // ctx->bnb_max_iters iterations or ctx->bnb_seconds, and the records still in their loop
-    // go back on top of the frontier (deferred).  Popped again, such a record rebuilds its DD
-    // and applies the whole pool -- its own new cuts included, so its bound is where the loop
-    // left it -- and resumes the loop: the first path is the last one found (its cut is in
-    // the pool, so the repeat costs one subproblem and then stops the loop as a seen path).
+    // go back on top of the frontier (deferred) with the paths they have seen.  Popped again,
+    // such a record rebuilds its DD, applies the pool (its own new cuts included, so its bound
+    // is where the loop left it) and resumes the loop with that seen list: the loop ends
+    // exactly where the uninterrupted one would (a path repeats), whatever happened between.
     std::vector<std::vector<std::vector<int16_t>>> seen(b);
     std::vector<uint16_t> plen(b);
     const size_t stride = (size_t)ctx->net.n_slots + 1;
     std::vector<int> deferred;
-    while (!act.empty()) {
-        if ((ctx->bnb_max_iters > 0 && S.refine_iters >= ctx->bnb_max_iters) ||
-            (ctx->bnb_seconds > 0 && seconds_since(t_round) >= ctx->bnb_seconds)) {
-            deferred.swap(act);
-            break;
+    if (!act.empty() && !ctx->deferred_seen.empty()) {
+        for (int k : act) {
+            std::string key;
+            if (!ctx->record_key(base + k, key)) return SGUFP_ERR_HIP;
+            auto it = ctx->deferred_seen.find(key);
+            if (it != ctx->deferred_seen.end()) {
+                seen[k] = std::move(it->second);
+                ctx->deferred_seen.erase(it);
+                S.resumed++;
+            }
         }
-        S.refine_iters++;
+    }
+    while (!act.empty()) {
         if (!ctx->download(plen.data(), o.path_len, b) || !ctx->sync()) return SGUFP_ERR_HIP;
         const int na = (int)act.size();
         std::vector<int64_t> off(na + 1, 0);
@@ -325,11 +353,18 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
             }
             paths.insert(paths.end(), p.begin(), p.end());
             poff.push_back((int64_t)paths.size());
-            sv.push_back(std::move(p));
             fresh.push_back(k);
         }
         act.clear();
         if (fresh.empty()) break;
+        if ((ctx->bnb_max_iters > 0 && S.refine_iters >= ctx->bnb_max_iters) ||
+            (ctx->bnb_seconds > 0 && seconds_since(t_round) >= ctx->bnb_seconds)) {
+            deferred.swap(fresh);    // their current path is unseen: solved when resumed
+            break;
+        }
+        S.refine_iters++;
+        for (size_t i = 0; i < fresh.size(); i++)
+            seen[fresh[i]].emplace_back(paths.begin() + poff[i], paths.begin() + poff[i + 1]);
         const int nf = (int)fresh.size();
         std::vector<int32_t> type(nf);
         std::vector<double> rhs(nf), rows((size_t)nf * stride);
@@ -393,6 +428,11 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
             if (!ctx->download(d_sol[i].data(), f.sol + d_soff[i], d_len[i])) return SGUFP_ERR_HIP;
         }
         if (nd && !ctx->sync()) return SGUFP_ERR_HIP;
+        for (int i = 0; i < nd; i++) {
+            std::string key;
+            sgufp_ctx::make_record_key(d_gl[i], d_mask[i], d_sol[i].data(), d_len[i], key);
+            ctx->deferred_seen[key] = std::move(seen[deferred[i]]);
+        }
     }
     S.deferred = nd;
 

@@ -105,6 +105,11 @@ struct sgufp_ctx {
     int perm_n = -1;                          // batch size d_perm was drawn for
     int64_t *d_boff = nullptr, *d_bsol = nullptr;  // [max_batch + 1]
     int16_t *d_bpaths = nullptr;              // [max_batch * Lcap] gathered paths
+    // seen-path lists of records whose refinement loop a round deferred, keyed by the
+    // record (gl, state mask, solution): restored when the record is popped again
+    std::unordered_map<std::string, std::vector<std::vector<int16_t>>> deferred_seen;
+    static void make_record_key(uint16_t gl, uint32_t mask, const int16_t *sol, size_t len, std::string &key);
+    bool record_key(int64_t entry, std::string &key);
     int bnb_max_iters = 0;                    // refinement iterations per round (0: no limit)
     double bnb_seconds = 0.0;                 // refinement-loop seconds per round (0: no limit)
     bool relax_current(double optimal_lb);

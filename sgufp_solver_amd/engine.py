@@ -41,7 +41,8 @@ class BnbStats(C.Structure):
         "popped", "relaxed", "pruned_bound", "pruned_feasibility", "pruned_optimality", "exact", "exact_closed",
         "subproblems", "new_feasibility_cuts", "new_optimality_cuts", "children", "pushed", "frontier",
         "dd_nodes", "dd_arcs", "sweeps")] + [("refine_iters", C.c_int32), ("improved", C.c_int32),
-                                             ("ms_relax", C.c_double), ("deferred", C.c_int64)]
+                                             ("ms_relax", C.c_double), ("deferred", C.c_int64),
+                                             ("resumed", C.c_int64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

@@ -36,8 +36,6 @@ import numpy as np
 
 from .pools import DOUBLE_MAX, DOUBLE_MIN, NodeRecord
 
-STEAL_SHARE = 0.4   # PROPORTION_OF_SHARE (DDSolver.h:22-38)
-
 
 class DDSolver:
     def __init__(self, network_path: Optional[str] = None, n_workers: int = 1, device: int = 0,
@@ -78,72 +76,27 @@ class DDSolver:
         self.counters = {}
         self.rounds = 0
         self.seconds = 0.0
+        self.shard_comm = None
+        self.received = 0
 
     # -- collectives ---------------------------------------------------------------
-    def _dist(self):
+    def _comm(self):
+        """ShardComm over the group (None with one rank)."""
         import torch.distributed as dist
         if not dist.is_available() or not dist.is_initialized():
             return None
         if dist.get_world_size(self.group) == 1:
             return None
-        return dist
-
-    def _allreduce_max(self, dist, z: float) -> float:
-        import torch
-        dev = "cuda" if dist.get_backend(self.group) == "nccl" else "cpu"
-        t = torch.tensor([z], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-        return float(t.item())
-
-    def _exchange_cuts(self, dist, marks):
-        """All-gather the cut rows appended locally since the last exchange; append the
-        other ranks' rows in rank order.  marks[t] = rows of list t already shared."""
-        mine = {}
-        for t in (1, 0):
-            n = self.eng.cuts_count(t)
-            mine[t] = self.eng.cut_rows(t, marks[t], n - marks[t]) if n > marks[t] else None
-        world = dist.get_world_size(self.group)
-        me = dist.get_rank(self.group)
-        got = [None] * world
-        dist.all_gather_object(got, mine, group=self.group)
-        for r in range(world):
-            if r == me:
-                continue
-            for t in (1, 0):
-                if got[r][t] is not None and len(got[r][t][0]):
-                    self.eng.add_cut_rows(t, got[r][t][0], got[r][t][1])
-        for t in (1, 0):
-            marks[t] = self.eng.cuts_count(t)
-
-    def _rebalance(self, dist, sizes):
-        """Shards with an empty stack get records from the largest shard (its oldest
-        records, i.e. the shallowest subtrees)."""
-        world = len(sizes)
-        me = dist.get_rank(self.group)
-        empty = [r for r in range(world) if sizes[r] == 0]
-        donor = int(np.argmax(sizes))
-        if not empty or sizes[donor] < 2:
-            return
-        give = max(1, int(sizes[donor] * STEAL_SHARE))
-        payload = [None]
-        if me == donor:
-            taken = self.eng.frontier_take(give, from_bottom=True)
-            payload = [taken]
-        dist.broadcast_object_list(payload, src=donor, group=self.group)
-        taken = payload[0]
-        if me in empty:
-            k = empty.index(me)
-            idx = np.arange(k, taken.n, len(empty))
-            if len(idx):
-                from .engine import batch_slice
-                self.eng.frontier_push(batch_slice(taken, idx))
+        from .shards import ShardComm
+        return ShardComm(self.group)
 
     # -- the solver -------------------------------------------------------------------
     def start_solver(self, known_optimal: float) -> float:
         """DDSolver::startSolver (DDSolver.cpp:782-846): incumbent := known_optimal, the root
         record Node{} on the frontier (rank 0), rounds until every shard is empty."""
-        dist = self._dist()
-        rank = dist.get_rank(self.group) if dist else 0
+        comm = self._comm()
+        self.shard_comm = comm
+        rank = comm.rank if comm else 0
         eng = self.eng
         eng.frontier_clear()
         if rank == 0:
@@ -159,8 +112,9 @@ class DDSolver:
             z = max(z, h)
         keys = ("popped", "relaxed", "pruned_bound", "pruned_feasibility", "pruned_optimality", "exact",
                 "exact_closed", "subproblems", "new_feasibility_cuts", "new_optimality_cuts", "children", "pushed",
-                "deferred")
+                "deferred", "resumed")
         self.counters = {k: 0 for k in keys}
+        self.received = 0     # records received from other shards (work sharing)
         self.rounds = 0
         t_last = time.perf_counter()
         diving = self.dive_batch > 0
@@ -193,25 +147,23 @@ class DDSolver:
             for k in keys:
                 self.counters[k] += int(getattr(st, k, 0) if not isinstance(st, dict) else st.get(k, 0))
             over = self.time_budget > 0 and time.perf_counter() - t_start > self.time_budget
-            if dist is None:
+            if comm is None:
                 if eng.frontier_size() == 0:
                     self.complete = True
                     break
                 if over:
                     break
                 continue
-            z = self._allreduce_max(dist, z)
-            self._exchange_cuts(dist, marks)
-            sizes = [None] * dist.get_world_size(self.group)
-            dist.all_gather_object(sizes, eng.frontier_size(), group=self.group)
+            z = comm.allreduce_max(z)
+            comm.exchange_cuts(eng, marks)
+            g = comm.allgather_i64([eng.frontier_size(), 1 if over else 0])
+            sizes = [int(x) for x in g[:, 0]]
             if sum(sizes) == 0:
                 self.complete = True
                 break
-            flags = [None] * dist.get_world_size(self.group)
-            dist.all_gather_object(flags, over, group=self.group)
-            if any(flags):
+            if g[:, 1].any():
                 break
-            self._rebalance(dist, sizes)
+            self.received += comm.rebalance(eng, sizes)
         return z
 
     def start(self, known_opt: float, solver_counters: bool = False):
@@ -223,17 +175,17 @@ class DDSolver:
         self.seconds = time.perf_counter() - t0
         # "Explored N nodes" = sum of nQueue = children produced (DDSolver.cpp:742, 856-865)
         explored = self.counters.get("children", 0)
-        dist = self._dist()
+        comm = self.shard_comm
         per_rank = [dict(self.counters)]
-        if dist is not None:
-            tot = [None] * dist.get_world_size(self.group)
-            dist.all_gather_object(tot, explored, group=self.group)
-            explored = sum(tot)
-            per_rank = [None] * dist.get_world_size(self.group)
-            dist.all_gather_object(per_rank, dict(self.counters), group=self.group)
-        if self.verbose and solver_counters and (dist is None or dist.get_rank(self.group) == 0):
+        if comm is not None:
+            keys = sorted(self.counters)
+            g = comm.allgather_i64([int(self.counters[k]) for k in keys])
+            per_rank = [{k: int(v) for k, v in zip(keys, row)} for row in g]
+            explored = sum(c.get("children", 0) for c in per_rank)
+        first = comm is None or comm.rank == 0
+        if self.verbose and solver_counters and first:
             print(worker_stats_text(per_rank, self.eng.cuts_count(1), self.eng.cuts_count(0)), end="")
-        if self.verbose and (dist is None or dist.get_rank(self.group) == 0):
+        if self.verbose and first:
             print(f"Optimal solution: {solution}. Explored {explored} nodes (entire search space) in "
                   f"{self.seconds} seconds.")
         return solution, self.seconds

@@ -61,6 +61,20 @@ def test_bnb_batch_size_does_not_change_the_optimum(batch):
         assert solver.rounds == solver.counters["popped"]
 
 
+@pytest.mark.parametrize("iters,batch", [(1, 64), (2, 3)])
+def test_bnb_deferred_refinement_keeps_the_optimum(iters, batch):
+    """Rounds whose refinement loops stop after `iters` subproblem batches
+    (sgufp_bnb_set_limits): the unfinished exact records go back on top of the frontier,
+    resume when popped again, and the search still ends at the extensive-form optimum."""
+    inst, path = _inst("T4", 3, 3)
+    opt = ef.solve(inst)
+    solver = DDSolver(path, max_batch=256, batch_nodes=batch, max_rounds=200000, verbose=False, round_iters=iters)
+    sol, _ = solver.start(DOUBLE_MIN)
+    solver.eng.close()
+    assert abs(sol - opt) <= TOL * max(1.0, abs(opt))
+    assert solver.counters["deferred"] > 0
+
+
 def _records(eng, n):
     """n real open-node records: root cutset children of a C2 instance."""
     eng.upload([NodeRecord(0, DOUBLE_MIN, DOUBLE_MAX, [], [])])

@@ -129,7 +129,8 @@ def _worker(rank, world, port, q):
     eng = ToyEngine()
     solver = DDSolver(engine=eng, batch_nodes=3, verbose=False)
     z = solver.start_solver(-1.0)
-    q.put((rank, z, sorted(eng.cuts[0]), sorted(eng.cuts[1]), eng.closed, solver.counters, solver.rounds))
+    q.put((rank, z, sorted(eng.cuts[0]), sorted(eng.cuts[1]), eng.closed, solver.counters, solver.rounds,
+           solver.received))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -156,7 +157,7 @@ def test_multi_rank_solver_protocol(world):
         assert p.exitcode == 0
     opt = brute()
     res.sort()
-    for rank, z, c0, c1, closed, counters, rounds in res:
+    for rank, z, c0, c1, closed, counters, rounds, received in res:
         assert z == opt, (rank, z, opt)
     # identical global pools on every rank (all-gathered rows)
     assert all(r[2] == res[0][2] and r[3] == res[0][3] for r in res)
@@ -164,6 +165,50 @@ def test_multi_rank_solver_protocol(world):
     leaves = [t for r in res for t in r[4]]
     assert len(leaves) == len(set(leaves))
     assert sum(1 for r in res if r[5]["relaxed"] > 0) == world
+
+
+def test_work_sharing_balances_shards():
+    """World 3, every record starts on rank 0: ranks 1 and 2 run dry and are fed from every
+    busy shard (40 % of a stack of >= 32 from its bottom, m_pop; half of a smaller one), so
+    both receive records and the relaxed counts end up within 1.5x of each other."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 3
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    relaxed = [r[5]["relaxed"] for r in res]
+    received = [r[7] for r in res]
+    assert received[1] > 0 and received[2] > 0, received
+    assert max(relaxed) <= 1.5 * min(relaxed), relaxed
+
+
+def test_work_sharing_plan():
+    """give counts follow m_pop(0.4) from 32 records up, the half split below; idle ranks
+    are the empty ones; nothing moves while no shard is idle."""
+    from sgufp_solver_amd.shards import give_count, plan
+    assert give_count(100) == 100 - int(100 * 0.6) == 40
+    assert give_count(32) == 32 - int(32 * 0.6) == 13
+    assert give_count(31) == 15 and give_count(2) == 1 and give_count(1) == 0
+    assert plan([5, 7]) == ([], [])
+    assert plan([0, 100, 3, 0]) == ([(1, 40), (2, 1)], [0, 3])
+
+
+def test_record_pack_roundtrip():
+    from sgufp_solver_amd.shards import pack_batch, unpack_batch
+    recs = [NodeRecord(3, -1.5, 7.25, [1, 4], [2, -1, 5]), NodeRecord(0, -1e300, 1e300, [], []),
+            NodeRecord(9, 0.0, 2.0, [-1, 3, 8], [1] * 9)]
+    b = unpack_batch(pack_batch(BatchArrays(recs)))
+    assert b.n == 3
+    for k, r in enumerate(recs):
+        assert int(b.gl[k]) == r.gl and b.lb[k] == r.lb and b.ub[k] == r.ub
+        assert list(b.states[b.states_off[k]:b.states_off[k + 1]]) == r.states
+        assert list(b.sol[b.sol_off[k]:b.sol_off[k + 1]]) == r.sol
 
 
 def test_single_rank_toy_matches_brute_force():

@@ -20,8 +20,9 @@ TOL = 1e-9
 
 
 def _net(cfg, seed, S, zero_lb=False):
-    """Seeded instance; zero_lb drops the sink-arc lower bounds so that most matchings
-    are feasible (optimality cuts), otherwise many scenarios are infeasible (feasibility cuts)."""
+    """Seeded instance (S None: the config's scenario count); zero_lb drops the sink-arc
+    lower bounds so that most matchings are feasible (optimality cuts), otherwise many
+    scenarios are infeasible (feasibility cuts)."""
     from sgufp_solver_amd import engine as E
     inst = instance.generate(instance.CONFIGS[cfg], seed, scenarios=S)
     if zero_lb:
@@ -166,6 +167,65 @@ def test_subproblem_matches_highs(cfg, seed, S, zl, trials):
         assert "opt" in seen            # optimality cuts exercised
     else:
         assert "feas" in seen           # feasibility rays exercised
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,seed,zl,n_paths,sample", [("C4", 1, True, 3, 16), ("C4", 2, False, 3, 16),
+                                                        ("C5", 1, True, 2, 6), ("C5", 2, False, 2, 6)])
+def test_subproblem_at_benchmark_scenario_counts(cfg, seed, zl, n_paths, sample):
+    """BASELINE configs[3] / [4] scenario counts (S = 256 on C4, 512 on C5).  Every scenario
+    runs on the device and the reduce runs over all S (grb.cpp:174-351: 1/S-weighted sum, or
+    the first infeasible scenario's ray); HiGHS checks a sampled subset of the scenarios plus
+    the first infeasible one.  The cut's value at y-bar equals the mean of all S device
+    objectives (tightness, so the 1/S reduction over every scenario is exact), and on C4 the
+    first optimality cut is valid at another matching (all 256 scenario LPs of HiGHS)."""
+    from sgufp_solver_amd import engine as E
+    inst, path, net = _net(cfg, seed, None, zl)
+    S = net.S
+    assert S == instance.CONFIGS[cfg].scenarios
+    eng = E.Engine(path, 0, 64)
+    keys = _keys(eng)
+    rng = np.random.default_rng(300 + seed)
+    ys = [_full_matching(net, rng, 1.0) for _ in range(n_paths)]
+    paths = [_path_of(inst, net, y) for y in ys]
+    typ, rhs, rows, obj_mean = eng.subproblem(paths)
+    st, obj, dual = eng.subproblem_detail(len(paths))
+    eng.close()
+    kinds = set()
+    for k, y in enumerate(ys):
+        assert (st[k] != 2).all(), f"path {k}: device error in scenarios {np.nonzero(st[k] == 2)[0][:8]}"
+        inf = np.nonzero(st[k] == 1)[0]
+        first_inf = int(inf[0]) if inf.size else None
+        check = set(int(x) for x in rng.choice(S if first_inf is None else first_inf + 1,
+                                               size=min(sample, S if first_inf is None else first_inf + 1),
+                                               replace=False))
+        if first_inf is not None:
+            check.add(first_inf)
+        for s in sorted(check):
+            ws, wo = so.dual_lp(net, y, s)[:2]
+            assert st[k, s] == (0 if ws == "optimal" else 1), (k, s, st[k, s], ws)
+            if ws == "optimal":
+                assert abs(obj[k, s] - wo) <= TOL * max(1.0, abs(wo)), (k, s, obj[k, s], wo)
+                assert dual[k, s] == obj[k, s]
+        if first_inf is None:
+            kinds.add("opt")
+            assert typ[k] == 0
+            mean = float(np.sum(obj[k])) / S
+            assert abs(obj_mean[k] - mean) <= TOL * max(1.0, abs(mean))
+            v = _cut_at(rhs[k], rows[k], keys, y)
+            assert abs(v - mean) <= 1e-7 * max(1.0, abs(mean)), (v, mean)
+            if cfg == "C4" and "valid" not in kinds:     # one path: 256 HiGHS LPs (~25 s)
+                kinds.add("valid")
+                y2 = _full_matching(net, rng, 0.9)
+                q2 = [so.dual_lp(net, y2, s)[:2] for s in range(S)]
+                if all(w == "optimal" for w, _ in q2):
+                    m2 = sum(o for _, o in q2) / S
+                    assert _cut_at(rhs[k], rows[k], keys, y2) >= m2 - 1e-7 * max(1.0, abs(m2))
+        else:
+            kinds.add("feas")
+            assert typ[k] == 1
+            assert _cut_at(rhs[k], rows[k], keys, y) < 0
+    assert ("opt" in kinds) if zl else ("feas" in kinds)
 
 
 @pytest.mark.gpu
