@@ -12,9 +12,18 @@ NEEDS_SUBPROBLEM, argmax path written) -- see DESIGN.md.
 Workload (config C4): seeded layered instance with 1000 arcs and 256
 scenarios, 16F + 64O synthetic cuts (tests2.cpp:259-286 recipe), a BFS frontier of
 open nodes from the root, incumbent = 40th percentile of the frontier's bounds.
-With N ranks every rank relaxes its own slice of a frontier N times as large
-(weak scaling, no collective on the data path; the per-step time is the max over
-ranks).
+With N ranks every rank relaxes its own slice of a frontier N times as large (weak
+scaling) and every step ends with the B&B round's exchanges over RCCL: the incumbent
+all-reduce(MAX) and the all-gather of the round's new cut rows (shards.py); the
+per-step time is the max over ranks.
+
+Beside the headline the line carries: `parity` (the timed step's results for the first
+--cpu-sample records against the reference's own RelaxedDDNew on the same records, bit for
+bit), `cpu_baseline` (that reference run's rate on the host cores), `roofline` (PMC-counted
+HBM bytes of this build per k_relax launch), `subproblem` (the scenario LP kernels alone),
+`bnb` (the device B&B with its exact-leaf subproblems on the same 256-scenario network) and
+`config5` (BASELINE configs[4]: 5k arcs, 512 scenarios, relaxation + subproblem + B&B with
+cut generation).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 the driver uses
 torch.distributed.run and this script reads RANK / LOCAL_RANK / WORLD_SIZE.
@@ -52,7 +61,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-sample", type=int, default=2048)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--profile-tag", default="r02")
+    ap.add_argument("--profile-tag", default="r03")
     ap.add_argument("--sub-paths", type=int, default=32, help="subproblem leg: random full-matching paths (0: skip)")
     ap.add_argument("--cpu-sub-seconds", type=float, default=8.0)
     ap.add_argument("--c5-nodes", type=int, default=1024,
@@ -65,6 +74,13 @@ def parse():
     ap.add_argument("--bnb-lb", choices=["zero", "gen"], default="zero",
                     help="zero: drop the generator's sink lower bounds so the instance is feasible and "
                          "incumbents / optimality cuts appear (with them most C3 paths are infeasible)")
+    ap.add_argument("--round-seconds", type=float, default=5.0,
+                    help="B&B: a round's exact-leaf refinement loops are deferred after this many seconds")
+    ap.add_argument("--bnb-leg-seconds", type=float, default=20.0,
+                    help="headline line: seconds of the C4 / 256-scenario B&B leg (0: skip)")
+    ap.add_argument("--c5-bnb-seconds", type=float, default=30.0,
+                    help="config-5 leg: seconds of the C5 / 512-scenario B&B with cut generation (0: skip)")
+    ap.add_argument("--no-parity", action="store_true", help="skip the reference parity check of the timed batch")
     return ap.parse_args()
 
 
@@ -128,12 +144,65 @@ def pmc_traffic(tag: str, workload: str, kernel: str = "k_relax"):
     return (FETCH_CORRECTION * np.mean(f) + np.mean(w)) * 1024.0, src
 
 
+def bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, work, device=0, progress=10.0, tag="bnb"):
+    """The device DDSolver (sgufp_bnb_step rounds) from the root record Node{} with no
+    incumbent, after a short warm-up search (kernels, allocations; its pool is cleared):
+    relaxations = NodeExplorer::process calls, exact-leaf refinement loops with the device
+    subproblem included; a round's loops stop after round_seconds (deferred, resumed later)."""
+    from sgufp_solver_amd import instance
+    from sgufp_solver_amd.pools import DOUBLE_MIN
+    from sgufp_solver_amd.solver import DDSolver
+    cfg = instance.CONFIGS[cfg_name]
+    inst = instance.generate(cfg, seed)
+    if lb_mode == "zero":
+        inst.lb[:] = 0
+    net = os.path.join(work, f"{tag}_{cfg_name}.txt")
+    inst.write(net)
+    solver = DDSolver(net, device=device, max_batch=batch, verbose=False, time_budget=2.0, progress=progress,
+                      round_seconds=min(round_seconds, 2.0))
+    solver.start_solver(DOUBLE_MIN)                        # warm-up
+    solver.eng.clear_cuts()
+    solver.eng.set_timing(True)
+    solver.time_budget = budget
+    solver.round_seconds = round_seconds
+    import torch
+    if solver.shard_comm is not None:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    z = solver.start_solver(DOUBLE_MIN)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    c = dict(solver.counters)
+    world = 1
+    if solver.shard_comm is not None:
+        comm = solver.shard_comm
+        world = comm.world
+        keys = sorted(c)
+        g = comm.allgather_i64([int(c[k]) for k in keys] + [int(elapsed * 1e6)])
+        c = {k: int(v) for k, v in zip(keys, g[:, :-1].sum(axis=0))}
+        elapsed = float(g[:, -1].max()) / 1e6
+    out = {
+        "workload": f"{cfg_name}: {cfg.n_arcs}-arc layered network, {inst.scenarios} scenarios"
+                    f"{' (lower bounds 0)' if lb_mode == 'zero' else ''}, root record, no incumbent, "
+                    f"up to {batch} records per round, refinement loops deferred after {round_seconds} s per round",
+        "instance_seed": seed, "total_layers": int(solver.eng.info.total_layers), "n_gpus": world,
+        "relaxations_per_s": round(c["relaxed"] / elapsed, 2),
+        "subproblems_per_s": round(c["subproblems"] / elapsed, 2),
+        "scenario_lps_per_s": round(c["subproblems"] * inst.scenarios / elapsed, 1),
+        "cuts_generated": int(c["new_feasibility_cuts"] + c["new_optimality_cuts"]),
+        "seconds": round(elapsed, 3), "rounds": solver.rounds, "complete": solver.complete, "incumbent": z,
+        "frontier_left": solver.eng.frontier_size(),
+        "pool": [solver.eng.cuts_count(1), solver.eng.cuts_count(0)], "counters": c,
+    }
+    solver.eng.close()
+    return out
+
+
 def bnb_main(args):
-    """Full B&B on the device (BASELINE configs[2]: 1k-arc network, 64 scenarios): the
-    DDSolver from the root record Node{} with no incumbent, for --bnb-seconds after a short
-    warm-up run; relaxations/s = NodeExplorer::process calls (exact-leaf refinement loops
-    with the device subproblem included) per second of the timed run.  With N ranks the
-    search is shared (incumbent all-reduce, cut all-gather, work stealing; strong scaling)."""
+    """Full B&B on the device (BASELINE configs[2]: 1k-arc network, 64 scenarios) for
+    --bnb-seconds; with N ranks the search is shared (incumbent all-reduce, cut all-gather,
+    work sharing: strong scaling)."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -146,71 +215,37 @@ def bnb_main(args):
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend)
-    from sgufp_solver_amd import instance
-    from sgufp_solver_amd.pools import DOUBLE_MIN
-    from sgufp_solver_amd.solver import DDSolver
-    cfg = instance.CONFIGS[args.bnb_config]
-    inst = instance.generate(cfg, args.seed)
-    if args.bnb_lb == "zero":
-        inst.lb[:] = 0
+    heartbeat("bnb", 20.0)
     work = tempfile.mkdtemp(prefix=f"sgufp_bnb_r{rank}_")
-    net = os.path.join(work, "net.txt")
-    inst.write(net)
-    # a round (and its refinement loops) can run for minutes: keep a heartbeat on stderr
-    import threading
-    t_hb = time.perf_counter()
-
-    def heartbeat():
-        while True:
-            time.sleep(20.0)
-            print(f"bnb: running, {time.perf_counter() - t_hb:.0f} s", file=sys.stderr, flush=True)
-
-    threading.Thread(target=heartbeat, daemon=True).start()
-    solver = DDSolver(net, device=local, max_batch=args.nodes, verbose=False, time_budget=2.0, progress=10.0)
-    solver.start_solver(DOUBLE_MIN)                        # warm-up (kernels, allocations)
-    solver.eng.clear_cuts()
-    solver.eng.set_timing(True)
-    solver.time_budget = args.bnb_seconds
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    z = solver.start_solver(DOUBLE_MIN)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    c = dict(solver.counters)
-    if dist:
-        t = torch.tensor([elapsed] + [float(c[k]) for k in sorted(c)], dtype=torch.float64,
-                         device="cuda" if torch.cuda.is_available() else "cpu")
-        tmax = t[:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        elapsed = float(tmax.item())
-        c = {k: int(v) for k, v in zip(sorted(c), t[1:].tolist())}
-    line = {
-        "metric": "device B&B: node relaxations/s (NodeExplorer::process incl. exact-leaf subproblems)",
-        "value": round(c["relaxed"] / elapsed, 2), "unit": "relaxations/s", "n_gpus": world,
-        "seconds": round(elapsed, 3), "rounds": solver.rounds, "complete": solver.complete, "incumbent": z,
-        "higher_is_better": True, "scaling": "strong", "dtype": "f64", "data": "synthetic",
-        "config": {"workload": f"{args.bnb_config}: {cfg.n_arcs}-arc layered network, {inst.scenarios} scenarios"
-                               f"{' (lower bounds 0)' if args.bnb_lb == 'zero' else ''}, root record, no incumbent, "
-                               f"up to {args.nodes} records per round",
-                   "instance_seed": args.seed, "total_layers": int(solver.eng.info.total_layers)},
-        "counters": c,
-        "pool": [solver.eng.cuts_count(1), solver.eng.cuts_count(0)],
-        "subproblems_per_s": round(c["subproblems"] / elapsed, 2),
-    }
+    out = bnb_run(args.bnb_config, args.seed, args.bnb_lb, args.bnb_seconds, args.nodes, args.round_seconds, work,
+                  device=local)
+    line = {"metric": "device B&B: node relaxations/s (NodeExplorer::process incl. exact-leaf subproblems)",
+            "value": out["relaxations_per_s"], "unit": "relaxations/s", "n_gpus": world,
+            "higher_is_better": True, "scaling": "strong", "dtype": "f64", "data": "synthetic", **out}
     if rank == 0:
         print(json.dumps(line), flush=True)
-    solver.eng.close()
     if dist:
         dist.destroy_process_group()
+
+
+def heartbeat(tag="bench", every=30.0):
+    """A progress line on stderr while the legs run (long phases print nothing else)."""
+    import threading
+    t0 = time.perf_counter()
+
+    def run():
+        while True:
+            time.sleep(every)
+            print(f"[{tag}] running, {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
 
 
 def main():
     args = parse()
     if args.mode == "bnb":
         return bnb_main(args)
+    heartbeat()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -253,19 +288,37 @@ def main():
     mine = E.batch_slice(full, np.arange(rank * n, min(full.n, (rank + 1) * n)))
     eng.upload(mine)
 
+    # With N ranks every step is one B&B round of a frontier shard: the relaxation of its
+    # records, then the round's exchanges over RCCL (sgufp_solver_amd/shards.py) -- the
+    # incumbent all-reduce(MAX) and the all-gather of the cut rows the round appended (a
+    # DD-only step closes no exact leaf and adds no rows: the collectives still run).
+    comm = None
+    marks = {1: eng.cuts_count(1), 0: eng.cuts_count(0)}
+    if dist:
+        from sgufp_solver_amd.shards import ShardComm
+        comm = ShardComm()
+
+    def step(z):
+        eng.relax_async(z)
+        eng.sync()
+        if comm is not None:
+            z = comm.allreduce_max(z)
+            comm.exchange_cuts(eng, marks)
+        return z
+
     eng.set_timing(True)
     for _ in range(args.warmup):
-        eng.relax_async(incumbent)
-        eng.sync()
+        step(incumbent)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     relax_ms = []
     emit_ms = []
+    bytes0 = comm.bytes if comm else 0
     t0 = time.perf_counter()
+    z = incumbent
     for _ in range(args.steps):
-        eng.relax_async(incumbent)
-        eng.sync()
+        z = step(incumbent)
         a, b = eng.last_timing()
         relax_ms.append(a)
         emit_ms.append(b)
@@ -278,21 +331,26 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # per-launch algorithmic bytes: 6A + sum_cuts(14A + 8N) + record in
+    # per-launch SURVEY 8(d) byte model: 6A + sum_cuts(14A + 8N) + record in
     st, ex, lb, ub, nc = eng.results_arrays()
     dn, da, dl, sw = eng.stats()
     g = mine.gl.astype(np.float64)
     ns = np.diff(mine.states_off).astype(np.float64)
     r_in = 2 * g + 2 * ns + 24
-    bytes_relax = float(np.sum(6.0 * da + sw * (14.0 * da + 8.0 * dn) + r_in))
+    bytes_model = float(np.sum(6.0 * da + sw * (14.0 * da + 8.0 * dn) + r_in))
     ch = eng.children_batch()
     r_out = float(np.sum(2 * ch.gl.astype(np.float64) + 2 * np.diff(ch.states_off) + 24)) if ch.n else 0.0
     t_relax = float(np.mean(relax_ms)) / 1e3
-    achieved = bytes_relax / t_relax / 1e9
+    model_gbps = bytes_model / t_relax / 1e9
     traffic, traffic_src = pmc_traffic(args.profile_tag, workload_key(args))
+    achieved = traffic / t_relax / 1e9 if traffic else None
 
     total_nodes = mine.n * world
     value = total_nodes * args.steps / elapsed
+    gpu_sample = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        k = min(args.cpu_sample, mine.n)
+        gpu_sample = eng._collect()[:k]          # the last timed step's results, record order
     sub = subproblem_leg(eng, inst, net, args) if rank == 0 else None
     line = {
         "metric": METRIC,
@@ -315,37 +373,41 @@ def main():
             "status_counts": {str(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
             "avg_dd_nodes": float(np.mean(dn)), "avg_dd_arcs": float(np.mean(da)),
             "avg_sweeps": float(np.mean(sw)), "children_per_step": int(ch.n),
-            "parallelism": f"frontier shards x{world}",
+            "parallelism": f"frontier shards x{world}" + (", per-step incumbent all-reduce + cut-row all-gather"
+                                                          if world > 1 else ""),
         },
-        "hbm_gbps_algorithmic": round(achieved, 2),
         "roofline": {
-            # the roofline that bounds this class of kernel (no MFMA work); the kernel itself
-            # is limited by instruction issue and LDS latency, not by HBM
+            # the roofline that bounds this class of kernel (no MFMA work): HBM.  achieved /
+            # frac are the HBM bytes the counters measured for this build (FETCH_SIZE x 2 +
+            # WRITE_SIZE per launch) over the launch time; the SURVEY 8(d) byte model counts
+            # every (arc, cut) operand as if streamed from HBM, which the kernel serves from LDS
+            # / L2 -- reported separately as model_gbps, it is not HBM traffic.
             "bound": "hbm",
-            "limiter": "latency/issue (measured HBM traffic is a fraction of the algorithmic bytes)",
-            # SURVEY 8(d)'s byte model streams every (arc, cut) operand from HBM; the kernel
-            # serves most of them from LDS / L2 (topology staged once per cut batch), so the
-            # model's rate can pass the HBM peak -- frac_traffic is the measured utilisation
-            "byte_model": "SURVEY 8(d): 6A + sum over applied cuts (14A + 8N) + records; not HBM traffic",
+            "limiter": "latency/issue (DESIGN.md section 5: issue counters in profiles/)",
             "kernel": "k_relax",
-            "achieved": round(achieved, 2),
+            "achieved": round(achieved, 2) if achieved else None,
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
             "traffic": traffic,
-            "traffic_gbps": round(traffic / t_relax / 1e9, 2) if traffic else None,
-            "frac_traffic": round(traffic / t_relax / 1e9 / HBM_PEAK_GBPS, 4) if traffic else None,
             "traffic_source": traffic_src,
-            "bytes_per_launch": bytes_relax,
             "avg_launch_ms": round(t_relax * 1e3, 4),
             "emit_ms": round(float(np.mean(emit_ms)), 4),
+            "model_gbps": round(model_gbps, 2),
+            "model_bytes_per_launch": bytes_model,
+            "model": "SURVEY 8(d): 6A + sum over applied cuts (14A + 8N) + records (A, N, cuts counted per record)",
             "children_record_bytes": r_out,
         },
         "cpu_baseline": None,
+        "parity": None,
         "subproblem": sub,
     }
+    if comm is not None:
+        line["exchange_bytes_per_step"] = round((comm.bytes - bytes0) / args.steps, 1)
     if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(work, net, pool, mine, incumbent, args)
+        cb, par = cpu_baseline(work, net, pool, mine, incumbent, args, gpu_sample)
+        line["cpu_baseline"] = cb
+        line["parity"] = par
         if sub is not None:
             i0, n0 = sub["_inst0"]
             sub["cpu_baseline"] = cpu_subproblem_baseline(inst, net, sub["_paths"], args, i0, n0)
@@ -353,6 +415,11 @@ def main():
         sub.pop("_paths", None)
         sub.pop("_inst0", None)
     eng.close()
+    if rank == 0 and world == 1 and args.bnb_leg_seconds > 0:
+        # BASELINE metric with the subproblems in the loop: the device B&B on the same
+        # 1k-arc network with its 256 scenarios (lower bounds 0: feasible, optimality cuts)
+        line["bnb"] = bnb_run(args.config, args.seed, "zero", args.bnb_leg_seconds, 1024, args.round_seconds, work,
+                              device=local, progress=0.0, tag="leg")
     if rank == 0 and world == 1 and args.config == "C4" and args.c5_nodes > 0:
         line["config5"] = config5_leg(args, work)
     if rank == 0:
@@ -416,6 +483,11 @@ def config5_leg(args, work):
                              "scenario_lps_per_s": round(len(paths) * inst.scenarios / t, 1),
                              "cut_types": {str(k): int(v) for k, v in zip(*np.unique(typ, return_counts=True))}}
     eng.close()
+    if args.c5_bnb_seconds > 0:
+        # BASELINE configs[4]: the device B&B with cut generation in the loop (exact leaves
+        # call the 512-scenario subproblem, new cuts join the pool every refinement step)
+        out["bnb"] = bnb_run("C5", args.seed, "zero", args.c5_bnb_seconds, 1024, args.round_seconds, work,
+                             progress=0.0, tag="c5leg")
     return out
 
 
@@ -482,9 +554,47 @@ def cpu_subproblem_baseline(inst, net, paths, args, inst0=None, net0=None):
                       f"{' (lower bounds 0)' if inst0 is not None else ''}, scipy HiGHS, {t:.1f} s"}
 
 
-def cpu_baseline(work, net, pool, batch, incumbent, args):
-    """The reference's own RelaxedDDNew (oracle/_ref/ref_dd, built from its sources)
-    when present, else the clean-room port, on the host cores, bounded sample."""
+def _bits(x: float) -> int:
+    import struct
+    return struct.unpack("<q", struct.pack("<d", x))[0]
+
+
+def compare_results(got, want):
+    """Bit-exact comparison of NodeExplorer::process outcomes (status, exact flag, lb / ub
+    bit patterns, argmax path of exact DDs, cutset children -- the branching indices --, DD
+    sizes); returns (number of records that differ, first messages)."""
+    def key(nd):
+        return (nd.gl, _bits(nd.lb), _bits(nd.ub), tuple(nd.states), tuple(nd.sol))
+    bad, msgs = 0, []
+    for k, (g, w) in enumerate(zip(got, want)):
+        why = None
+        if g.status != w.status or g.exact != w.exact:
+            why = f"status/exact {(g.status, g.exact)} != {(w.status, w.exact)}"
+        elif _bits(g.lb) != _bits(w.lb) or _bits(g.ub) != _bits(w.ub):
+            why = f"bounds {(g.lb, g.ub)} != {(w.lb, w.ub)}"
+        elif g.path != w.path:
+            why = "argmax path differs"
+        elif [key(c) for c in g.children] != [key(c) for c in w.children]:
+            why = f"children differ ({len(g.children)} vs {len(w.children)})"
+        elif (g.dd_nodes, g.dd_arcs, g.dd_layers) != (w.dd_nodes, w.dd_arcs, w.dd_layers):
+            why = "DD size differs"
+        if why:
+            bad += 1
+            if len(msgs) < 5:
+                msgs.append(f"record {k}: {why}")
+    if len(got) != len(want):
+        bad += abs(len(got) - len(want))
+        msgs.append(f"{len(got)} results vs {len(want)}")
+    return bad, msgs
+
+
+def cpu_baseline(work, net, pool, batch, incumbent, args, gpu_sample=None):
+    """The reference's own RelaxedDDNew (oracle/_ref/ref_dd, built from its sources) on the
+    host cores over a bounded sample of the same frontier (same pool and incumbent): every
+    record of the sample, a work queue over the threads ("relaxp").  Its outputs are also
+    the parity check of the timed workload: the GPU results of the last timed step for the
+    same records must equal them bit for bit.  Falls back to the clean-room port's timing
+    (no parity) when the reference build is absent.  Returns (cpu_baseline, parity)."""
     from sgufp_solver_amd import engine as E
     from sgufp_solver_amd import pools
     sample = E.batch_slice(batch, np.arange(min(args.cpu_sample, batch.n)))
@@ -493,26 +603,44 @@ def cpu_baseline(work, net, pool, batch, incumbent, args):
     pools.write_nodes(nodes, E.batch_to_records(sample))
     pools.write_pool(cuts, pool)
     threads = max(1, min(16, os.cpu_count() or 1))
-    for kind, exe in (("reference", os.path.join(ROOT, "oracle", "_ref", "ref_dd")),
-                      ("port", os.path.join(ROOT, "oracle", "_build", "dd_oracle"))):
-        if not os.path.exists(exe):
-            continue
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            cpu_model = next(l.split(":", 1)[1].strip() for l in fh if l.startswith("model name"))
+    except Exception:
+        pass
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_dd")
+    if os.path.exists(ref):
+        out_path = os.path.join(work, "ref_results.txt")
+        r = subprocess.run([ref, "relaxp", net, cuts, nodes, incumbent.hex(), str(threads), out_path],
+                           capture_output=True, text=True, timeout=600)
+        if r.returncode == 0:
+            out = json.loads(r.stdout.strip().splitlines()[-1])
+            cb = {"value": round(out["relaxations"] / out["seconds"], 2), "unit": "relaxations/s", "cores": threads,
+                  "kind": "reference", "cpu": cpu_model,
+                  "sample": f"the first {sample.n} open nodes of the timed frontier, same pool and incumbent, "
+                            f"{out['seconds']:.1f} s on {threads} threads"}
+            parity = None
+            if gpu_sample is not None and not args.no_parity:
+                want = pools.read_results(out_path)
+                bad, msgs = compare_results(gpu_sample, want)
+                parity = {"checked": len(want), "mismatches": bad, "bit_exact": bad == 0,
+                          "against": "oracle/_ref/ref_dd relaxp (the reference's RelaxedDDNew) on the same records, "
+                                     "pool and incumbent",
+                          "fields": "status, exact, lb/ub bits, argmax path, cutset children, DD sizes",
+                          "first_mismatches": msgs}
+            return cb, parity
+    exe = os.path.join(ROOT, "oracle", "_build", "dd_oracle")
+    if os.path.exists(exe):
         r = subprocess.run([exe, "time", net, cuts, nodes, incumbent.hex(), str(threads), str(args.cpu_seconds)],
                            capture_output=True, text=True, timeout=args.cpu_seconds * 4 + 120)
-        if r.returncode != 0:
-            continue
-        out = json.loads(r.stdout.strip().splitlines()[-1])
-        cpu_model = ""
-        try:
-            with open("/proc/cpuinfo") as fh:
-                cpu_model = next(l.split(":", 1)[1].strip() for l in fh if l.startswith("model name"))
-        except Exception:
-            pass
-        return {"value": round(out["relaxations"] / out["seconds"], 2), "unit": "relaxations/s", "cores": threads,
-                "kind": kind, "cpu": cpu_model,
-                "sample": f"{out['relaxations']} of the first {sample.n} open nodes of the same frontier, same pool and "
-                          f"incumbent, {out['seconds']:.1f} s on {threads} threads"}
-    return None
+        if r.returncode == 0:
+            out = json.loads(r.stdout.strip().splitlines()[-1])
+            return ({"value": round(out["relaxations"] / out["seconds"], 2), "unit": "relaxations/s", "cores": threads,
+                     "kind": "port", "cpu": cpu_model,
+                     "sample": f"{out['relaxations']} of the first {sample.n} open nodes of the same frontier, same "
+                               f"pool and incumbent, {out['seconds']:.1f} s on {threads} threads"}, None)
+    return None, None
 
 
 if __name__ == "__main__":

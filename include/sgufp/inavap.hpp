@@ -157,6 +157,15 @@ class DDSolver {
     explicit DDSolver(const std::shared_ptr<Network> &networkPtr_, uint16_t nWorkers, int batch = 4096);
     std::pair<double, double> start(double opt);
     double startSolver(double optimal);
+    // One shard of a multi-GPU search (one process and one DDSolver per GPU): after every
+    // round the shards exchange the incumbent (CAS-max, DDSolver.cpp:723-731), the new cut
+    // rows (the global Containers, DDSolver.h:415-416) and work (half-split / 40 % steal,
+    // DDSolver.cpp:603-652) over RCCL; the root record starts on rank 0.  id comes from
+    // sgufp_comm_unique_id on one rank (SGUFP_COMM_ID_BYTES bytes).
+    void shard(int world, int rank, const uint8_t *id);
+    // bound a round's exact-leaf refinement loops (sgufp_bnb_set_limits)
+    void roundLimits(int maxRefineIters, double roundSeconds);
+    int64_t received = 0;   // records this shard got through work sharing
     // counters of the last solve (SOLVER_COUNTERS, DDSolver.h:380-392)
     sgufp_bnb_stats totals{};
     // the reference's printWorkerStats report (DDSolver.h:441-501) for the last solve: one

@@ -207,6 +207,32 @@ int sgufp_bnb_set_limits(sgufp_ctx *ctx, int max_refine_iters, double round_seco
  * e.g. to all-gather the cuts a round produced to the other frontier shards. */
 int sgufp_cuts_rows(sgufp_ctx *ctx, int is_feasibility, int first, int count, double *rhs, double *rows);
 
+/* -- frontier shards over RCCL (one context per GPU / process; shard.cpp) -------------
+ * The reference's threads share the incumbent (std::atomic<double> CAS, DDSolver.cpp:723-731),
+ * the global cut Containers (DDSolver.h:415-416) and the work queues (master half-split and
+ * 40 % steal, DDSolver.cpp:603-652).  A sharded DDSolver runs one context per GPU and, after
+ * every sgufp_bnb_step, makes those exchanges between the contexts of one RCCL communicator,
+ * device buffer to device buffer on the context stream.  Without sgufp_comm_init (one shard)
+ * every call below is a no-op that leaves its outputs as for a single shard. */
+#define SGUFP_COMM_ID_BYTES 128
+/* On one rank; the bytes reach the other ranks by any side channel (MPI, a file, a store). */
+int sgufp_comm_unique_id(uint8_t *id, int bytes);
+int sgufp_comm_init(sgufp_ctx *ctx, int world, int rank, const uint8_t *id);
+int sgufp_comm_info(const sgufp_ctx *ctx, int *world, int *rank);
+void sgufp_comm_destroy(sgufp_ctx *ctx);
+/* *inout := max over the shards (replaces the CAS-max, DDSolver.cpp:723-731). */
+int sgufp_incumbent_allreduce(sgufp_ctx *ctx, double *inout);
+/* Every shard's pool rows appended since the last exchange are appended on every other
+ * shard, in rank order, feasibility list then optimality list (Container::add of another
+ * worker's cut).  *received = rows this shard appended. */
+int sgufp_cuts_exchange(sgufp_ctx *ctx, int64_t *received);
+/* sizes[world] := every shard's frontier size (termination: all zero). */
+int sgufp_frontier_sizes(sgufp_ctx *ctx, int64_t *sizes);
+/* While a shard is idle, every busy shard gives records from the bottom of its stack (40 %
+ * of >= 32, lf_queue::m_pop; half of fewer, the master's hand-out) and the idle shards
+ * split each donor's records in contiguous chunks.  *received = records this shard got. */
+int sgufp_frontier_balance(sgufp_ctx *ctx, int64_t *received);
+
 /* -- restricted decision diagram (replaces Inavap::RestrictedDDNew, DD.h:653-730 /
  *    DD.cpp:3090-3505, driven as in NodeExplorer::processX3, NodeExplorer.cpp:605-656) --
  * For every staged node (sgufp_batch_upload): RestrictedDDNew{net, width}.compile(node)

@@ -1,6 +1,6 @@
 """Native build: hipcc for gfx950, in-tree outputs (they travel to the GPU box).
 
-    libsgufp_hip.so   kernels + C ABI (include/sgufp_hip.h)
+    libsgufp_hip.so   kernels + C ABI (include/sgufp_hip.h), linked with RCCL (frontier shards)
     lib_verify/libsgufp_hip.so
                       the same with SGUFP_SUB_VERIFY: every warm-started Bellman-Ford of the
                       subproblem is re-run cold and compared (debug build for tests)
@@ -26,7 +26,8 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unus
           f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}"]
 
 HIP_SOURCES = ["dd_kernels.hip", "sub_kernels.hip", "bnb_kernels.hip", "rdd_kernels.hip", "capi.cpp", "bnb.cpp",
-               "network.cpp"]
+               "network.cpp", "shard.cpp"]
+LINK = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]   # frontier shards (shard.cpp)
 HOST_SOURCES = ["host/inavap.cpp"]
 
 
@@ -64,7 +65,7 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
             _run(cmd)
     lib = os.path.join(LIBDIR, "libsgufp_hip.so")
     if force or _stale(lib, objs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs])
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs, *LINK])
     # debug variant: subproblem kernels with the warm Bellman-Ford cross-check
     vdir = os.path.join(HERE, "lib_verify")
     os.makedirs(vdir, exist_ok=True)
@@ -75,7 +76,7 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
     vlib = os.path.join(vdir, "libsgufp_hip.so")
     vobjs = [vobj if os.path.basename(o) == "sub_kernels.hip.o" else o for o in objs]
     if force or _stale(vlib, vobjs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", vlib, *vobjs])
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", vlib, *vobjs, *LINK])
     host_srcs = [os.path.join(CSRC, s) for s in HOST_SOURCES if os.path.exists(os.path.join(CSRC, s))]
     if host_srcs:
         hlib = os.path.join(LIBDIR, "libsgufp_host.so")

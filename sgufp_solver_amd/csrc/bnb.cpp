@@ -25,6 +25,11 @@
 
 #include "ctx.hpp"
 
+namespace sgufp {
+hipError_t launch_gather_rows(const double *rows, const double *rhs, const int32_t *ids, int k, int stride, double *out,
+                              hipStream_t st);
+}  // namespace sgufp
+
 void sgufp_ctx::decode_states(const uint16_t *gl, const uint32_t *mask, size_t count, int64_t *states_off,
                               int16_t *states) const {
     int64_t ss = 0;
@@ -207,42 +212,38 @@ int sgufp_frontier_take(sgufp_ctx *ctx, int n, int from_bottom, uint16_t *gl, do
         ctx->fr_sol_top = ctx->fr_n ? s_lo : 0;
         return SGUFP_OK;
     }
-    // from the bottom: move the remaining entries down (through a bounce buffer, the ranges overlap)
-    const size_t rest = (size_t)(total - n);
-    const size_t srest = (size_t)(ctx->fr_sol_top - s_hi);
-    std::vector<int64_t> soff(rest);
-    if (!ctx->download(soff.data(), f.sol_off + n, rest) || !ctx->sync()) return SGUFP_ERR_HIP;
-    for (auto &x : soff) x -= s_hi;
-    void *tmp = nullptr;
-    const size_t tbytes = std::max(rest * 8, srest * 2);
-    if (!ctx->hip_ok(hipMalloc(&tmp, std::max<size_t>(tbytes, 8)), "bounce")) return SGUFP_ERR_HIP;
-    auto move = [&](void *dst, const void *src, size_t bytes) {
-        return ctx->hip_ok(hipMemcpyAsync(tmp, src, bytes, hipMemcpyDeviceToDevice, ctx->stream), "D2D") &&
-               ctx->hip_ok(hipMemcpyAsync(dst, tmp, bytes, hipMemcpyDeviceToDevice, ctx->stream), "D2D");
-    };
-    bool ok = move(f.gl, f.gl + n, rest * 2) && move(f.lb, f.lb + n, rest * 8) && move(f.ub, f.ub + n, rest * 8) &&
-              move(f.mask, f.mask + n, rest * 4) && move(f.valid, f.valid + n, rest) &&
-              move(f.sol_len, f.sol_len + n, rest * 2) && (srest == 0 || move(f.sol, f.sol + s_hi, srest * 2)) &&
-              ctx->upload(f.sol_off, soff.data(), rest) && ctx->sync();
-    (void)hipFree(tmp);
-    if (!ok) return SGUFP_ERR_HIP;
-    ctx->fr_n = (int64_t)rest;
-    ctx->fr_sol_top = (int64_t)srest;
-    return SGUFP_OK;
+    // from the bottom: the remaining entries move down (frontier_drop_bottom, shard.cpp)
+    return ctx->frontier_drop_bottom(n) ? SGUFP_OK : SGUFP_ERR_HIP;
 }
 
 int sgufp_cuts_rows(sgufp_ctx *ctx, int is_feasibility, int first, int count, double *rhs, double *rows) {
     if (!ctx || first < 0 || count < 0) return SGUFP_ERR_ARG;
     const auto &v = is_feasibility ? ctx->f_rows : ctx->o_rows;
     if (first + count > (int)v.size()) return SGUFP_ERR_ARG;
-    const size_t stride = (size_t)ctx->net.n_slots + 1;
-    for (int c = 0; c < count; c++) {
-        const int r = v[first + c];
-        if ((rhs && !ctx->download(rhs + c, ctx->d_rhs + r, 1)) ||
-            (rows && !ctx->download(rows + (size_t)c * stride, ctx->d_rows + (size_t)r * stride, stride)))
-            return SGUFP_ERR_HIP;
+    if (count == 0) return SGUFP_OK;
+    // one gather kernel ({rhs, row} blocks) and one download instead of a copy per row
+    const size_t stride = (size_t)ctx->net.n_slots + 1, blk = stride + 1;
+    if ((size_t)count * blk > ctx->rowbuf_cap) {
+        if (ctx->d_rowbuf) ctx->release(ctx->d_rowbuf);
+        ctx->rowbuf_cap = std::max((size_t)count * blk, 2 * ctx->rowbuf_cap);
+        if (!ctx->alloc(ctx->d_rowbuf, ctx->rowbuf_cap, "cut rows")) return SGUFP_ERR_HIP;
     }
-    return ctx->sync() ? SGUFP_OK : SGUFP_ERR_HIP;
+    if ((size_t)count > ctx->rowids_cap) {
+        if (ctx->d_rowids) ctx->release(ctx->d_rowids);
+        ctx->rowids_cap = std::max((size_t)count, 2 * ctx->rowids_cap);
+        if (!ctx->alloc(ctx->d_rowids, ctx->rowids_cap, "cut rows")) return SGUFP_ERR_HIP;
+    }
+    std::vector<double> buf((size_t)count * blk);
+    if (!ctx->upload(ctx->d_rowids, v.data() + first, (size_t)count) ||
+        !ctx->hip_ok(launch_gather_rows(ctx->d_rows, ctx->d_rhs, ctx->d_rowids, count, (int)stride, ctx->d_rowbuf,
+                                        ctx->stream), "k_gather_rows") ||
+        !ctx->download(buf.data(), ctx->d_rowbuf, buf.size()) || !ctx->sync())
+        return SGUFP_ERR_HIP;
+    for (int c = 0; c < count; c++) {
+        if (rhs) rhs[c] = buf[(size_t)c * blk];
+        if (rows) std::memcpy(rows + (size_t)c * stride, &buf[(size_t)c * blk + 1], stride * sizeof(double));
+    }
+    return SGUFP_OK;
 }
 
 int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_stats *stats) {

@@ -71,3 +71,82 @@ hipError_t launch_push_children(const ChildOut &co, const BatchOut &out, const i
 }
 
 }  // namespace sgufp
+
+namespace sgufp {
+
+// ---- cut-pool rows and frontier records between frontier shards (shard.cpp) ----------
+
+// pool rows ids[k] -> out[k] = {rhs, row[0 .. stride)}: one send block for the RCCL all-gather
+__global__ void __launch_bounds__(256) k_gather_rows(const double *rows, const double *rhs, const int32_t *ids, int k,
+                                                     int stride, double *out) {
+    const int c = blockIdx.x;
+    if (c >= k) return;
+    const size_t r = (size_t)ids[c];
+    double *o = out + (size_t)c * (stride + 1);
+    if (threadIdx.x == 0) o[0] = rhs[r];
+    for (int v = threadIdx.x; v < stride; v += blockDim.x) o[1 + v] = rows[r * stride + v];
+}
+
+// n rows {rhs, row} appended at pool rows first ..: the dense row (its last, absent-key slot
+// zeroed), the RHS, the per-(layer, state rank) table of the batched sweeps and the
+// node-independent bound of the screening order -- what sgufp_ctx::append_rows builds on
+// the host, in the same order of operations (the bound: RHS + sum over layers, in layer
+// order, of max(0, max over ranks)).
+__global__ void __launch_bounds__(256) k_append_rows(const double *src, int n, int stride, int first, double *rows,
+                                                     double *rhs, double *coefT, const int32_t *slot_tab, int L,
+                                                     int us, double *row_ub) {
+    const int c = blockIdx.x;
+    if (c >= n) return;
+    const double *s = src + (size_t)c * (stride + 1);
+    const size_t r = (size_t)(first + c);
+    for (int v = threadIdx.x; v < stride; v += blockDim.x) rows[r * stride + v] = (v == stride - 1) ? 0.0 : s[1 + v];
+    const size_t tstride = (size_t)(L > 0 ? L : 1) * us;
+    for (int e = threadIdx.x; e < L * us; e += blockDim.x) {
+        const int l = e / us, k = e - l * us;
+        const int sl = slot_tab[(size_t)l * kMaxU + k];
+        coefT[r * tstride + e] = (sl >= 0 && sl < stride - 1) ? s[1 + sl] : 0.0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        rhs[r] = s[0];
+        double b = s[0];
+        for (int l = 0; l < L; l++) {
+            double m = 0.0;
+            for (int k = 0; k < us; k++) {
+                const int sl = slot_tab[(size_t)l * kMaxU + k];
+                const double x = (sl >= 0 && sl < stride - 1) ? s[1 + sl] : 0.0;
+                m = (m < x) ? x : m;   // std::max(m, x)
+            }
+            b += m;
+        }
+        row_ub[c] = b;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_rebase(int64_t *off, int n, int64_t delta) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) off[i] += delta;
+}
+
+hipError_t launch_gather_rows(const double *rows, const double *rhs, const int32_t *ids, int k, int stride, double *out,
+                              hipStream_t st) {
+    if (k <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gather_rows, dim3(k), dim3(256), 0, st, rows, rhs, ids, k, stride, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_append_rows(const double *src, int n, int stride, int first, double *rows, double *rhs,
+                              double *coefT, const int32_t *slot_tab, int L, int us, double *row_ub, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_append_rows, dim3(n), dim3(256), 0, st, src, n, stride, first, rows, rhs, coefT, slot_tab, L,
+                       us, row_ub);
+    return hipGetLastError();
+}
+
+hipError_t launch_rebase(int64_t *off, int n, int64_t delta, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rebase, dim3((n + 255) / 256), dim3(256), 0, st, off, n, delta);
+    return hipGetLastError();
+}
+
+}  // namespace sgufp

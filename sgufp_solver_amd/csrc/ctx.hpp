@@ -164,11 +164,30 @@ struct sgufp_ctx {
     RddIO rio{};
     bool rdd_init();
 
+    // frontier shards over RCCL (shard.cpp); comm is an ncclComm_t, nullptr for one shard
+    void *comm = nullptr;
+    int world = 1, rank = 0;
+    int shared[2] = {0, 0};                   // rows of the optimality [0] / feasibility [1] list
+                                              // already exchanged (own rows after that are new)
+    int64_t *d_comm_i64 = nullptr;            // [4 * world + 4] small all-gathers
+    double *d_comm_f64 = nullptr;             // [1] incumbent all-reduce
+    double *d_xsend = nullptr, *d_xrecv = nullptr, *d_xub = nullptr;
+    int32_t *d_xids = nullptr;
+    int64_t *d_xspan = nullptr;
+    size_t xsend_cap = 0, xrecv_cap = 0, xub_cap = 0, xids_cap = 0, xspan_cap = 0;
+    uint8_t *bounce = nullptr;                // overlapping frontier moves (frontier_drop_bottom)
+    size_t bounce_cap = 0;
+    bool frontier_drop_bottom(int64_t count);
+    double *d_rowbuf = nullptr;               // sgufp_cuts_rows gather buffer
+    int32_t *d_rowids = nullptr;
+    size_t rowbuf_cap = 0, rowids_cap = 0;
+
     bool timing = false;
     hipEvent_t ev[4] = {};
     float ms_relax = 0, ms_emit = 0;
 
-    ~sgufp_ctx() {
+    ~sgufp_ctx();
+    void destroy_all() {
         if (device >= 0) (void)hipSetDevice(device);
         for (auto &b : allocs) (void)hipFree(b.p);
         for (auto &e : ev)

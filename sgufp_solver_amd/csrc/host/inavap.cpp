@@ -6,6 +6,7 @@
 #include <chrono>
 #include <ctime>
 #include <sstream>
+#include <vector>
 #include <cstdio>
 #include <fstream>
 #include <iostream>
@@ -197,15 +198,28 @@ OutObject NodeExplorer::process(Node node, double optimalLB, Container &globalFe
 DDSolver::DDSolver(const std::shared_ptr<Network> &networkPtr_, uint16_t nWorkers, int batch_)
     : networkPtr{networkPtr_}, N_WORKERS{nWorkers}, dev{*networkPtr_, std::max(1, batch_)}, batch{std::max(1, batch_)} {}
 
+void DDSolver::shard(int world, int rank, const uint8_t *id) {
+    dev.check(sgufp_comm_init(dev.get(), world, rank, id), "comm init");
+}
+
+void DDSolver::roundLimits(int maxRefineIters, double roundSeconds) {
+    dev.check(sgufp_bnb_set_limits(dev.get(), maxRefineIters, roundSeconds), "round limits");
+}
+
 double DDSolver::startSolver(double known_optimal) {
     sgufp_ctx *g = dev.get();
     dev.check(sgufp_frontier_clear(g), "frontier clear");
-    // root record Node{} (DDSolver.cpp:788-791); its cutset is taken with ub = DOUBLE_MAX
+    int world = 1, rank = 0;
+    dev.check(sgufp_comm_info(g, &world, &rank), "comm info");
+    // root record Node{} (DDSolver.cpp:788-791) on the first shard; its cutset is taken with
+    // ub = DOUBLE_MAX
     uint16_t gl = 0;
     double lb = DOUBLE_MIN, ub = DOUBLE_MAX;
     int64_t z2[2] = {0, 0};
     static const int16_t empty = 0;
-    dev.check(sgufp_frontier_push(g, 1, &gl, &lb, &ub, z2, &empty, z2, &empty), "frontier push");
+    if (rank == 0) dev.check(sgufp_frontier_push(g, 1, &gl, &lb, &ub, z2, &empty, z2, &empty), "frontier push");
+    received = 0;
+    std::vector<int64_t> sizes((size_t)world);
     double z = known_optimal;
     totals = sgufp_bnb_stats{};
     rounds = 0;
@@ -239,7 +253,23 @@ double DDSolver::startSolver(double known_optimal) {
         totals.dd_arcs += st.dd_arcs;
         totals.sweeps += st.sweeps;
         totals.frontier = st.frontier;
-        if (st.frontier == 0) break;
+        totals.deferred += st.deferred;
+        totals.resumed += st.resumed;
+        if (world == 1) {
+            if (st.frontier == 0) break;
+            continue;
+        }
+        // the round's exchanges between the shards (shard.cpp)
+        int64_t got = 0;
+        dev.check(sgufp_incumbent_allreduce(g, &z), "incumbent all-reduce");
+        dev.check(sgufp_cuts_exchange(g, &got), "cut exchange");
+        dev.check(sgufp_frontier_sizes(g, sizes.data()), "frontier sizes");
+        int64_t left = 0;
+        for (int64_t s : sizes) left += s;
+        if (left == 0) break;
+        dev.check(sgufp_frontier_balance(g, &got), "work sharing");
+        received += got;
+        if (st.exact > 0 || got > 0) diving = false;
     }
     return z;
 }

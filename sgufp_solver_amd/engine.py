@@ -31,7 +31,9 @@ EXPORTS = [
     "sgufp_cuts_append_rows", "sgufp_frontier_clear", "sgufp_frontier_size", "sgufp_frontier_push",
     "sgufp_frontier_take_size", "sgufp_frontier_take", "sgufp_bnb_step", "sgufp_cuts_rows",
     "sgufp_restricted_relax", "sgufp_restricted_results", "sgufp_restricted_paths", "sgufp_restricted_cutset_size",
-    "sgufp_restricted_cutset", "sgufp_bnb_set_limits",
+    "sgufp_restricted_cutset", "sgufp_bnb_set_limits", "sgufp_comm_unique_id", "sgufp_comm_init",
+    "sgufp_comm_info", "sgufp_comm_destroy", "sgufp_incumbent_allreduce", "sgufp_cuts_exchange",
+    "sgufp_frontier_sizes", "sgufp_frontier_balance",
 ]
 
 
@@ -56,6 +58,15 @@ class NetworkInfo(C.Structure):
 
 
 _lib = None
+
+
+def comm_unique_id() -> bytes:
+    """sgufp_comm_unique_id: the RCCL communicator id, made on one rank."""
+    lib = load_library()
+    buf = (C.c_uint8 * 128)()
+    if lib.sgufp_comm_unique_id(buf, 128) != 0:
+        raise RuntimeError("sgufp_comm_unique_id failed")
+    return bytes(buf)
 
 
 def load_library(path: str = LIB_PATH) -> C.CDLL:
@@ -104,6 +115,15 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.sgufp_frontier_take.argtypes = [P, C.c_int, C.c_int, P, P, P, P, P, P, P]
     lib.sgufp_bnb_step.argtypes = [P, C.c_int, P, P]
     lib.sgufp_bnb_set_limits.argtypes = [P, C.c_int, C.c_double]
+    lib.sgufp_comm_unique_id.argtypes = [P, C.c_int]
+    lib.sgufp_comm_init.argtypes = [P, C.c_int, C.c_int, P]
+    lib.sgufp_comm_info.argtypes = [P, P, P]
+    lib.sgufp_comm_destroy.argtypes = [P]
+    lib.sgufp_comm_destroy.restype = None
+    lib.sgufp_incumbent_allreduce.argtypes = [P, P]
+    lib.sgufp_cuts_exchange.argtypes = [P, P]
+    lib.sgufp_frontier_sizes.argtypes = [P, P]
+    lib.sgufp_frontier_balance.argtypes = [P, P]
     lib.sgufp_cuts_rows.argtypes = [P, C.c_int, C.c_int, C.c_int, P, P]
     lib.sgufp_restricted_relax.argtypes = [P, C.c_int, C.c_double]
     lib.sgufp_restricted_results.argtypes = [P, P, P, P, P, P]
@@ -496,6 +516,31 @@ class Engine:
         """Bound the refinement loops of one bnb_step (0: no limit); unfinished exact
         records go back on top of the frontier."""
         self._check(self.lib.sgufp_bnb_set_limits(self.ctx, int(max_refine_iters), C.c_double(round_seconds)))
+
+    # -- frontier shards over RCCL (shard.cpp) --------------------------------------
+    def comm_init(self, world: int, rank: int, uid: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self._check(self.lib.sgufp_comm_init(self.ctx, int(world), int(rank), buf))
+
+    def incumbent_allreduce(self, z: float) -> float:
+        v = C.c_double(z)
+        self._check(self.lib.sgufp_incumbent_allreduce(self.ctx, C.byref(v)))
+        return v.value
+
+    def cuts_exchange(self) -> int:
+        n = C.c_int64(0)
+        self._check(self.lib.sgufp_cuts_exchange(self.ctx, C.byref(n)))
+        return n.value
+
+    def frontier_sizes(self, world: int) -> List[int]:
+        a = (C.c_int64 * max(world, 1))()
+        self._check(self.lib.sgufp_frontier_sizes(self.ctx, a))
+        return [int(x) for x in a]
+
+    def frontier_balance(self) -> int:
+        n = C.c_int64(0)
+        self._check(self.lib.sgufp_frontier_balance(self.ctx, C.byref(n)))
+        return n.value
 
     # -- convenience: NodeExplorer::process for a list of nodes ----------------
     def relax(self, nodes: Sequence[NodeRecord], incumbent: float) -> List[RelaxResult]:

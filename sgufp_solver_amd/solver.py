@@ -41,7 +41,8 @@ class DDSolver:
     def __init__(self, network_path: Optional[str] = None, n_workers: int = 1, device: int = 0,
                  max_batch: int = 4096, batch_nodes: int = 0, engine=None, group=None, verbose: bool = True,
                  progress: float = 0.0, max_rounds: int = 0, dive_batch: int = 64, time_budget: float = 0.0,
-                 restricted_width: int = 0, round_seconds: float = 0.0, round_iters: int = 0):
+                 restricted_width: int = 0, round_seconds: float = 0.0, round_iters: int = 0,
+                 native_world: int = 0):
         """n_workers is accepted for API compatibility with the reference (threads there);
         the parallelism here is the batch of ``batch_nodes`` (<= max_batch) records per
         round and one rank per GPU."""
@@ -68,6 +69,11 @@ class DDSolver:
         # NodeExplorer::processX3 (NodeExplorer.cpp:605-796) on the root record seeds the
         # incumbent with the value of the routing its refinement loop converges to
         self.restricted_width = restricted_width
+        # > 0: the engine's context is one shard of an RCCL communicator of that many ranks
+        # (Engine.comm_init done by the caller) and the round's exchanges are the library's own
+        # (sgufp_incumbent_allreduce / _cuts_exchange / _frontier_sizes / _frontier_balance,
+        # shard.cpp: device buffers, no host staging); 0: torch.distributed (shards.py)
+        self.native_world = native_world
         # bound of one round's exact-leaf refinement loops (0: none; see Engine.bnb_set_limits)
         self.round_seconds = round_seconds
         self.round_iters = round_iters
@@ -94,10 +100,15 @@ class DDSolver:
     def start_solver(self, known_optimal: float) -> float:
         """DDSolver::startSolver (DDSolver.cpp:782-846): incumbent := known_optimal, the root
         record Node{} on the frontier (rank 0), rounds until every shard is empty."""
-        comm = self._comm()
+        comm = None if self.native_world else self._comm()
         self.shard_comm = comm
         rank = comm.rank if comm else 0
         eng = self.eng
+        if self.native_world:
+            import ctypes
+            w, r = ctypes.c_int(0), ctypes.c_int(0)
+            eng._check(eng.lib.sgufp_comm_info(eng.ctx, ctypes.byref(w), ctypes.byref(r)))
+            rank = r.value
         eng.frontier_clear()
         if rank == 0:
             eng.frontier_push([NodeRecord(0, DOUBLE_MIN, DOUBLE_MAX, [], [])])
@@ -147,6 +158,17 @@ class DDSolver:
             for k in keys:
                 self.counters[k] += int(getattr(st, k, 0) if not isinstance(st, dict) else st.get(k, 0))
             over = self.time_budget > 0 and time.perf_counter() - t_start > self.time_budget
+            if self.native_world:
+                z = eng.incumbent_allreduce(z)
+                eng.cuts_exchange()
+                sizes = eng.frontier_sizes(self.native_world)
+                if sum(sizes) == 0:
+                    self.complete = True
+                    break
+                if eng.incumbent_allreduce(1.0 if over else 0.0) > 0.0:
+                    break
+                self.received += eng.frontier_balance()
+                continue
             if comm is None:
                 if eng.frontier_size() == 0:
                     self.complete = True

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <stdexcept>
 #include <vector>
 
 #include "sgufp/inavap.hpp"
@@ -26,6 +27,17 @@ int main(int argc, char **argv) {
             Inavap::DDSolver solver{net, 4};
             auto [sol, secs] = solver.start(known);
             std::printf("ddsolver %a %.3f\n", sol, secs);
+        }
+        {
+            // the same search as a one-shard communicator: every round runs the RCCL
+            // exchanges of a multi-GPU search (shard.cpp) with a bounded refinement loop
+            uint8_t id[SGUFP_COMM_ID_BYTES];
+            if (sgufp_comm_unique_id(id, SGUFP_COMM_ID_BYTES) != SGUFP_OK) throw std::runtime_error("unique id");
+            Inavap::DDSolver solver{net, 4, 64};
+            solver.shard(1, 0, id);
+            solver.roundLimits(2, 0.0);
+            auto [sol, secs] = solver.start(known);
+            std::printf("sharded %a %.3f %lld\n", sol, secs, (long long)solver.totals.deferred);
         }
         Inavap::NodeExplorer explorer{net};
         Inavap::Container feas, opt;

@@ -75,6 +75,23 @@ def test_bnb_deferred_refinement_keeps_the_optimum(iters, batch):
     assert solver.counters["deferred"] > 0
 
 
+def test_native_shard_calls_single_rank():
+    """The library's own RCCL exchanges (shard.cpp) on a one-rank communicator: the search
+    runs them after every round (incumbent all-reduce, cut exchange, frontier sizes, work
+    sharing) and still ends at the extensive-form optimum; the calls are identities there."""
+    inst, path = _inst("T4", 3, 3)
+    opt = ef.solve(inst)
+    uid = E.comm_unique_id()
+    solver = DDSolver(path, max_batch=256, batch_nodes=8, max_rounds=50000, verbose=False, native_world=1)
+    solver.eng.comm_init(1, 0, uid)
+    assert solver.eng.incumbent_allreduce(12.5) == 12.5
+    assert solver.eng.frontier_sizes(1) == [0]
+    sol, _ = solver.start(DOUBLE_MIN)
+    assert abs(sol - opt) <= TOL * max(1.0, abs(opt))
+    assert solver.eng.cuts_exchange() == 0 and solver.received == 0
+    solver.eng.close()
+
+
 def _records(eng, n):
     """n real open-node records: root cutset children of a C2 instance."""
     eng.upload([NodeRecord(0, DOUBLE_MIN, DOUBLE_MAX, [], [])])

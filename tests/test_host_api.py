@@ -2,8 +2,10 @@
 
 CPU: the library exports the reference's class surface (Network, Inavap::NodeExplorer::process,
 Inavap::GuroSolver::solveSubProblem, Inavap::DDSolver::start / startSolver, Container::add).
-GPU: tests/host/host_api_test.cpp solves seeded instances twice -- Inavap::DDSolver::start
-(batched device rounds) and a reference-style single-worker LIFO loop over
+GPU: tests/host/host_api_test.cpp solves seeded instances three times -- Inavap::DDSolver::start
+(batched device rounds), the same as a one-rank RCCL shard with deferred refinement loops
+(DDSolver::shard, the exchanges of shard.cpp after every round), and a reference-style
+single-worker LIFO loop over
 NodeExplorer::process with two global Containers (DDSolver.cpp:658-776) -- and both optima
 must equal the extensive form within 1e-5 (main.cpp:43,76).
 """
@@ -43,8 +45,8 @@ def test_host_api_solves_to_the_extensive_form_optimum(cfg, seed, S, seeding):
     got = {}
     for line in r.stdout.splitlines():
         parts = line.split()
-        if parts and parts[0] in ("ddsolver", "explorer"):
+        if parts and parts[0] in ("ddsolver", "explorer", "sharded"):
             got[parts[0]] = float.fromhex(parts[1])
     assert "Optimal solution:" in r.stdout
-    for k in ("ddsolver", "explorer"):
+    for k in ("ddsolver", "explorer", "sharded"):
         assert abs(got[k] - opt) <= 1e-5 * max(1.0, abs(opt)), (k, got, opt)

@@ -155,6 +155,36 @@ def test_oracle_vs_reference_fresh_instances(oracle_bin, tmp_path, seed):
         assert (tmp_path / "a.txt").read_text() == (tmp_path / "b.txt").read_text()
 
 
+@pytest.mark.skipif(not os.path.exists(REF_BIN), reason="reference build (oracle/_ref) absent")
+@pytest.mark.parametrize("cfg,seed,n_nodes", [("C4", 1, 48), ("C5", 1, 4)])
+def test_oracle_vs_reference_at_bench_scale(oracle_bin, tmp_path, cfg, seed, n_nodes):
+    """The restatement is pinned at the scale the GPU parity tests use it: a BFS frontier of
+    the bench's C4 network (1k arcs) and of C5 (5k arcs, ~90k-node DDs) with the bench's
+    16F + 64O pool recipe, at DOUBLE_MIN and at the 40th percentile of the bounds (the
+    bench's incumbent rule: optimality prunes and width-1 pruning fire)."""
+    inst = instance.generate(instance.CONFIGS[cfg], seed, scenarios=2)
+    net = tmp_path / "net.txt"
+    inst.write(str(net))
+    pools.write_pool(str(tmp_path / "cuts.txt"), pools.synthetic_pool(inst, 16, 64, seed))
+    pools.write_pool(str(tmp_path / "none.txt"), [])
+    subprocess.run([REF_BIN, "bfs", str(net), str(tmp_path / "none.txt"), pools.DOUBLE_MIN.hex(), str(n_nodes),
+                    str(tmp_path / "nodes.txt")], check=True)
+    incs = [pools.DOUBLE_MIN]
+    threads = str(min(8, os.cpu_count() or 1))
+    subprocess.run([REF_BIN, "relaxp", str(net), str(tmp_path / "cuts.txt"), str(tmp_path / "nodes.txt"),
+                    pools.DOUBLE_MIN.hex(), threads, str(tmp_path / "a0.txt")], check=True, capture_output=True)
+    fin = [r.ub for r in pools.read_results(str(tmp_path / "a0.txt")) if r.status in (0, 3)]
+    incs.append(float(np.percentile(fin, 40)))
+    for k, inc in enumerate(incs):
+        a = tmp_path / f"a{k}.txt"
+        if k:
+            subprocess.run([REF_BIN, "relaxp", str(net), str(tmp_path / "cuts.txt"), str(tmp_path / "nodes.txt"),
+                            inc.hex(), threads, str(a)], check=True, capture_output=True)
+        subprocess.run([oracle_bin, "relax", str(net), str(tmp_path / "cuts.txt"), str(tmp_path / "nodes.txt"),
+                        inc.hex(), str(tmp_path / "b.txt")], check=True)
+        assert a.read_text() == (tmp_path / "b.txt").read_text(), f"incumbent {inc!r}"
+
+
 @pytest.mark.parametrize("name", ["c2_s2_dfs", "c3_s1_dfs"])
 def test_oracle_clean_under_sanitizers(tmp_path, name):
     """The restatement built with -fsanitize=address,undefined (oracle/Makefile `asan`, SURVEY.md
