@@ -26,6 +26,13 @@
 #include "ctx.hpp"
 
 namespace sgufp {
+hipError_t launch_loop_check(const BatchOut &out, const SeenLists &S, const int32_t *act, int na, int m, int32_t *flag,
+                             int32_t *chains, hipStream_t st);
+hipError_t launch_seen_append(const BatchOut &out, const SeenLists &S, const int32_t *fresh, int nf, int m,
+                              hipStream_t st);
+hipError_t launch_append_cuts(const int32_t *cut_type, const double *cut_rhs, const double *cut_row, int nf, int stride,
+                              int first, double *rows, double *rhs, double *coefT, const int32_t *slot_tab, int L,
+                              int us, double *row_ub, int32_t *row_id, uint8_t *is_feas, hipStream_t st);
 hipError_t launch_gather_rows(const double *rows, const double *rhs, const int32_t *ids, int k, int stride, double *out,
                               hipStream_t st);
 }  // namespace sgufp
@@ -79,6 +86,89 @@ bool sgufp_ctx::frontier_reserve(int64_t entries, size_t sol_entries) {
         fr.sol = s;
         fr_sol_cap = cap;
     }
+    return true;
+}
+
+bool sgufp_ctx::loop_reserve(int slots, int cap) {
+    const int Lc = std::max(sc.Lcap, 1);
+    if (!d_lact) {
+        const size_t B = (size_t)std::max(max_batch, 1);
+        if (!alloc(d_lact, B, "loop") || !alloc(d_lflag, B, "loop") || !alloc(d_lchain, B, "loop") ||
+            !alloc(d_lrowub, B, "loop"))
+            return false;
+    }
+    if (seen.paths && slots <= seen_slots && cap <= seen.cap) return true;
+    // grow (keeping the lists: a loop can outgrow the capacity mid-round)
+    const int ns = std::max(slots, seen_slots);
+    const int nc = std::max(cap, std::max(64, seen.cap ? 2 * seen.cap : 0));
+    SeenLists t{};
+    t.cap = nc;
+    t.Lcap = Lc;
+    if (!alloc(t.paths, (size_t)ns * nc * Lc, "seen paths") || !alloc(t.len, (size_t)ns * nc, "seen paths") ||
+        !alloc(t.hash, (size_t)ns * nc, "seen paths") || !alloc(t.n, (size_t)ns, "seen paths"))
+        return false;
+    if (seen.paths) {
+        const int oc = seen.cap;
+        for (int sl = 0; sl < seen_slots; sl++) {
+            if (!hip_ok(hipMemcpyAsync(t.paths + (size_t)sl * nc * Lc, seen.paths + (size_t)sl * oc * Lc,
+                                       (size_t)oc * Lc * 2, hipMemcpyDeviceToDevice, stream), "D2D") ||
+                !hip_ok(hipMemcpyAsync(t.len + (size_t)sl * nc, seen.len + (size_t)sl * oc, (size_t)oc * 2,
+                                       hipMemcpyDeviceToDevice, stream), "D2D") ||
+                !hip_ok(hipMemcpyAsync(t.hash + (size_t)sl * nc, seen.hash + (size_t)sl * oc, (size_t)oc * 8,
+                                       hipMemcpyDeviceToDevice, stream), "D2D"))
+                return false;
+        }
+        if (!hip_ok(hipMemcpyAsync(t.n, seen.n, (size_t)seen_slots * 4, hipMemcpyDeviceToDevice, stream), "D2D") ||
+            !sync())
+            return false;
+        release(seen.paths); release(seen.len); release(seen.hash); release(seen.n);
+    } else if (!hip_ok(hipMemsetAsync(t.n, 0, (size_t)ns * 4, stream), "memset")) {
+        return false;
+    }
+    seen = t;
+    seen_slots = ns;
+    return true;
+}
+
+// the same 64-bit order-free hash as path_hash (bnb_kernels.hip)
+static uint64_t mix64h(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+bool sgufp_ctx::seen_upload(int slot, const std::vector<std::vector<int16_t>> &paths) {
+    const int cnt = (int)paths.size();
+    if (cnt > seen.cap) return false;
+    std::vector<int16_t> flat((size_t)cnt * seen.Lcap, 0);
+    std::vector<uint16_t> len(cnt);
+    std::vector<uint64_t> h(cnt);
+    for (int i = 0; i < cnt; i++) {
+        const auto &p = paths[i];
+        len[i] = (uint16_t)p.size();
+        uint64_t x = 0;
+        for (size_t t = 0; t < p.size(); t++) {
+            flat[(size_t)i * seen.Lcap + t] = p[t];
+            x += mix64h(((uint64_t)(uint32_t)t << 16) ^ (uint64_t)(uint16_t)p[t] ^ 0x9E3779B97F4A7C15ull);
+        }
+        h[i] = x + mix64h((uint64_t)p.size() + 1);
+    }
+    const size_t e = (size_t)slot * seen.cap;
+    const int32_t n32 = cnt;
+    return upload(seen.paths + e * seen.Lcap, flat.data(), flat.size()) && upload(seen.len + e, len.data(), len.size()) &&
+           upload(seen.hash + e, h.data(), h.size()) && upload(seen.n + slot, &n32, 1) && sync();
+}
+
+bool sgufp_ctx::seen_download(int slot, int count, std::vector<std::vector<int16_t>> &paths) {
+    const size_t e = (size_t)slot * seen.cap;
+    std::vector<int16_t> flat((size_t)count * seen.Lcap);
+    std::vector<uint16_t> len(count);
+    if (!download(flat.data(), seen.paths + e * seen.Lcap, flat.size()) || !download(len.data(), seen.len + e, len.size()) ||
+        !sync())
+        return false;
+    paths.resize(count);
+    for (int i = 0; i < count; i++)
+        paths[i].assign(flat.begin() + (size_t)i * seen.Lcap, flat.begin() + (size_t)i * seen.Lcap + len[i]);
     return true;
 }
 
@@ -282,7 +372,7 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
         return SGUFP_ERR_HIP;
     if (ctx->timing) hipEventElapsedTime(&ctx->ms_relax, ctx->ev[0], ctx->ev[1]);
     S.ms_relax = ctx->timing ? ctx->ms_relax : 0.0;
-    std::vector<int> act;
+    std::vector<int> act, closed;
     for (int k = 0; k < b; k++) {
         switch (st[k]) {
             case SGUFP_PRUNED_BY_BOUND: S.pruned_bound++; continue;
@@ -306,102 +396,166 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
     }
     S.exact = (int64_t)act.size();
 
-    // 4: refinement loop of the exact DDs (NodeExplorer.cpp:946-969).  The loop of one record
-    // is a chain of dependent subproblems (one new cut per iteration); a round stops it after
-    // ctx->bnb_max_iters iterations or ctx->bnb_seconds, and the records still in their loop
-    // go back on top of the frontier (deferred) with the paths they have seen.  Popped again,
-    // such a record rebuilds its DD, applies the pool (its own new cuts included, so its bound
-    // is where the loop left it) and resumes the loop with that seen list: the loop ends
-    // exactly where the uninterrupted one would (a path repeats), whatever happened between.
-    std::vector<std::vector<std::vector<int16_t>>> seen(b);
-    std::vector<uint16_t> plen(b);
-    const size_t stride = (size_t)ctx->net.n_slots + 1;
+    // 4: refinement loop of the exact DDs (NodeExplorer.cpp:946-969), device-resident: per
+    // iteration k_loop_check (argmax path seen? -> {ub, ub}; else fresh), one synchronisation,
+    // then k_seen_append, the scenario subproblem on the fresh paths read in place,
+    // k_append_cuts (Container::add on the device) and k_refine, back to back on the stream.
+    // The host files the appended rows under the F / O lists at the next synchronisation.
+    // The loop of one record is a chain of dependent subproblems (one new cut per iteration);
+    // a round stops it after ctx->bnb_max_iters iterations or ctx->bnb_seconds, and the
+    // records still in their loop go back on top of the frontier (deferred) with the paths
+    // they have seen.  Popped again, such a record rebuilds its DD, applies the pool (its own
+    // new cuts included, so its bound is where the loop left it) and resumes the loop with
+    // that seen list: it ends exactly where the uninterrupted loop would (a path repeats).
     std::vector<int> deferred;
-    if (!act.empty() && !ctx->deferred_seen.empty()) {
-        for (int k : act) {
-            std::string key;
-            if (!ctx->record_key(base + k, key)) return SGUFP_ERR_HIP;
-            auto it = ctx->deferred_seen.find(key);
-            if (it != ctx->deferred_seen.end()) {
-                seen[k] = std::move(it->second);
+    std::vector<std::vector<std::vector<int16_t>>> seen_host;   // deferred records' lists
+    const int stride = ctx->net.n_slots + 1;
+    if (!act.empty()) {
+        if (!ctx->loop_reserve(b, 64)) return SGUFP_ERR_HIP;
+        std::vector<int32_t> nseen(b, 0);
+        if (!ctx->hip_ok(hipMemsetAsync(ctx->seen.n, 0, (size_t)b * 4, ctx->stream), "memset")) return SGUFP_ERR_HIP;
+        if (!ctx->deferred_seen.empty()) {
+            for (int k : act) {
+                std::string key;
+                if (!ctx->record_key(base + k, key)) return SGUFP_ERR_HIP;
+                auto it = ctx->deferred_seen.find(key);
+                if (it == ctx->deferred_seen.end()) continue;
+                const int cnt = (int)it->second.size();
+                if (!ctx->loop_reserve(b, cnt + 1)) return SGUFP_ERR_HIP;
+                if (!ctx->seen_upload(k, it->second)) return SGUFP_ERR_HIP;
+                nseen[k] = cnt;
                 ctx->deferred_seen.erase(it);
                 S.resumed++;
             }
         }
-    }
-    while (!act.empty()) {
-        if (!ctx->download(plen.data(), o.path_len, b) || !ctx->sync()) return SGUFP_ERR_HIP;
-        const int na = (int)act.size();
-        std::vector<int64_t> off(na + 1, 0);
-        for (int a = 0; a < na; a++) off[a + 1] = off[a] + plen[act[a]];
-        std::vector<int16_t> packed((size_t)off[na]);
-        if (!ctx->upload(ctx->d_bidx, act.data(), na) || !ctx->upload(ctx->d_boff, off.data(), na + 1) ||
-            !ctx->hip_ok(launch_gather_paths(o, ctx->sc.Lcap, ctx->d_bidx, ctx->d_boff, na, ctx->d_bpaths, ctx->stream),
-                         "k_gather_paths") ||
-            !ctx->download(packed.data(), ctx->d_bpaths, packed.size()) || !ctx->sync())
-            return SGUFP_ERR_HIP;
-        std::vector<int> fresh;
-        std::vector<int64_t> poff{0};
-        std::vector<int16_t> paths;
-        for (int a = 0; a < na; a++) {
-            const int k = act[a];
-            std::vector<int16_t> p(packed.begin() + off[a], packed.begin() + off[a + 1]);
-            auto &sv = seen[k];
-            if (std::find(sv.begin(), sv.end(), p) != sv.end()) {   // {ub, ub, {}, SUCCESS}
-                lbv[k] = ub[k];
-                S.exact_closed++;
-                continue;
-            }
-            paths.insert(paths.end(), p.begin(), p.end());
-            poff.push_back((int64_t)paths.size());
-            fresh.push_back(k);
-        }
-        act.clear();
-        if (fresh.empty()) break;
-        if ((ctx->bnb_max_iters > 0 && S.refine_iters >= ctx->bnb_max_iters) ||
-            (ctx->bnb_seconds > 0 && seconds_since(t_round) >= ctx->bnb_seconds)) {
-            deferred.swap(fresh);    // their current path is unseen: solved when resumed
-            break;
-        }
-        S.refine_iters++;
-        for (size_t i = 0; i < fresh.size(); i++)
-            seen[fresh[i]].emplace_back(paths.begin() + poff[i], paths.begin() + poff[i + 1]);
-        const int nf = (int)fresh.size();
-        std::vector<int32_t> type(nf);
-        std::vector<double> rhs(nf), rows((size_t)nf * stride);
-        int rc = sgufp_subproblem(ctx, nf, poff.data(), paths.data(), type.data(), rhs.data(), rows.data(), nullptr);
-        if (rc != SGUFP_OK) return rc;
-        S.subproblems += nf;
-        // Container::add in node order, feasibility list then optimality list
-        std::vector<int32_t> idx(nf), cut(nf);
-        std::vector<uint8_t> isf(nf);
-        for (int want = 1; want >= 0; want--) {
-            std::vector<double> r, h;
-            int cnt = 0, first = sgufp_cuts_count(ctx, want);
-            for (int i = 0; i < nf; i++) {
-                if (type[i] < 0) {
+        int na = (int)act.size();
+        if (!ctx->upload(ctx->d_lact, act.data(), (size_t)na)) return SGUFP_ERR_HIP;
+        std::vector<int32_t> flag, chains, ptype;
+        std::vector<double> pub;
+        std::vector<int> prev;            // fresh records of the previous iteration (rows filed below)
+        int prev_first = 0;
+        auto file_rows = [&]() -> bool {  // Container::add: feasibility list, optimality list
+            for (size_t i = 0; i < prev.size(); i++) {
+                if (ptype[i] < 0) {
                     ctx->err = "scenario subproblem failed (invalid path or numerical failure)";
-                    return SGUFP_ERR_STATE;
+                    return false;
                 }
-                if (type[i] != want) continue;
-                r.insert(r.end(), rows.begin() + (size_t)i * stride, rows.begin() + (size_t)(i + 1) * stride);
-                h.push_back(rhs[i]);
-                idx[i] = fresh[i];
-                isf[i] = (uint8_t)want;
-                cut[i] = first + cnt++;
             }
-            if (cnt && (rc = sgufp_cuts_append_rows(ctx, want, cnt, h.data(), r.data())) != SGUFP_OK) return rc;
-            (want ? S.new_feasibility_cuts : S.new_optimality_cuts) += cnt;
+            ctx->row_ub.resize((size_t)ctx->n_rows);
+            for (int want = 1; want >= 0; want--)
+                for (size_t i = 0; i < prev.size(); i++) {
+                    if (ptype[i] != want) continue;
+                    (want ? ctx->f_rows : ctx->o_rows).push_back(prev_first + (int)i);
+                    ctx->row_ub[(size_t)prev_first + i] = pub[i];
+                    (want ? S.new_feasibility_cuts : S.new_optimality_cuts)++;
+                }
+            ctx->order_dirty = true;
+            prev.clear();
+            return true;
+        };
+        while (na > 0) {
+            if (!ctx->hip_ok(launch_loop_check(o, ctx->seen, ctx->d_lact, na, ctx->net.m, ctx->d_lflag, ctx->d_lchain,
+                                               ctx->stream), "k_loop_check"))
+                return SGUFP_ERR_HIP;
+            flag.resize(na);
+            chains.resize(na);
+            ptype.resize(prev.size());
+            pub.resize(prev.size());
+            if (!ctx->download(flag.data(), ctx->d_lflag, (size_t)na) ||
+                !ctx->download(chains.data(), ctx->d_lchain, (size_t)na) ||
+                !ctx->download(ptype.data(), ctx->sio.cut_type, prev.size()) ||
+                !ctx->download(pub.data(), ctx->d_lrowub, prev.size()) || !ctx->sync())   // the one sync
+                return SGUFP_ERR_HIP;
+            if (!file_rows()) return SGUFP_ERR_STATE;
+            std::vector<int> fresh;
+            int nct = 1;
+            for (int a = 0; a < na; a++) {
+                const int k = act[a];
+                if (flag[a] == 1) {                 // {ub, ub, {}, SUCCESS}
+                    closed.push_back(k);
+                    S.exact_closed++;
+                } else if (flag[a] == 2) {
+                    fresh.push_back(k);
+                    nct = std::max(nct, chains[a]);
+                } else {
+                    st[k] = flag[a] - 3;
+                    if (st[k] == SGUFP_PRUNED_BY_FEASIBILITY_CUT) S.pruned_feasibility++;
+                    else if (st[k] == SGUFP_PRUNED_BY_OPTIMALITY_CUT) S.pruned_optimality++;
+                }
+            }
+            if (fresh.empty()) break;
+            if ((ctx->bnb_max_iters > 0 && S.refine_iters >= ctx->bnb_max_iters) ||
+                (ctx->bnb_seconds > 0 && seconds_since(t_round) >= ctx->bnb_seconds)) {
+                deferred.swap(fresh);    // their current path is unseen: solved when resumed
+                break;
+            }
+            // With a round deadline, one iteration solves at most kChunkLps scenario LPs
+            // (a 1024-leaf iteration of the 512-scenario C5 network would take minutes); the
+            // other fresh records stay in the loop unchanged (path not yet seen) for the next
+            // iteration, or are deferred at the deadline.
+            std::vector<int> rest;
+            if (ctx->bnb_seconds > 0) {
+                constexpr int64_t kChunkLps = 16384;
+                const size_t chunk = (size_t)std::max<int64_t>(1, kChunkLps / std::max(1, ctx->net.S));
+                if (fresh.size() > chunk) {
+                    rest.assign(fresh.begin() + (long)chunk, fresh.end());
+                    fresh.resize(chunk);
+                    nct = 1;
+                    for (int a = 0; a < na; a++)
+                        if (flag[a] == 2 && std::find(fresh.begin(), fresh.end(), act[a]) != fresh.end())
+                            nct = std::max(nct, chains[a]);
+                }
+            }
+            S.refine_iters++;
+            const int nf = (int)fresh.size();
+            int most = 0;
+            for (int k : fresh) most = std::max(most, ++nseen[k]);
+            if (!ctx->loop_reserve(b, most) || !ctx->upload(ctx->d_lact, fresh.data(), (size_t)nf) ||
+                !ctx->hip_ok(launch_seen_append(o, ctx->seen, ctx->d_lact, nf, ctx->net.m, ctx->stream), "k_seen_append") ||
+                !ctx->sub_init() || !ctx->sub_grow(nf, 1) || !ctx->grow_rows(ctx->n_rows + nf))
+                return SGUFP_ERR_HIP;
+            SubIO io = ctx->sio;
+            io.n_paths = nf;
+            io.nct_cap = nct;
+            io.path_slot = ctx->d_lact;
+            io.path_len = o.path_len;
+            io.path_stride = ctx->sc.Lcap;
+            io.paths = o.path;
+            io.path_off = nullptr;
+            if (!ctx->hip_ok(launch_subproblem(ctx->sn, io, ctx->stream), "subproblem launch")) return SGUFP_ERR_HIP;
+            ctx->sub_last_n = nf;
+            const int first = ctx->n_rows;
+            if (!ctx->hip_ok(launch_append_cuts(io.cut_type, io.cut_rhs, io.cut_row, nf, stride, first, ctx->d_rows,
+                                                ctx->d_rhs, ctx->d_coefT, ctx->nd.slot_tab, ctx->net.L, ctx->ustride,
+                                                ctx->d_lrowub, ctx->d_rcuts, ctx->d_rfeas, ctx->stream),
+                             "k_append_cuts") ||
+                !ctx->hip_ok(launch_refine(ctx->nd, ctx->sc, ctx->batch(), ctx->pool(), o, ctx->d_lact, ctx->d_rcuts,
+                                           ctx->d_rfeas, nf, z, ctx->stream), "k_refine"))
+                return SGUFP_ERR_HIP;
+            ctx->n_rows += nf;
+            S.subproblems += nf;
+            prev = fresh;
+            prev_first = first;
+            act = fresh;
+            act.insert(act.end(), rest.begin(), rest.end());
+            na = (int)act.size();
+            if (!rest.empty() && !ctx->upload(ctx->d_lact + nf, rest.data(), rest.size())) return SGUFP_ERR_HIP;
         }
-        if ((rc = sgufp_batch_refine(ctx, nf, idx.data(), isf.data(), cut.data(), z)) != SGUFP_OK) return rc;
-        std::vector<int32_t> st2(b);
-        if (!ctx->download(st2.data(), o.status, b) || !ctx->download(ub.data(), o.ub, b) || !ctx->sync())
-            return SGUFP_ERR_HIP;
-        for (int k : fresh) {
-            if (st2[k] == SGUFP_NEEDS_SUBPROBLEM) act.push_back(k);
-            else if (st2[k] == SGUFP_PRUNED_BY_FEASIBILITY_CUT) S.pruned_feasibility++;
-            else if (st2[k] == SGUFP_PRUNED_BY_OPTIMALITY_CUT) S.pruned_optimality++;
-            st[k] = st2[k];
+        if (!prev.empty()) {
+            ptype.resize(prev.size());
+            pub.resize(prev.size());
+            if (!ctx->download(ptype.data(), ctx->sio.cut_type, prev.size()) ||
+                !ctx->download(pub.data(), ctx->d_lrowub, prev.size()) || !ctx->sync())
+                return SGUFP_ERR_HIP;
+            if (!file_rows()) return SGUFP_ERR_STATE;
+        }
+        // bounds after the loop: closed records' lb (the incumbent candidates) and the
+        // deferred records' bound
+        if (!ctx->download(ub.data(), o.ub, b) || !ctx->sync()) return SGUFP_ERR_HIP;
+        for (int k : closed) lbv[k] = ub[k];
+        for (int k : deferred) {
+            seen_host.emplace_back();
+            if (!ctx->seen_download(k, nseen[k], seen_host.back())) return SGUFP_ERR_HIP;
         }
     }
 
@@ -432,7 +586,7 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
         for (int i = 0; i < nd; i++) {
             std::string key;
             sgufp_ctx::make_record_key(d_gl[i], d_mask[i], d_sol[i].data(), d_len[i], key);
-            ctx->deferred_seen[key] = std::move(seen[deferred[i]]);
+            ctx->deferred_seen[key] = std::move(seen_host[i]);
         }
     }
     S.deferred = nd;

@@ -673,6 +673,9 @@ int sgufp_subproblem(sgufp_ctx *ctx, int n, const int64_t *path_off, const int16
     }
     io.path_off = ctx->d_spoff;
     io.paths = ctx->d_spaths;
+    io.path_slot = nullptr;
+    io.path_len = nullptr;
+    io.path_stride = 0;
     if (!ctx->hip_ok(launch_subproblem(ctx->sn, io, ctx->stream), "subproblem launch")) return SGUFP_ERR_HIP;
     ctx->sub_last_n = n;
     const size_t stride = (size_t)ctx->net.n_slots + 1;

@@ -110,6 +110,15 @@ struct sgufp_ctx {
     std::unordered_map<std::string, std::vector<std::vector<int16_t>>> deferred_seen;
     static void make_record_key(uint16_t gl, uint32_t mask, const int16_t *sol, size_t len, std::string &key);
     bool record_key(int64_t entry, std::string &key);
+    // device-resident refinement loop (bnb.cpp, bnb_kernels.hip): seen-path lists per batch
+    // slot and the per-iteration index / flag arrays
+    SeenLists seen{};
+    int seen_slots = 0;
+    int32_t *d_lact = nullptr, *d_lflag = nullptr, *d_lchain = nullptr;
+    double *d_lrowub = nullptr;
+    bool loop_reserve(int slots, int cap);
+    bool seen_upload(int slot, const std::vector<std::vector<int16_t>> &paths);
+    bool seen_download(int slot, int count, std::vector<std::vector<int16_t>> &paths);
     int bnb_max_iters = 0;                    // refinement iterations per round (0: no limit)
     double bnb_seconds = 0.0;                 // refinement-loop seconds per round (0: no limit)
     bool relax_current(double optimal_lb);

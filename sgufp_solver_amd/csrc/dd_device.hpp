@@ -167,4 +167,14 @@ struct ChildOut {
     int16_t SGUFP_GBL *sol;
 };
 
+// Seen-path lists of the exact DDs' refinement loops (bnb_kernels.hip), per batch slot.
+struct SeenLists {
+    int16_t SGUFP_GBL *paths;   // [slots][cap][Lcap]
+    uint16_t SGUFP_GBL *len;    // [slots][cap]
+    uint64_t SGUFP_GBL *hash;   // [slots][cap]
+    int32_t SGUFP_GBL *n;       // [slots]
+    int cap;
+    int Lcap;
+};
+
 }  // namespace sgufp

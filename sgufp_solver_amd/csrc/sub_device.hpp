@@ -43,6 +43,11 @@ struct SubIO {
                                          // fewest decided arcs over the batch (host, per call)
     const int64_t SGUFP_GBL *path_off;   // [n_paths+1]
     const int16_t SGUFP_GBL *paths;
+    // paths read in place from the relaxation outputs (B&B refinement loop): path p is
+    // paths[path_slot[p] * path_stride ...] of length path_len[path_slot[p]]; path_off unused
+    const int32_t SGUFP_GBL *path_slot;  // null: path_off / paths as above
+    const uint16_t SGUFP_GBL *path_len;
+    int64_t path_stride;
     // per (path, scenario)
     int32_t SGUFP_GBL *status;           // [P*S]
     double SGUFP_GBL *obj;               // [P*S] scenario objective (optimal scenarios)

@@ -778,7 +778,15 @@ __global__ void __launch_bounds__(kWave * NW) k_sub_scenario(SubNet N, SubIO io)
 #endif
     const int n = N.n, m = N.m;
     const size_t so = (size_t)s * m;
-    const int64_t poff = io.path_off[p], plen = io.path_off[p + 1] - poff;
+    int64_t poff, plen;
+    if (io.path_slot) {
+        const int sl = io.path_slot[p];
+        poff = (int64_t)sl * io.path_stride;
+        plen = io.path_len[sl];
+    } else {
+        poff = io.path_off[p];
+        plen = io.path_off[p + 1] - poff;
+    }
     const size_t b = (size_t)p * S + s;
 
     // 1. decisions and matching
