@@ -144,6 +144,46 @@ def pmc_traffic(tag: str, workload: str, kernel: str = "k_relax"):
     return (FETCH_CORRECTION * np.mean(f) + np.mean(w)) * 1024.0, src
 
 
+def pmc_issue(tag: str, workload: str, kernel: str = "k_relax"):
+    """Issue-side counters of `kernel` (profiles/<tag>_pmc_issue, same build and workload as
+    the HBM passes): per launch the wave-instructions issued and where the waves' cycles went.
+    SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_ANY count quad-cycles and partition the
+    waves' lifetime (MI355X_MICROARCH.md, rocprofv3 PMC slots)."""
+    want = lib_sha256()
+    d = os.path.join(ROOT, "profiles", f"{tag}_pmc_issue")
+    try:
+        if open(os.path.join(d, "lib.sha256")).read().strip() != want or \
+                open(os.path.join(d, "workload.txt")).read().strip() != workload:
+            return None
+    except OSError:
+        return None
+    import csv
+    rows = []
+    for path in glob.glob(os.path.join(d, "*counter_collection.csv")):
+        with open(path) as fh:
+            rows += [r for r in csv.DictReader(fh) if kernel in r.get("Kernel_Name", "")]
+    if not rows:
+        return None
+    g = max(int(r["Grid_Size"]) for r in rows)
+    acc = {}
+    for r in rows:
+        if int(r["Grid_Size"]) == g:
+            acc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    c = {k: float(np.mean(v)) for k, v in acc.items()}
+    wc = c.get("SQ_WAVE_CYCLES", 0.0)
+    if not wc:
+        return None
+    waves = c.get("SQ_WAVES", 1.0)
+    return {"source": f"profiles/{tag}_pmc_issue (rocprofv3 --pmc SQ_*)",
+            "valu_insts_per_launch": c.get("SQ_INSTS_VALU"), "salu_insts_per_launch": c.get("SQ_INSTS_SALU"),
+            "valu_insts_per_wave": round(c.get("SQ_INSTS_VALU", 0.0) / waves),
+            "active_frac": round(c.get("SQ_ACTIVE_INST_ANY", 0.0) / wc, 4),
+            "wait_frac": round(c.get("SQ_WAIT_ANY", 0.0) / wc, 4),
+            "issue_stall_frac": round(c.get("SQ_WAIT_INST_ANY", 0.0) / wc, 4),
+            "cycles_per_wave_instruction": round(4.0 * wc / max(1.0, c.get("SQ_INSTS_VALU", 0.0) +
+                                                                 c.get("SQ_INSTS_SALU", 0.0)), 2)}
+
+
 def bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, work, device=0, progress=10.0, tag="bnb"):
     """The device DDSolver (sgufp_bnb_step rounds) from the root record Node{} with no
     incumbent, after a short warm-up search (kernels, allocations; its pool is cleared):
@@ -393,6 +433,7 @@ def main():
             "traffic_source": traffic_src,
             "avg_launch_ms": round(t_relax * 1e3, 4),
             "emit_ms": round(float(np.mean(emit_ms)), 4),
+            "issue": pmc_issue(args.profile_tag, workload_key(args)),
             "model_gbps": round(model_gbps, 2),
             "model_bytes_per_launch": bytes_model,
             "model": "SURVEY 8(d): 6A + sum over applied cuts (14A + 8N) + records (A, N, cuts counted per record)",

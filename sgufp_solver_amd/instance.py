@@ -49,6 +49,11 @@ CONFIGS = {
     "T2": InstanceConfig("T2", 24, 3, 4, 2, 0.6, 1),
     "T3": InstanceConfig("T3", 30, 3, 5, 2, 0.6, 1),
     "T4": InstanceConfig("T4", 40, 4, 5, 2, 0.4, 1),
+    # M1 / M2: the largest networks whose whole B&B tree and whose 64-scenario extensive form
+    # (HiGHS) both close in minutes -- the end-to-end optimum check of BASELINE configs[2]
+    # (64 scenarios) at a size that finishes; C3 itself closes neither
+    "M1": InstanceConfig("M1", 60, 4, 6, 2, 0.5, 64),
+    "M2": InstanceConfig("M2", 100, 5, 8, 2, 0.4, 64),
     "C1": InstanceConfig("C1", 40, 3, 6, 2, 1.0, 1),
     "C2": InstanceConfig("C2", 200, 6, 12, 3, 0.5, 1),
     "C3": InstanceConfig("C3", 1000, 12, 30, 3, 0.3, 64),

@@ -16,6 +16,8 @@ from sgufp_solver_amd import instance  # noqa: E402
 
 # (config, seed, scenarios)
 CASES = [("C1", 1, 1), ("C1", 2, 1), ("C1", 3, 1), ("C1", 4, 2), ("C1", 5, 3), ("C2", 1, 1), ("C2", 3, 2)]
+# lower bounds 0 (suffix "z"): the 64-scenario end-to-end case of tests/test_bnb.py
+CASES_LB0 = [("T4", 1, 64)]
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "extensive_form.json")
 
 
@@ -31,6 +33,17 @@ def main(argv):
             continue
         t = time.time()
         v = ef.solve(instance.generate(instance.CONFIGS[cfg], seed, scenarios=S))
+        data[k] = {"optimum": v, "optimum_hex": v.hex(), "seconds": round(time.time() - t, 2)}
+        print(k, data[k], flush=True)
+        json.dump(data, open(OUT, "w"), indent=1, sort_keys=True)
+    for cfg, seed, S in CASES_LB0:
+        k = key(cfg, seed, S) + "z"
+        if argv and k not in argv:
+            continue
+        inst = instance.generate(instance.CONFIGS[cfg], seed, scenarios=S)
+        inst.lb[:] = 0
+        t = time.time()
+        v = ef.solve(inst)
         data[k] = {"optimum": v, "optimum_hex": v.hex(), "seconds": round(time.time() - t, 2)}
         print(k, data[k], flush=True)
         json.dump(data, open(OUT, "w"), indent=1, sort_keys=True)

@@ -49,6 +49,28 @@ def test_bnb_optimum_matches_extensive_form(cfg, seed, S, seeding):
     assert solver.counters["exact_closed"] >= 1
 
 
+# T4 with BASELINE configs[2]'s 64 scenarios (lower bounds 0): the whole tree closes in
+# seconds.  The extensive-form optimum (HiGHS, 26 s on one core) is pinned here from
+# tests/golden/make_extensive_form.py ("T4-1-64z").  Larger 64-scenario networks (M1: 60 arcs,
+# 13 V-bar nodes; C3: 1000 arcs, 107) do not close -- DESIGN.md section 5.
+T4_64 = float.fromhex("0x1.b664400000000p+12")   # 7014.265625
+
+
+def test_bnb_64_scenarios_matches_extensive_form():
+    inst = instance.generate(instance.CONFIGS["T4"], 1, scenarios=64)
+    inst.lb[:] = 0
+    d = tempfile.mkdtemp(prefix="sgufp_bnb_")
+    path = os.path.join(d, "net.txt")
+    inst.write(path)
+    for seeding in ("opt-10", "none"):
+        known = T4_64 - 10.0 if seeding == "opt-10" else DOUBLE_MIN
+        solver = DDSolver(path, max_batch=1024, max_rounds=20000, verbose=False, round_seconds=5.0)
+        sol, _ = solver.start(known)
+        solver.eng.close()
+        assert solver.complete
+        assert abs(sol - T4_64) <= TOL * max(1.0, abs(T4_64)), (seeding, sol, T4_64, solver.counters)
+
+
 @pytest.mark.parametrize("batch", [1, 3, 64])
 def test_bnb_batch_size_does_not_change_the_optimum(batch):
     inst, path = _inst("T4", 3, 3)

@@ -12,6 +12,6 @@ FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-u
 for f in dd_kernels.hip bnb_kernels.hip rdd_kernels.hip; do
   cp sgufp_solver_amd/lib/obj/$f.o $OUT/obj/$f.o
 done
-for f in capi.cpp bnb.cpp network.cpp; do cp sgufp_solver_amd/lib/obj/$f.o $OUT/obj/$f.o; done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libsgufp_hip.so $OUT/obj/*.o
+for f in capi.cpp bnb.cpp network.cpp shard.cpp; do cp sgufp_solver_amd/lib/obj/$f.o $OUT/obj/$f.o; done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libsgufp_hip.so $OUT/obj/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo $OUT/libsgufp_hip.so
