@@ -251,14 +251,14 @@ def bnb_main(args):
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(local)
+        backend = dist_backend(torch)
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
         dist.init_process_group(backend)
     heartbeat("bnb", 20.0)
     work = tempfile.mkdtemp(prefix=f"sgufp_bnb_r{rank}_")
     out = bnb_run(args.bnb_config, args.seed, args.bnb_lb, args.bnb_seconds, args.nodes, args.round_seconds, work,
-                  device=local)
+                  device=local % max(1, torch.cuda.device_count()))
     line = {"metric": "device B&B: node relaxations/s (NodeExplorer::process incl. exact-leaf subproblems)",
             "value": out["relaxations_per_s"], "unit": "relaxations/s", "n_gpus": world,
             "higher_is_better": True, "scaling": "strong", "dtype": "f64", "data": "synthetic", **out}
@@ -266,6 +266,12 @@ def bnb_main(args):
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def dist_backend(torch) -> str:
+    """RCCL ("nccl") between GPUs; SGUFP_BENCH_BACKEND=gloo rehearses the multi-rank protocol
+    with several ranks on one card (RCCL refuses two ranks on one device)."""
+    return os.environ.get("SGUFP_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
 
 
 def heartbeat(tag="bench", every=30.0):
@@ -294,9 +300,9 @@ def main():
         import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(local)
+        backend = dist_backend(torch)
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
         dist.init_process_group(backend)
     import torch
 
@@ -311,7 +317,7 @@ def main():
     pool = pools.synthetic_pool(inst, args.n_feas, args.n_opt, args.seed)
 
     n = args.nodes
-    eng = E.Engine(net, local, max(n, 1024))
+    eng = E.Engine(net, local % max(1, torch.cuda.device_count()), max(n, 1024))
     if rank == 0:
         print(f"[bench] L={eng.info.total_layers} slots={eng.info.max_batch} node_cap={eng.info.node_capacity} "
               f"arc_cap={eng.info.arc_capacity} scratch={eng.info.scratch_bytes / 2**30:.2f} GiB", file=sys.stderr)
