@@ -129,7 +129,9 @@ int sgufp_batch_refine(sgufp_ctx *ctx, int n, const int32_t *node_idx, const uin
                        const int32_t *cut_index, double optimal_lb);
 
 /* Diagnostics of the last relax: wall_clock64 ticks (100 MHz) of each node's wave and
- * the number of batched-sweep restarts (exact single-cut redo after pruning). */
+ * the number of batched-sweep restarts (exact single-cut redo after pruning).  Ticks and
+ * phases are stamped only by the profiling build (sgufp_solver_amd/lib_prof, -DSGUFP_PHASES);
+ * the production library returns zeros for them. */
 int sgufp_batch_debug(sgufp_ctx *ctx, int64_t *ticks, int32_t *redo);
 /* ticks per phase [n * 8]: build, narrow sweep, tail layers, last layer, replay/post, redo, finish, tail */
 int sgufp_batch_phases(sgufp_ctx *ctx, int64_t *phase);

@@ -4,6 +4,9 @@
     lib_verify/libsgufp_hip.so
                       the same with SGUFP_SUB_VERIFY: every warm-started Bellman-Ford of the
                       subproblem is re-run cold and compared (debug build for tests)
+    lib_prof/libsgufp_hip.so
+                      the same with k_relax's per-wave clock stamps (SGUFP_PHASES) for the
+                      diagnostics tools; the production kernel carries none
     libsgufp_host.so  C++ mirror of the reference's host API (Network / NodeExplorer /
                       GuroSolver / DDSolver, include/sgufp/inavap.hpp) on top of the C ABI
     host_api_test     C++ driver of that API (tests/host/host_api_test.cpp)
@@ -77,6 +80,17 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
     vobjs = [vobj if os.path.basename(o) == "sub_kernels.hip.o" else o for o in objs]
     if force or _stale(vlib, vobjs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", vlib, *vobjs, *LINK])
+    # profiling variant: k_relax with its per-wave / per-phase clock stamps (tools/*_diag.py)
+    pdir = os.path.join(HERE, "lib_prof")
+    os.makedirs(pdir, exist_ok=True)
+    psrc = os.path.join(CSRC, "dd_kernels.hip")
+    pobj = os.path.join(objdir, "dd_kernels_prof.o")
+    if force or _stale(pobj, [psrc] + headers):
+        _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-DSGUFP_PHASES", "-x", "hip", "-c", psrc, "-o", pobj])
+    plib = os.path.join(pdir, "libsgufp_hip.so")
+    pobjs = [pobj if os.path.basename(o) == "dd_kernels.hip.o" else o for o in objs]
+    if force or _stale(plib, pobjs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", plib, *pobjs, *LINK])
     host_srcs = [os.path.join(CSRC, s) for s in HOST_SOURCES if os.path.exists(os.path.join(CSRC, s))]
     if host_srcs:
         hlib = os.path.join(LIBDIR, "libsgufp_host.so")

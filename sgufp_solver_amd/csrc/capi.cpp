@@ -881,6 +881,10 @@ int sgufp_batch_refine(sgufp_ctx *ctx, int n, const int32_t *node_idx, const uin
 
 int sgufp_batch_phases(sgufp_ctx *ctx, int64_t *phase) {
     if (!ctx || !ctx->relaxed || !phase) return ctx ? SGUFP_ERR_STATE : SGUFP_ERR_ARG;
+    if (!relax_has_phases()) {   // production build: no clock stamps in k_relax
+        std::fill(phase, phase + (size_t)ctx->n * 8, (int64_t)0);
+        return SGUFP_OK;
+    }
     std::vector<uint64_t> t((size_t)ctx->n * 8);
     if (!ctx->download(t.data(), ctx->out.phase, t.size()) || !ctx->sync()) return SGUFP_ERR_HIP;
     for (size_t k = 0; k < t.size(); k++) phase[k] = (int64_t)t[k];
@@ -894,8 +898,9 @@ int sgufp_batch_debug(sgufp_ctx *ctx, int64_t *ticks, int32_t *redo) {
     std::vector<uint32_t> r(n);
     if (!ctx->download(t.data(), ctx->out.ticks, n) || !ctx->download(r.data(), ctx->out.redo, n) || !ctx->sync())
         return SGUFP_ERR_HIP;
+    const bool stamped = relax_has_phases();
     for (int k = 0; k < n; k++) {
-        if (ticks) ticks[k] = (int64_t)t[k];
+        if (ticks) ticks[k] = stamped ? (int64_t)t[k] : 0;
         if (redo) redo[k] = (int32_t)r[k];
     }
     return SGUFP_OK;

@@ -36,6 +36,8 @@ hipError_t launch_gather_paths(const BatchOut &, int Lcap, const int32_t *idx, c
                                int16_t *dst, hipStream_t);
 hipError_t launch_push_children(const ChildOut &, const BatchOut &, const int32_t *parents, const int64_t *dst_child,
                                 const int64_t *dst_sol, int n, const FrontierDev &, hipStream_t);
+// 1 when k_relax was built with its per-wave clock stamps (SGUFP_PHASES, lib_prof/)
+bool relax_has_phases();
 // rdd_kernels.hip
 size_t rdd_lds_bytes(int Tcap, int Lcap, int us);
 hipError_t launch_restrict(const NetDev &, const BatchIn &, const Pool &, const RddIO &, double, hipStream_t);

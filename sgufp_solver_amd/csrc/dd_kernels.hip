@@ -1805,6 +1805,7 @@ struct LoopState {
     int last_cut;
     uint32_t applied;
     uint32_t redo;
+#ifdef SGUFP_PHASES
     uint64_t ph[8];   // diagnostic ticks per phase (see BatchOut::phase)
     uint64_t t;       // last stamp
     __device__ __forceinline__ void stamp(int k) {
@@ -1812,6 +1813,10 @@ struct LoopState {
         ph[k] += now - t;
         t = now;
     }
+#else
+    // the production build keeps no clock stamps in the hot kernel (lib_prof/ has them)
+    __device__ __forceinline__ void stamp(int) {}
+#endif
 };
 
 // one cut at a time from pool position s onwards
@@ -2274,7 +2279,9 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
     LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
     if ((int)blockIdx.x >= in.n) return;
     const int slot = in.perm ? in.perm[blockIdx.x] : (int)blockIdx.x;
+#ifdef SGUFP_PHASES
     const uint64_t t_start = wall_clock64();
+#endif
     DD d;
     dd_bind(d, smem, sc, slot, CB);
     d.stream = 0;
@@ -2287,7 +2294,11 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
     const GBL int16_t *rsol = in.sol + in.sol_off[slot];
     d.aligned = (d.len == d.g) ? 1 : 0;
     int cut_layer = 0;
+#ifdef SGUFP_PHASES
     LoopState st{kSuccess, in.ub[slot], -1, 0, 0, {0, 0, 0, 0, 0, 0, 0, 0}, t_start};
+#else
+    LoopState st{kSuccess, in.ub[slot], -1, 0, 0};
+#endif
     double lb = DMIN;
     uint32_t nchild = 0, n_nodes = 0, n_arcs = 0, n_merged = 0;
     d.T = 1; d.exact = 1;
@@ -2345,7 +2356,7 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
         build_stream(d, n_merged, CB * pool.ustride);   // tmir_cap = Ncap + Acap >= Nn + Amir
         if (d.stream) cut_loop_batched<CB>(net, d, sc, bv, pool, incumbent, st);
         else cut_loop_single(net, d, pool, incumbent, 0, st);
-#ifdef SGUFP_PROF
+#if defined(SGUFP_PROF) && defined(SGUFP_PHASES)
         st.ph[6] += bv.prof[0];
         st.ph[7] += bv.prof[1];
 #endif
@@ -2399,10 +2410,12 @@ done:
     }
     store_meta_layers(d, sc, slot, st.last_cut, st.status, cut_layer, st.ub);
     st.stamp(7);
+#ifdef SGUFP_PHASES
     if (lane() == 0) {
         out.ticks[slot] = wall_clock64() - t_start;
         for (int k = 0; k < 8; k++) out.phase[(size_t)slot * 8 + k] = st.ph[k];
     }
+#endif
 }
 
 // ------------------------------------------------------------------------------------
@@ -2589,6 +2602,14 @@ hipError_t launch_emit(const NetDev &net, const Scratch &sc, const BatchIn &in, 
     size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, 1, sc.us);
     hipLaunchKernelGGL(k_emit_children, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, co);
     return hipGetLastError();
+}
+
+bool relax_has_phases() {
+#ifdef SGUFP_PHASES
+    return true;
+#else
+    return false;
+#endif
 }
 
 hipError_t launch_refine(const NetDev &net, const Scratch &sc, const BatchIn &in, const Pool &pool,
