@@ -588,6 +588,11 @@ bool sgufp_ctx::sub_init() {
         for (int a = 0; a < m; a++) sr += std::abs((int64_t)rew[a]);
         for (size_t i = 0; i < ub.size(); i++) umax = std::max<int64_t>(umax, ub[i]);
         sn.cost_bound = 2 * (1 + 2 * sr * (umax + 1));
+        bool any_lb = false;
+        for (size_t i = 0; i < lb.size(); i++) any_lb |= lb[i] != 0;
+        sn.key32 = (!any_lb && sr < ((int64_t)1 << 18) && n + 2 < (1 << 11)) ? 1 : 0;
+        const char *ep = getenv("SGUFP_SUB_PREDS_LDS");
+        sn.preds_lds = (ep && atoi(ep) == 1) ? 1 : 0;
     }
     sn.tail = d_tail; sn.head = d_head; sn.vbar = d_vb; sn.inner = d_inner; sn.arc_layer = d_layer;
     sn.lb = d_lb; sn.ub = d_ub; sn.reward = d_rew;

@@ -23,7 +23,7 @@
 namespace sgufp {
 // dd_kernels.hip
 size_t relax_lds_bytes(int Tcap, int Lcap, int cb, int us);
-size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw);
+size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw, int kbytes = 8);
 hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st);
 hipError_t launch_relax(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &, double, int,
                         hipStream_t);

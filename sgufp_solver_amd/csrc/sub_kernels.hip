@@ -43,8 +43,20 @@ namespace sgufp {
 
 namespace {
 
-constexpr int64_t kInf = INT64_MAX / 4;
-constexpr int kHopBits = 16;
+// Bellman-Ford keys: (cost << hop bits) | hops.  64-bit keys in general (big-M costs of the
+// lower bounds); 32-bit keys when the launch has no lower bound and the rewards are small
+// (host check, launch_subproblem): half the LDS bytes and atomics, single-register adds.
+template <typename KT> struct KeyT;
+template <> struct KeyT<int64_t> {
+    static constexpr int hop_bits = 16;
+    static constexpr int64_t inf = INT64_MAX / 4;
+};
+template <> struct KeyT<int32_t> {
+    // |path cost| <= sum_a |r_a| < 2^18 (host), hops < 2^11: keys below 2^29 in magnitude
+    static constexpr int hop_bits = 11;
+    static constexpr int32_t inf = 1 << 30;
+};
+constexpr int64_t kInf = INT64_MAX / 4;   // 64-bit sentinel for capacities (delta)
 constexpr int kMaxChain = 64;      // arcs per chain (V-bar nodes in a row + 1)
 constexpr int32_t kNoPred = INT32_MAX;
 
@@ -53,15 +65,23 @@ constexpr int32_t kNoPred = INT32_MAX;
 //   cta: tail:16 | head:16 | reward sum:32          (-1 ends as 0xFFFF)
 //   ctb: max l:16 | min u:16 | flow x:16 | first arc:16
 // Node / arc ids fit 16 bits (Cut.h:342-344 packs them so); the host checks the bounds.
+// ALLREG: every chain group of the launch sits in the registers of the (single-wave) kernel
+// (nct_cap <= 16 x 64): no sweep reads chain records from LDS, predecessors come from the
+// registers too
+template <typename KT, bool ALLREG = false>
 struct SubLds {
+    using Key = KT;
+    static constexpr bool kAllReg = ALLREG;
+    static constexpr int kHop = KeyT<KT>::hop_bits;
+    static constexpr KT kKInf = KeyT<KT>::inf;
     LDS int16_t *dec;       // [m] decision at the head (out-arc id, -1 none, -2 head not V-bar);
                             //     phases 1-2 only (union), phase 5 reads dec_of from HBM
     LDS uint64_t *cta;      // [nct_cap] chains, in the topological order of their tails
     LDS uint64_t *ctb;      // [nct_cap]
     LDS int16_t *chosen;    // [m] in-arc that chose this out-arc of a V-bar node (phases 1-2;
                             //     aliases key / pred)
-    LDS int64_t *key;       // [n+2] Bellman-Ford keys (cost << 16 | hops); then alpha in place
-    LDS int64_t *alpha;     // == key: dual node potentials after the last Bellman-Ford
+    LDS KT *key;            // [n+2] Bellman-Ford keys (cost << hop bits | hops); then alpha in place
+    LDS KT *alpha;          // == key: dual node potentials after the last Bellman-Ford
     LDS int32_t *pred;      // [n+2] code of the tight in-arc << 15 | its tail (kNoPred: none)
     LDS uint16_t *plist;    // [n+2] arc codes of the augmenting path (sink to source)
     double GBL *coef;       // [n_slots] this (path, scenario)'s row of SubIO::coef (phase 5)
@@ -70,7 +90,7 @@ struct SubLds {
     LDS int64_t *red;       // [8] cross-wave reduction slots (multi-wave workgroups)
     LDS uint16_t *anc2;     // [n+2] second ancestor buffer of invalidate_subtrees (multi-wave)
 #ifdef SGUFP_SUB_VERIFY
-    LDS int64_t *vkey;      // [n+2] warm Bellman-Ford keys, compared with a cold run
+    LDS KT *vkey;           // [n+2] warm Bellman-Ford keys, compared with a cold run
 #endif
 };
 
@@ -112,12 +132,12 @@ struct Blk {
 // LDS: chains, then a union -- phases 1-2: chosen and dec (int16 [m] each);
 // phases 3-5: key (alpha), pred, plist -- then the free-node list and flags.
 constexpr int kSubLdsParts = 12;
-__host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int nz, int nw, size_t *off) {
+__host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int nz, int nw, size_t *off, int kbytes = 8) {
     size_t o = 0;
     off[1] = o; o = a16(o + (size_t)nct_cap * 8);
     off[2] = o; o = a16(o + (size_t)nct_cap * 8);
     const size_t u0 = o;
-    off[3] = o; o = a16(o + (size_t)(n + 2) * 8);   // key | chosen
+    off[3] = o; o = a16(o + (size_t)(n + 2) * kbytes);   // key | chosen
     off[4] = o; o = a16(o + (size_t)(n + 2) * 4);   // pred
     off[8] = o; o = a16(o + (size_t)(n + 2) * 2);   // plist
     off[11] = o; o = a16(o + (nw > 1 ? (size_t)(n + 2) * 2 : 0));   // anc2
@@ -128,7 +148,7 @@ __host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int 
     off[7] = o; o = a16(o + 8 * 4);
     off[10] = o; o = a16(o + (nw > 1 ? 8 * 8 : 0));   // red
 #ifdef SGUFP_SUB_VERIFY
-    off[9] = o; o = a16(o + (size_t)(n + 2) * 8);
+    off[9] = o; o = a16(o + (size_t)(n + 2) * kbytes);
 #endif
     return o;
 }
@@ -148,12 +168,13 @@ __device__ __forceinline__ uint64_t pack_b(int L, int U, int x, int first) {
            (uint64_t)(uint16_t)first << 48;
 }
 // the flow field of chain k (lane 0 augments)
-__device__ __forceinline__ LDS int16_t *ch_xp(const SubLds &W, int k) { return (LDS int16_t *)&W.ctb[k] + 2; }
+template <class WS>
+__device__ __forceinline__ LDS int16_t *ch_xp(const WS &W, int k) { return (LDS int16_t *)&W.ctb[k] + 2; }
 
-__device__ inline bool is_src(const SubNet &N, int v) { return N.in_off[v + 1] == N.in_off[v]; }
-__device__ inline bool is_snk(const SubNet &N, int v) { return N.out_off[v + 1] == N.out_off[v]; }
+__device__ __forceinline__ bool is_src(const SubNet &N, int v) { return N.in_off[v + 1] == N.in_off[v]; }
+__device__ __forceinline__ bool is_snk(const SubNet &N, int v) { return N.out_off[v + 1] == N.out_off[v]; }
 
-__device__ inline int slot_of(const SubNet &N, int layer, int j) {
+__device__ __forceinline__ int slot_of(const SubNet &N, int layer, int j) {
     for (int s = N.slot_off[layer]; s < N.slot_off[layer + 1]; s++)
         if (N.slot_head[s] == j) return s;
     return -1;
@@ -168,8 +189,8 @@ __device__ inline int slot_of(const SubNet &N, int layer, int j) {
 //             BIGM selects the big-M costs (dual ray) or the plain ones (optimal duals).
 enum BfMode { kSsp = 0, kPotPlain = 1, kPotBigM = 2 };
 
-template <int NW, typename F>
-__device__ inline void for_residual(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M, F visit) {
+template <int NW, typename F, class WS>
+__device__ __forceinline__ void for_residual(const SubNet &N, const WS &W, int nct, int nz, int mode, int64_t M, F visit) {
     using B = Blk<NW>;
     // contracted arcs: code 2k (forward), 2k+1 (backward)
     for (int k = B::tid(); k < nct; k += B::T) {
@@ -216,15 +237,17 @@ constexpr int kLargeWaves = SGUFP_LARGE_WAVES;
 static_assert(kLargeWaves >= 1 && kLargeWaves <= 8, "the cross-wave reduction array holds 8 waves");
 constexpr int kRegGroupsSmall = 16, kRegGroupsLarge = (80 + kLargeWaves - 1) / kLargeWaves;
 
+template <typename KT>
 struct ChainArcs {
     uint32_t th;
-    int64_t wf, wb;     // key increments (cost << 16) + 1
+    KT wf, wb;          // key increments (cost << hop bits) + 1
     int64_t cf, cbk;    // the costs
     bool fwd, bwd;
 };
 
-__device__ __forceinline__ ChainArcs chain_arcs(uint64_t ca, uint64_t cb, bool in_range, int n, int mode, int64_t M) {
-    ChainArcs c;
+template <typename KT>
+__device__ __forceinline__ ChainArcs<KT> chain_arcs(uint64_t ca, uint64_t cb, bool in_range, int n, int mode, int64_t M) {
+    ChainArcs<KT> c;
     const int t = ch_t(ca), h = ch_h(ca);
     const bool ok = in_range && t >= 0 && h >= 0;
     c.th = ok ? ((uint32_t)t | (uint32_t)h << 16) : ((uint32_t)n | (uint32_t)n << 16);
@@ -234,15 +257,16 @@ __device__ __forceinline__ ChainArcs chain_arcs(uint64_t ca, uint64_t cb, bool i
     const int64_t w_b = (mode == kPotPlain) ? R : R + (x <= L ? M : 0);
     c.cf = w_f;
     c.cbk = w_b;
-    c.wf = (w_f << kHopBits) + 1;
-    c.wb = (w_b << kHopBits) + 1;
+    c.wf = (KT)((w_f << KeyT<KT>::hop_bits) + 1);
+    c.wb = (KT)((w_b << KeyT<KT>::hop_bits) + 1);
     c.fwd = ok && x < U;
     c.bwd = ok && (mode == kPotPlain ? x > L : x > 0);
     return c;
 }
 
-// WT: the type the costs are kept in (int32_t for the large variant, whose host check bounds
-// the big-M costs below 2^30; the key increment (cost << 16) + 1 is formed at use)
+// WT: the type the costs are kept in: key increments (cost << hop bits) + 1, formed once, when
+// WT is the key type; costs, the increment formed at use, for the large variant with 64-bit keys
+// (int32_t, whose host check bounds the big-M costs below 2^30)
 template <int RG, typename WT>
 struct ChainRegs {
     uint32_t th[RG];
@@ -251,8 +275,9 @@ struct ChainRegs {
 };
 
 // register slot j of wave w holds chain group j * NW + w
-template <int RG, typename WT, int NW>
-__device__ __forceinline__ void load_chain_regs(const SubLds &W, int n, int nct, int mode, int64_t M, ChainRegs<RG, WT> &C) {
+template <int RG, typename WT, int NW, class WS>
+__device__ __forceinline__ void load_chain_regs(const WS &W, int n, int nct, int mode, int64_t M, ChainRegs<RG, WT> &C) {
+    using KT = typename WS::Key;
     C.fmask = 0;
     C.bmask = 0;
 #pragma unroll
@@ -260,9 +285,9 @@ __device__ __forceinline__ void load_chain_regs(const SubLds &W, int n, int nct,
         const int k = (g * NW + Blk<NW>::wid()) * kWave + lane();
         uint64_t ca = 0, cb = 0;
         if (k < nct) { ca = W.cta[k]; cb = W.ctb[k]; }
-        const ChainArcs c = chain_arcs(ca, cb, k < nct, n, mode, M);
+        const ChainArcs<KT> c = chain_arcs<KT>(ca, cb, k < nct, n, mode, M);
         C.th[g] = c.th;
-        if constexpr (sizeof(WT) == 8) {   // key increments, formed once
+        if constexpr (sizeof(WT) == sizeof(KT)) {   // key increments, formed once
             C.wf[g] = c.wf;
             C.wb[g] = c.wb;
         } else {                           // costs, the increment formed at use
@@ -290,26 +315,28 @@ __device__ __forceinline__ void load_chain_regs(const SubLds &W, int n, int nct,
 // wave) and a barrier closes the step: the groups of one step are consecutive chains, almost
 // always tails of one layer of the network, so the in-order propagation along runs of arcs
 // is kept.
-template <int RG, typename WT, int NW>
-__device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M,
+template <int RG, typename WT, int NW, class WS>
+__device__ __forceinline__ uint32_t bf_sweep(const SubNet &N, const WS &W, int nct, int nz, int mode, int64_t M,
                                     const ChainRegs<RG, WT> &C, bool forward) {
+    using KT = typename WS::Key;
+    constexpr KT kKInf = WS::kKInf;
     uint32_t changed = 0;
-    auto relax = [&](int v, int64_t nk) {
+    auto relax = [&](int v, KT nk) {
         if (nk < W.key[v]) {
             __hip_atomic_fetch_min(&W.key[v], nk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             changed = 1;
         }
     };
     // one arc of a group: both end keys in one LDS round trip, then the atomic minimum
-    auto arc = [&](uint32_t th, int64_t w, bool exists, bool forward) {
+    auto arc = [&](uint32_t th, KT w, bool exists, bool forward) {
         const int t = (int)(th & 0xFFFFu), h = (int)(th >> 16);
         const int u = forward ? t : h, v = forward ? h : t;
         // both end keys in one LDS round trip (fenced: the compiler would otherwise sink the
         // second load under the first comparison and pay two)
-        const int64_t ku = W.key[u], kv = W.key[v];
+        const KT ku = W.key[u], kv = W.key[v];
         sched_fence();
-        const int64_t nk = ku + w;
-        if (exists & (ku < kInf) & (nk < kv)) {
+        const KT nk = ku + w;
+        if (exists & (ku < kKInf) & (nk < kv)) {
             __hip_atomic_fetch_min(&W.key[v], nk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             changed = 1;
         }
@@ -323,7 +350,7 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
         cb = 0;
         if (k < nct) { ca = W.cta[k]; cb = W.ctb[k]; }
     };
-    auto reg_w = [&](WT w) -> int64_t { return sizeof(WT) == 8 ? (int64_t)w : ((int64_t)w << kHopBits) + 1; };
+    auto reg_w = [&](WT w) -> KT { return sizeof(WT) == sizeof(KT) ? (KT)w : (KT)(((int64_t)w << WS::kHop) + 1); };
     if constexpr (NW > 1) {
         using B = Blk<NW>;
         const int S = (G + NW - 1) / NW, wv = B::wid();
@@ -333,7 +360,7 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
                 if (g < G) {
                     uint64_t ca, cb;
                     fetch(g, ca, cb);
-                    const ChainArcs c = chain_arcs(ca, cb, g * kWave + lane() < nct, n, mode, M);
+                    const ChainArcs<KT> c = chain_arcs<KT>(ca, cb, g * kWave + lane() < nct, n, mode, M);
                     arc(c.th, c.wb, c.bwd, false);
                 }
                 __syncthreads();
@@ -351,8 +378,8 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
             return changed;
         }
         {
-            const int64_t kz = W.key[n];
-            if (kz < kInf)
+            const KT kz = W.key[n];
+            if (kz < kKInf)
                 for (int i = B::tid(); i < nz; i += B::T) {
                     const uint32_t e = (uint32_t)W.zlist[i];
                     if (mode != kSsp || ((e >> 30) & 1u)) relax((int)(e & 0x1FFFFFFFu), kz + 1);
@@ -371,7 +398,7 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
             if (g < G) {
                 uint64_t ca, cb;
                 fetch(g, ca, cb);
-                const ChainArcs c = chain_arcs(ca, cb, g * kWave + lane() < nct, n, mode, M);
+                const ChainArcs<KT> c = chain_arcs<KT>(ca, cb, g * kWave + lane() < nct, n, mode, M);
                 arc(c.th, c.wf, c.fwd, true);
             }
             __syncthreads();
@@ -379,8 +406,8 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
         for (int i = B::tid(); i < nz; i += B::T) {
             const uint32_t e = (uint32_t)W.zlist[i];
             const int v = (int)(e & 0x1FFFFFFFu);
-            const int64_t kv = W.key[v];
-            if (kv >= kInf) continue;
+            const KT kv = W.key[v];
+            if (kv >= kKInf) continue;
             if (mode == kSsp) { if ((e >> 29) & 1u) relax(n + 1, kv + 1); }
             else relax(n, kv + 1);
         }
@@ -388,11 +415,12 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
     }
     constexpr bool kPrefetch = RG >= 32;
     if (!forward) {
-        if (!kPrefetch) {
+        if constexpr (WS::kAllReg) {
+        } else if (!kPrefetch) {
             for (int g = G - 1; g >= RG; g--) {
                 uint64_t ca, cb;
                 fetch(g, ca, cb);
-                const ChainArcs c = chain_arcs(ca, cb, g * kWave + lane() < nct, n, mode, M);
+                const ChainArcs<KT> c = chain_arcs<KT>(ca, cb, g * kWave + lane() < nct, n, mode, M);
                 arc(c.th, c.wb, c.bwd, false);
             }
         } else if (G > RG) {
@@ -401,7 +429,7 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
             for (int g = G - 1; g >= RG; g--) {
                 const uint64_t ca = na, cb = nb;
                 if (g > RG) fetch(g - 1, na, nb);   // next group's chains load under this group's keys
-                const ChainArcs c = chain_arcs(ca, cb, g * kWave + lane() < nct, n, mode, M);
+                const ChainArcs<KT> c = chain_arcs<KT>(ca, cb, g * kWave + lane() < nct, n, mode, M);
                 arc(c.th, c.wb, c.bwd, false);
             }
         }
@@ -413,8 +441,8 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
     }
     // Z_out -> sources (SSP) / Z -> every free node (potentials), cost 0
     {
-        const int64_t kz = W.key[n];
-        if (kz < kInf)
+        const KT kz = W.key[n];
+        if (kz < kKInf)
             for (int i = lane(); i < nz; i += kWave) {
                 const uint32_t e = (uint32_t)W.zlist[i];
                 if (mode != kSsp || ((e >> 30) & 1u)) relax((int)(e & 0x1FFFFFFFu), kz + 1);
@@ -425,11 +453,12 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
     for (int g = 0; g < RG; g++) {
         if (g < G) arc(C.th[g], reg_w(C.wf[g]), (C.fmask >> g) & 1ull, true);
     }
-    if (!kPrefetch) {
+    if constexpr (WS::kAllReg) {
+    } else if (!kPrefetch) {
         for (int g = RG; g < G; g++) {
             uint64_t ca, cb;
             fetch(g, ca, cb);
-            const ChainArcs c = chain_arcs(ca, cb, g * kWave + lane() < nct, n, mode, M);
+            const ChainArcs<KT> c = chain_arcs<KT>(ca, cb, g * kWave + lane() < nct, n, mode, M);
             arc(c.th, c.wf, c.fwd, true);
         }
     } else if (G > RG) {
@@ -438,7 +467,7 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
         for (int g = RG; g < G; g++) {
             const uint64_t ca = na, cb = nb;
             if (g + 1 < G) fetch(g + 1, na, nb);
-            const ChainArcs c = chain_arcs(ca, cb, g * kWave + lane() < nct, n, mode, M);
+            const ChainArcs<KT> c = chain_arcs<KT>(ca, cb, g * kWave + lane() < nct, n, mode, M);
             arc(c.th, c.wf, c.fwd, true);
         }
     }
@@ -446,8 +475,8 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
     for (int i = lane(); i < nz; i += kWave) {
         const uint32_t e = (uint32_t)W.zlist[i];
         const int v = (int)(e & 0x1FFFFFFFu);
-        const int64_t kv = W.key[v];
-        if (kv >= kInf) continue;
+        const KT kv = W.key[v];
+        if (kv >= kKInf) continue;
         if (mode == kSsp) { if ((e >> 29) & 1u) relax(n + 1, kv + 1); }
         else relax(n, kv + 1);
     }
@@ -456,8 +485,8 @@ __device__ inline uint32_t bf_sweep(const SubNet &N, const SubLds &W, int nct, i
 
 // Iterate sweeps, forward and backward alternating, to the fixed point (false: not within
 // the pass bound).
-template <int RG, typename WT, int NW>
-__device__ inline bool bf_converge(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M,
+template <int RG, typename WT, int NW, class WS>
+__device__ __forceinline__ bool bf_converge(const SubNet &N, const WS &W, int nct, int nz, int mode, int64_t M,
                                    const ChainRegs<RG, WT> &C) {
     using B = Blk<NW>;
     bool prev_quiet = false;   // the sweep before the current one changed nothing
@@ -477,26 +506,64 @@ __device__ inline bool bf_converge(const SubNet &N, const SubLds &W, int nct, in
 // Predecessors of the SSP labels: the smallest arc code among the residual arcs into each
 // node that are tight in (cost, hops).  Hops grow by one along such arcs, so the
 // predecessor graph has no cycle and the walk from Z_in ends at Z_out.
-template <int NW>
-__device__ inline void ssp_preds(const SubNet &N, const SubLds &W, int nct, int nz, int64_t M) {
+template <int NW, class WS>
+__device__ __forceinline__ void ssp_preds(const SubNet &N, const WS &W, int nct, int nz, int64_t M) {
+    using KT = typename WS::Key;
     for_residual<NW>(N, W, nct, nz, kSsp, M, [&](int u, int v, int64_t w, int code) {
-        const int64_t ku = W.key[u];
-        if (ku >= kInf) return;
-        if (ku + (w << kHopBits) + 1 == W.key[v])
+        const KT ku = W.key[u];
+        if (ku >= WS::kKInf) return;
+        if ((KT)(ku + (KT)((w << WS::kHop) + 1)) == W.key[v])
             __hip_atomic_fetch_min(&W.pred[v], code << 15 | u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     });
     Blk<NW>::sync();
 }
 
+// Predecessors (as ssp_preds) from the register groups of one wave (every chain group in
+// registers): the costs are the ones the Bellman-Ford used, no chain record is re-read.
+template <int RG, typename WT, class WS>
+__device__ __forceinline__ void ssp_preds_regs(const SubNet &N, const WS &W, int nct, int nz, const ChainRegs<RG, WT> &C) {
+    using KT = typename WS::Key;
+    const int n = N.n, m = N.m;
+    const int G = (nct + kWave - 1) / kWave;
+    auto reg_w = [&](WT w) -> KT { return sizeof(WT) == sizeof(KT) ? (KT)w : (KT)(((int64_t)w << WS::kHop) + 1); };
+    auto tight = [&](int u, int v, KT w, int code, bool exists) {
+        const KT ku = W.key[u], kv = W.key[v];
+        sched_fence();
+        if (exists & (ku < WS::kKInf) & ((KT)(ku + w) == kv))
+            __hip_atomic_fetch_min(&W.pred[v], code << 15 | u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+#pragma unroll
+    for (int g = 0; g < RG; g++) {
+        if (g < G) {
+            const uint32_t th = C.th[g];
+            tight((int)(th & 0xFFFFu), (int)(th >> 16), reg_w(C.wf[g]), 2 * (g * kWave + lane()), (C.fmask >> g) & 1ull);
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < RG; g++) {
+        if (g < G) {
+            const uint32_t th = C.th[g];
+            tight((int)(th >> 16), (int)(th & 0xFFFFu), reg_w(C.wb[g]), 2 * (g * kWave + lane()) + 1, (C.bmask >> g) & 1ull);
+        }
+    }
+    for (int i = lane(); i < nz; i += kWave) {
+        const uint32_t e = (uint32_t)W.zlist[i];
+        const int v = (int)(e & 0x1FFFFFFFu);
+        if ((e >> 30) & 1u) tight(n, v, (KT)1, 2 * m + 2 * v, true);
+        if ((e >> 29) & 1u) tight(v, n + 1, (KT)1, 2 * m + 2 * v + 1, true);
+    }
+    wave_lds_sync();
+}
+
 // warm: keep the keys (exact or infinite, see invalidate_subtrees) instead of starting from
 // Z_out alone -- Bellman-Ford from any upper bounds of the shortest keys reaches them.
-template <int RG, typename WT, int NW>
-__device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, int nz, int mode, int64_t M,
+template <int RG, typename WT, int NW, class WS>
+__device__ __forceinline__ bool bellman_ford(const SubNet &N, const WS &W, int nct, int nz, int mode, int64_t M,
                                     bool warm = false) {
     using B = Blk<NW>;
     const int nn = N.n + 2;
     for (int v = B::tid(); v < nn; v += B::T) {
-        if (!warm) W.key[v] = (mode == kSsp) ? (v == N.n ? 0 : kInf) : 0;
+        if (!warm) W.key[v] = (mode == kSsp) ? (v == N.n ? 0 : WS::kKInf) : 0;
         W.pred[v] = kNoPred;
     }
     ChainRegs<RG, WT> C;
@@ -510,7 +577,7 @@ __device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, i
     if (warm) {
         for (int v = B::tid(); v < nn; v += B::T) {
             W.vkey[v] = W.key[v];
-            W.key[v] = (v == N.n) ? 0 : kInf;
+            W.key[v] = (v == N.n) ? 0 : WS::kKInf;
         }
         B::sync();
         const bool cold_ok = bf_converge<RG, WT, NW>(N, W, nct, nz, mode, M, C);
@@ -520,11 +587,14 @@ __device__ inline bool bellman_ford(const SubNet &N, const SubLds &W, int nct, i
         B::sync();
     }
 #endif
-    ssp_preds<NW>(N, W, nct, nz, M);
+    // one wave with every chain group in registers: predecessors from the registers
+    if constexpr (NW == 1 && WS::kAllReg) ssp_preds_regs<RG, WT>(N, W, nct, nz, C);
+    else ssp_preds<NW>(N, W, nct, nz, M);
     return true;
 }
 
-__device__ inline int64_t key_cost(int64_t k) { return k >> kHopBits; }
+template <class WS>
+__device__ __forceinline__ int64_t key_cost(typename WS::Key k) { return (int64_t)(k >> WS::kHop); }
 
 // After an augmentation along the predecessor path of Z_in, whose used-up arcs (those whose
 // residual segment the bottleneck exhausted: the arc vanishes or its big-M cost changes)
@@ -538,8 +608,9 @@ __device__ inline int64_t key_cost(int64_t k) { return k >> kHopBits; }
 // With several waves the rounds are double-buffered (every pointer of a round is read from
 // the previous round's buffer); a node killed in the same round as a descendant reads it is
 // caught one round later through the very ancestor that killed it.
-template <int NW>
-__device__ inline void invalidate_subtrees(const SubNet &N, const SubLds &W) {
+template <int NW, class WS>
+__device__ __forceinline__ void invalidate_subtrees(const SubNet &N, const WS &W) {
+    constexpr auto kKInf = WS::kKInf;
     const int nn = N.n + 2;
     if constexpr (NW > 1) {
         using B = Blk<NW>;
@@ -554,7 +625,7 @@ __device__ inline void invalidate_subtrees(const SubNet &N, const SubLds &W) {
             for (int v = B::tid(); v < nn; v += B::T) {
                 const int a = a_in[v];
                 const int aa = a_in[a];
-                if (W.key[a] >= kInf && W.key[v] < kInf) W.key[v] = kInf;
+                if (W.key[a] >= kKInf && W.key[v] < kKInf) W.key[v] = kKInf;
                 a_out[v] = (uint16_t)aa;
                 moved |= (aa != a) ? 1u : 0u;
             }
@@ -576,8 +647,8 @@ __device__ inline void invalidate_subtrees(const SubNet &N, const SubLds &W) {
         for (int v = lane(); v < nn; v += kWave) {
             const int a = anc[v];
             const int aa = anc[a];
-            const bool dead_a = W.key[a] >= kInf, dead_v = W.key[v] >= kInf;
-            if (dead_a && !dead_v) W.key[v] = kInf;
+            const bool dead_a = W.key[a] >= kKInf, dead_v = W.key[v] >= kKInf;
+            if (dead_a && !dead_v) W.key[v] = kKInf;
             if (aa != a) { anc[v] = (uint16_t)aa; moved = 1; }
         }
         wave_lds_sync();
@@ -598,7 +669,8 @@ struct ChainOut {
     int64_t obj;     // sum (u gamma - l beta): the dual objective at y-bar
 };
 
-__device__ inline void add_coef(const SubNet &N, const SubLds &W, int layer, int j, int64_t v) {
+template <class WS>
+__device__ __forceinline__ void add_coef(const SubNet &N, const WS &W, int layer, int j, int64_t v) {
     if (v == 0) return;
     const int s = slot_of(N, layer, j);
     // integral values far below 2^53: the sum is exact in any order
@@ -606,27 +678,30 @@ __device__ inline void add_coef(const SubNet &N, const SubLds &W, int layer, int
 }
 
 // sigma on in-arc a of V-bar node q: every (i, q, j) of q gets u_iq * sigma (grb.cpp:257-266)
-__device__ inline void add_sigma(const SubNet &N, const SubLds &W, int a, int64_t sig, int s) {
+template <class WS>
+__device__ __forceinline__ void add_sigma(const SubNet &N, const WS &W, int a, int64_t sig, int s) {
     if (sig == 0) return;
     const int q = N.head[a], layer = N.arc_layer[a];
     const int64_t u = N.ub[(size_t)s * N.m + a];
     for (int k = N.out_off[q]; k < N.out_off[q + 1]; k++) add_coef(N, W, layer, N.head[N.out_list[k]], u * sig);
 }
 // phi on out-arc b of V-bar node q: every (i, q, j) of q gets u_qj * phi (grb.cpp:268-277)
-__device__ inline void add_phi(const SubNet &N, const SubLds &W, int b, int64_t ph, int s) {
+template <class WS>
+__device__ __forceinline__ void add_phi(const SubNet &N, const WS &W, int b, int64_t ph, int s) {
     if (ph == 0) return;
     const int q = N.tail[b], j = N.head[b];
     const int64_t u = N.ub[(size_t)s * N.m + b];
     for (int k = N.in_off[q]; k < N.in_off[q + 1]; k++) add_coef(N, W, N.arc_layer[N.in_list[k]], j, u * ph);
 }
 
-__device__ inline int64_t alpha_of(const SubNet &N, const SubLds &W, int v) {
-    return (v >= 0 && N.inner[v] && !N.vbar[v]) ? W.alpha[v] : 0;
+template <class WS>
+__device__ __forceinline__ int64_t alpha_of(const SubNet &N, const WS &W, int v) {
+    return (v >= 0 && N.inner[v] && !N.vbar[v]) ? (int64_t)W.alpha[v] : 0;
 }
 
 // Decision at the head of arc a from the path in HBM (phase 1 keeps it in LDS as dec; the
 // dual assembly re-reads it, the LDS space being reused)
-__device__ inline int dec_of(const SubNet &N, const SubIO &io, int64_t poff, int64_t plen, int a) {
+__device__ __forceinline__ int dec_of(const SubNet &N, const SubIO &io, int64_t poff, int64_t plen, int a) {
     const int q = N.head[a];
     if (!N.vbar[q]) return -2;
     const int l = N.arc_layer[a];
@@ -641,7 +716,8 @@ __device__ inline int dec_of(const SubNet &N, const SubIO &io, int64_t poff, int
 // memory): the first walk gets its length, reward sum, binding arcs and the transfer total
 // of a broken start; the second emits e, the transfers of the matched pairs and sigma / phi,
 // in the order of the closed forms below (all integers: any summation order is exact).
-__device__ ChainOut assemble_chain(const SubNet &N, const SubLds &W, const SubIO &io, int64_t poff, int64_t plen,
+template <class WS>
+__device__ __forceinline__ ChainOut assemble_chain(const SubNet &N, const WS &W, const SubIO &io, int64_t poff, int64_t plen,
                                    int k, int s, bool ray_mode, int ray_p, int ray_q, bool &ok) {
     ChainOut o{0, 0};
     const uint64_t ca = W.cta[k], cb = W.ctb[k];
@@ -747,8 +823,9 @@ __device__ ChainOut assemble_chain(const SubNet &N, const SubLds &W, const SubIO
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
-template <int RG, typename WT, int NW>
+template <int RG, typename WT, int NW, typename KT, bool ALLREG>
 __global__ void __launch_bounds__(kWave * NW) k_sub_scenario(SubNet N, SubIO io) {
+    using WS = SubLds<KT, ALLREG>;
     using B = Blk<NW>;
     const int tid = B::tid();
     constexpr int T = B::T;
@@ -758,13 +835,13 @@ __global__ void __launch_bounds__(kWave * NW) k_sub_scenario(SubNet N, SubIO io)
     const int p = blockIdx.x / S, s = blockIdx.x - p * S;
     if (p >= io.n_paths) return;
     size_t off[kSubLdsParts];
-    sub_lds_layout(N.n, N.m, io.nct_cap, N.nz, NW, off);
-    SubLds W;
+    sub_lds_layout(N.n, N.m, io.nct_cap, N.nz, NW, off, (int)sizeof(KT));
+    WS W;
     W.dec = (LDS int16_t *)(smem + off[0]);
     W.cta = (LDS uint64_t *)(smem + off[1]);
     W.ctb = (LDS uint64_t *)(smem + off[2]);
     W.chosen = (LDS int16_t *)(smem + off[3]);
-    W.key = (LDS int64_t *)(smem + off[3]);
+    W.key = (LDS KT *)(smem + off[3]);
     W.alpha = W.key;
     W.pred = (LDS int32_t *)(smem + off[4]);
     W.plist = (LDS uint16_t *)(smem + off[8]);
@@ -774,7 +851,7 @@ __global__ void __launch_bounds__(kWave * NW) k_sub_scenario(SubNet N, SubIO io)
     W.red = (LDS int64_t *)(smem + off[10]);
     W.anc2 = (LDS uint16_t *)(smem + off[11]);
 #ifdef SGUFP_SUB_VERIFY
-    W.vkey = (LDS int64_t *)(smem + off[9]);
+    W.vkey = (LDS KT *)(smem + off[9]);
 #endif
     const int n = N.n, m = N.m;
     const size_t so = (size_t)s * m;
@@ -893,6 +970,7 @@ __global__ void __launch_bounds__(kWave * NW) k_sub_scenario(SubNet N, SubIO io)
     // sum of the chains' capacities (min u): the loop below stops after that many.
     max_aug = B::all(max_aug, [](int64_t x, int64_t y) { return x + y; }, W.red);
     int ray_chain = -1, ray_p = -1, ray_q = -1;
+    int err_site = 0;   // which check failed (an error scenario reports it as its dual: diagnostics)
     int64_t primal = 0;
 
     if (first_bad != INT_MAX) {
@@ -937,14 +1015,14 @@ __global__ void __launch_bounds__(kWave * NW) k_sub_scenario(SubNet N, SubIO io)
         bool warm = false;
         for (; status == kSubOptimal; iters++) {
             SUB_T0();
-            if (!bellman_ford<RG, WT, NW>(N, W, nct, nz, kSsp, M, warm)) { status = kSubError; break; }
+            if (!bellman_ford<RG, WT, NW>(N, W, nct, nz, kSsp, M, warm)) { status = kSubError; err_site = 1; break; }
             SUB_T1(t_bf);
 #ifdef SGUFP_SUB_VERIFY
             if (W.misc[6]) { status = kSubError; break; }
 #endif
-            const int64_t kz = W.key[n + 1];
-            if (kz >= kInf || key_cost(kz) >= 0) break;
-            if (iters >= max_aug) { status = kSubError; break; }   // cannot happen (bound above)
+            const KT kz = W.key[n + 1];
+            if (kz >= WS::kKInf || key_cost<WS>(kz) >= 0) break;
+            if (iters >= max_aug) { status = kSubError; err_site = 2; break; }   // cannot happen (bound above)
             // lane 0 chases the predecessors from Z_in back to Z_out into a list (one LDS
             // round trip per arc: the entry holds the tail), then the wave takes the
             // bottleneck and augments (a simple path uses each chain once)
@@ -971,7 +1049,7 @@ __global__ void __launch_bounds__(kWave * NW) k_sub_scenario(SubNet N, SubIO io)
                 delta = cap < delta ? cap : delta;
             }
             delta = B::all(delta, [](int64_t p, int64_t q) { return p < q ? p : q; }, W.red);
-            if (plen < 0 || delta <= 0 || delta >= kInf) { status = kSubError; break; }
+            if (plen < 0 || delta <= 0 || delta >= kInf) { status = kSubError; err_site = plen < 0 ? 3 : 4; break; }
             for (int i = tid; i < plen; i += T) {
                 const int code = W.plist[i];
                 if (code >= 2 * m) continue;
@@ -980,7 +1058,7 @@ __global__ void __launch_bounds__(kWave * NW) k_sub_scenario(SubNet N, SubIO io)
                 const int64_t x = ch_x(cb), L = ch_L(cb), U = ch_U(cb);
                 const int64_t cap = (code & 1) ? (x > L ? x - L : x) : (x < L ? L - x : U - x);
                 *ch_xp(W, k) += (int16_t)((code & 1) ? -delta : delta);
-                if (cap == delta) W.key[(code & 1) ? ch_t(ca) : ch_h(ca)] = kInf;   // segment used up
+                if (cap == delta) W.key[(code & 1) ? ch_t(ca) : ch_h(ca)] = WS::kKInf;   // segment used up
             }
             B::sync();
             SUB_T1(t_walk);
@@ -1014,18 +1092,18 @@ __global__ void __launch_bounds__(kWave * NW) k_sub_scenario(SubNet N, SubIO io)
             //    costs (their M-multiple is a dual ray, case (iii))
             const int mode = unmet ? kPotBigM : kPotPlain;
             if (unmet) status = kSubInfeasible;
-            if (!bellman_ford<RG, WT, NW>(N, W, nct, nz, mode, M)) status = kSubError;
-            const int64_t dz = key_cost(W.key[n]);
+            if (!bellman_ford<RG, WT, NW>(N, W, nct, nz, mode, M)) { status = kSubError; err_site = 5; }
+            const int64_t dz = key_cost<WS>(W.key[n]);
             B::sync();   // every thread read Z's key before the alphas overwrite it in place
             for (int v = tid; v < n; v += T) {
-                int64_t d = key_cost(W.key[v]) - dz;
+                int64_t d = key_cost<WS>(W.key[v]) - dz;
                 int64_t al;
                 if (mode == kPotPlain) al = -d;
                 else {
                     const int64_t r = (d >= 0 ? d + M / 2 : d - M / 2) / M;   // round(d / M)
                     al = -r;
                 }
-                W.alpha[v] = (N.inner[v] && !N.vbar[v]) ? al : 0;
+                W.alpha[v] = (KT)((N.inner[v] && !N.vbar[v]) ? al : 0);
             }
             B::sync();
         }
@@ -1052,13 +1130,13 @@ __global__ void __launch_bounds__(kWave * NW) k_sub_scenario(SubNet N, SubIO io)
             rhs += d0;
             dual += d0;
         }
-        if (!ok || (ray ? dual >= 0 : dual != primal)) status = kSubError;
+        if (!ok || (ray ? dual >= 0 : dual != primal)) { status = kSubError; err_site = ok ? 6 : 7; }
     }
     B::sync();
     if (tid == 0) {
         io.status[b] = status;
         io.obj[b] = (double)primal;
-        io.dual[b] = (double)dual;
+        io.dual[b] = status == kSubError ? -(double)err_site : (double)dual;
         io.rhs[b] = (double)rhs;
     }
 }
@@ -1117,14 +1195,16 @@ __global__ void __launch_bounds__(256) k_sub_reduce(SubNet N, SubIO io) {
 }
 
 // ---------------------------------------------------------------------------------------
-size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw) {
+size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw, int kbytes) {
     size_t off[kSubLdsParts];
-    return sub_lds_layout(n, m, nct_cap, nz, nw, off);
+    return sub_lds_layout(n, m, nct_cap, nz, nw, off, kbytes);
 }
 
-hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st) {
-    if (io.n_paths <= 0) return hipSuccess;
-    size_t lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, 1);
+namespace {
+template <typename KT>
+hipError_t launch_scenarios(const SubNet &N, const SubIO &io, hipStream_t st) {
+    constexpr int kb = (int)sizeof(KT);
+    size_t lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, 1, kb);
 #ifdef SGUFP_SUB_LDS_MIN
     if (lds < SGUFP_SUB_LDS_MIN) lds = SGUFP_SUB_LDS_MIN;   // occupancy experiments
 #endif
@@ -1133,13 +1213,29 @@ hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st) {
     const bool large = lds > 64 * 1024 && io.nct_cap > kRegGroupsSmall * kWave && N.cost_bound < ((int64_t)1 << 30);
     const char *ev = getenv("SGUFP_SUB_WAVES");
     if (large && !(ev && atoi(ev) == 1)) {
-        lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, kLargeWaves);
-        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsLarge, int32_t, kLargeWaves>), dim3((unsigned)io.n_paths * N.S),
-                           dim3(kWave * kLargeWaves), lds, st, N, io);
+        lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, kLargeWaves, kb);
+        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsLarge, int32_t, kLargeWaves, KT, false>),
+                           dim3((unsigned)io.n_paths * N.S), dim3(kWave * kLargeWaves), lds, st, N, io);
+    } else if (io.nct_cap <= kRegGroupsSmall * kWave && !N.preds_lds) {
+        // register groups hold key increments: 64-bit with 64-bit keys, 32-bit with 32-bit keys
+        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsSmall, KT, 1, KT, true>), dim3((unsigned)io.n_paths * N.S),
+                           dim3(kWave), lds, st, N, io);
     } else {
-        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsSmall, int64_t, 1>), dim3((unsigned)io.n_paths * N.S), dim3(kWave),
-                           lds, st, N, io);
+        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsSmall, KT, 1, KT, false>), dim3((unsigned)io.n_paths * N.S),
+                           dim3(kWave), lds, st, N, io);
     }
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st) {
+    if (io.n_paths <= 0) return hipSuccess;
+    // 32-bit keys (N.key32, host: no lower bound in any scenario, sum_a |r_a| < 2^18, n + 2 <
+    // 2^11); SGUFP_SUB_KEY64=1 forces the 64-bit keys (A/B)
+    const char *ek = getenv("SGUFP_SUB_KEY64");
+    const hipError_t e = (N.key32 && !(ek && atoi(ek) == 1)) ? launch_scenarios<int32_t>(N, io, st)
+                                                           : launch_scenarios<int64_t>(N, io, st);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_sub_reduce, dim3((unsigned)io.n_paths), dim3(256), 0, st, N, io);
     return hipGetLastError();
 }
