@@ -824,7 +824,7 @@ __device__ __forceinline__ ChainOut assemble_chain(const SubNet &N, const WS &W,
 
 // ---------------------------------------------------------------------------------------
 template <int RG, typename WT, int NW, typename KT, bool ALLREG>
-__global__ void __launch_bounds__(kWave * NW) k_sub_scenario(SubNet N, SubIO io) {
+__global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : 1) k_sub_scenario(SubNet N, SubIO io) {
     using WS = SubLds<KT, ALLREG>;
     using B = Blk<NW>;
     const int tid = B::tid();
