@@ -76,6 +76,10 @@ def parse():
                          "incumbents / optimality cuts appear (with them most C3 paths are infeasible)")
     ap.add_argument("--round-seconds", type=float, default=5.0,
                     help="B&B: a round's exact-leaf refinement loops are deferred after this many seconds")
+    ap.add_argument("--bnb-heuristic", type=int, default=0,
+                    help="--mode bnb: seed the incumbent with the restricted-DD heuristic of this width (0: none)")
+    ap.add_argument("--bnb-seeded-width", type=int, default=128,
+                    help="B&B leg with the incumbent seeded by the restricted-DD heuristic of this width (0: skip)")
     ap.add_argument("--bnb-leg-seconds", type=float, default=20.0,
                     help="headline line: seconds of the C4 / 256-scenario B&B leg (0: skip)")
     ap.add_argument("--c5-bnb-seconds", type=float, default=30.0,
@@ -184,11 +188,15 @@ def pmc_issue(tag: str, workload: str, kernel: str = "k_relax"):
                                                                  c.get("SQ_INSTS_SALU", 0.0)), 2)}
 
 
-def bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, work, device=0, progress=10.0, tag="bnb"):
+def bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, work, device=0, progress=10.0, tag="bnb",
+            heuristic=0):
     """The device DDSolver (sgufp_bnb_step rounds) from the root record Node{} with no
     incumbent, after a short warm-up search (kernels, allocations; its pool is cleared):
     relaxations = NodeExplorer::process calls, exact-leaf refinement loops with the device
-    subproblem included; a round's loops stop after round_seconds (deferred, resumed later)."""
+    subproblem included; a round's loops stop after round_seconds (deferred, resumed later).
+    heuristic > 0: the incumbent is seeded inside the timed region by the restricted-DD
+    heuristic of that width on the root record (processX3's restricted half, restricted.py),
+    as the reference seeds it with a known value (main.cpp:75), so incumbent pruning acts."""
     from sgufp_solver_amd import instance
     from sgufp_solver_amd.pools import DOUBLE_MIN
     from sgufp_solver_amd.solver import DDSolver
@@ -205,6 +213,7 @@ def bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, work, device=
     solver.eng.set_timing(True)
     solver.time_budget = budget
     solver.round_seconds = round_seconds
+    solver.restricted_width = heuristic
     import torch
     if solver.shard_comm is not None:
         torch.distributed.barrier()
@@ -224,7 +233,8 @@ def bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, work, device=
         elapsed = float(g[:, -1].max()) / 1e6
     out = {
         "workload": f"{cfg_name}: {cfg.n_arcs}-arc layered network, {inst.scenarios} scenarios"
-                    f"{' (lower bounds 0)' if lb_mode == 'zero' else ''}, root record, no incumbent, "
+                    f"{' (lower bounds 0)' if lb_mode == 'zero' else ''}, root record, "
+                    f"{f'incumbent seeded by the width-{heuristic} restricted-DD heuristic' if heuristic else 'no incumbent'}, "
                     f"up to {batch} records per round, refinement loops deferred after {round_seconds} s per round",
         "instance_seed": seed, "total_layers": int(solver.eng.info.total_layers), "n_gpus": world,
         "relaxations_per_s": round(c["relaxed"] / elapsed, 2),
@@ -232,6 +242,7 @@ def bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, work, device=
         "scenario_lps_per_s": round(c["subproblems"] * inst.scenarios / elapsed, 1),
         "cuts_generated": int(c["new_feasibility_cuts"] + c["new_optimality_cuts"]),
         "seconds": round(elapsed, 3), "rounds": solver.rounds, "complete": solver.complete, "incumbent": z,
+        "heuristic_incumbent": solver.heuristic_incumbent,
         "frontier_left": solver.eng.frontier_size(),
         "pool": [solver.eng.cuts_count(1), solver.eng.cuts_count(0)], "counters": c,
     }
@@ -258,6 +269,7 @@ def bnb_main(args):
     heartbeat("bnb", 20.0)
     work = tempfile.mkdtemp(prefix=f"sgufp_bnb_r{rank}_")
     out = bnb_run(args.bnb_config, args.seed, args.bnb_lb, args.bnb_seconds, args.nodes, args.round_seconds, work,
+                  heuristic=args.bnb_heuristic,
                   device=local % max(1, torch.cuda.device_count()))
     line = {"metric": "device B&B: node relaxations/s (NodeExplorer::process incl. exact-leaf subproblems)",
             "value": out["relaxations_per_s"], "unit": "relaxations/s", "n_gpus": world,
@@ -467,6 +479,12 @@ def main():
         # 1k-arc network with its 256 scenarios (lower bounds 0: feasible, optimality cuts)
         line["bnb"] = bnb_run(args.config, args.seed, "zero", args.bnb_leg_seconds, 1024, args.round_seconds, work,
                               device=local, progress=0.0, tag="leg")
+        if args.bnb_seeded_width > 0:
+            # the same search with incumbent pruning acting (BASELINE configs[2]): the incumbent
+            # seeded inside the timed region by the restricted-DD heuristic on the root record
+            line["bnb_seeded"] = bnb_run(args.config, args.seed, "zero", args.bnb_leg_seconds, 1024,
+                                         args.round_seconds, work, device=local, progress=0.0, tag="legs",
+                                         heuristic=args.bnb_seeded_width)
     if rank == 0 and world == 1 and args.config == "C4" and args.c5_nodes > 0:
         line["config5"] = config5_leg(args, work)
     if rank == 0:
