@@ -65,9 +65,9 @@ constexpr int32_t kNoPred = INT32_MAX;
 //   cta: tail:16 | head:16 | reward sum:32          (-1 ends as 0xFFFF)
 //   ctb: max l:16 | min u:16 | flow x:16 | first arc:16
 // Node / arc ids fit 16 bits (Cut.h:342-344 packs them so); the host checks the bounds.
-// ALLREG: every chain group of the launch sits in the registers of the (single-wave) kernel
-// (nct_cap <= 16 x 64): no sweep reads chain records from LDS, predecessors come from the
-// registers too
+// ALLREG: every chain group of the launch sits in registers (single wave: nct_cap <= 16 x 64;
+// eight waves: <= 10 x 8 x 64): no sweep reads chain records from LDS, predecessors come from
+// the registers too
 template <typename KT, bool ALLREG = false>
 struct SubLds {
     using Key = KT;
@@ -355,7 +355,7 @@ __device__ __forceinline__ uint32_t bf_sweep(const SubNet &N, const WS &W, int n
         using B = Blk<NW>;
         const int S = (G + NW - 1) / NW, wv = B::wid();
         if (!forward) {
-            for (int j = S - 1; j >= RG; j--) {
+            for (int j = S - 1; j >= RG && !WS::kAllReg; j--) {
                 const int g = j * NW + wv;
                 if (g < G) {
                     uint64_t ca, cb;
@@ -393,7 +393,7 @@ __device__ __forceinline__ uint32_t bf_sweep(const SubNet &N, const WS &W, int n
                 __syncthreads();
             }
         }
-        for (int j = RG; j < S; j++) {
+        for (int j = RG; j < S && !WS::kAllReg; j++) {
             const int g = j * NW + wv;
             if (g < G) {
                 uint64_t ca, cb;
@@ -518,11 +518,13 @@ __device__ __forceinline__ void ssp_preds(const SubNet &N, const WS &W, int nct,
     Blk<NW>::sync();
 }
 
-// Predecessors (as ssp_preds) from the register groups of one wave (every chain group in
-// registers): the costs are the ones the Bellman-Ford used, no chain record is re-read.
-template <int RG, typename WT, class WS>
+// Predecessors (as ssp_preds) from the register groups (every chain group of the launch in
+// registers; slot j of wave w holds group j * NW + w): the costs are the ones the Bellman-Ford
+// used, no chain record is re-read.
+template <int RG, typename WT, int NW, class WS>
 __device__ __forceinline__ void ssp_preds_regs(const SubNet &N, const WS &W, int nct, int nz, const ChainRegs<RG, WT> &C) {
     using KT = typename WS::Key;
+    using B = Blk<NW>;
     const int n = N.n, m = N.m;
     const int G = (nct + kWave - 1) / kWave;
     auto reg_w = [&](WT w) -> KT { return sizeof(WT) == sizeof(KT) ? (KT)w : (KT)(((int64_t)w << WS::kHop) + 1); };
@@ -533,26 +535,28 @@ __device__ __forceinline__ void ssp_preds_regs(const SubNet &N, const WS &W, int
             __hip_atomic_fetch_min(&W.pred[v], code << 15 | u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
 #pragma unroll
-    for (int g = 0; g < RG; g++) {
+    for (int j = 0; j < RG; j++) {
+        const int g = j * NW + B::wid();
         if (g < G) {
-            const uint32_t th = C.th[g];
-            tight((int)(th & 0xFFFFu), (int)(th >> 16), reg_w(C.wf[g]), 2 * (g * kWave + lane()), (C.fmask >> g) & 1ull);
+            const uint32_t th = C.th[j];
+            tight((int)(th & 0xFFFFu), (int)(th >> 16), reg_w(C.wf[j]), 2 * (g * kWave + lane()), (C.fmask >> j) & 1ull);
         }
     }
 #pragma unroll
-    for (int g = 0; g < RG; g++) {
+    for (int j = 0; j < RG; j++) {
+        const int g = j * NW + B::wid();
         if (g < G) {
-            const uint32_t th = C.th[g];
-            tight((int)(th >> 16), (int)(th & 0xFFFFu), reg_w(C.wb[g]), 2 * (g * kWave + lane()) + 1, (C.bmask >> g) & 1ull);
+            const uint32_t th = C.th[j];
+            tight((int)(th >> 16), (int)(th & 0xFFFFu), reg_w(C.wb[j]), 2 * (g * kWave + lane()) + 1, (C.bmask >> j) & 1ull);
         }
     }
-    for (int i = lane(); i < nz; i += kWave) {
+    for (int i = B::tid(); i < nz; i += B::T) {
         const uint32_t e = (uint32_t)W.zlist[i];
         const int v = (int)(e & 0x1FFFFFFFu);
         if ((e >> 30) & 1u) tight(n, v, (KT)1, 2 * m + 2 * v, true);
         if ((e >> 29) & 1u) tight(v, n + 1, (KT)1, 2 * m + 2 * v + 1, true);
     }
-    wave_lds_sync();
+    B::sync();
 }
 
 // warm: keep the keys (exact or infinite, see invalidate_subtrees) instead of starting from
@@ -588,7 +592,7 @@ __device__ __forceinline__ bool bellman_ford(const SubNet &N, const WS &W, int n
     }
 #endif
     // one wave with every chain group in registers: predecessors from the registers
-    if constexpr (NW == 1 && WS::kAllReg) ssp_preds_regs<RG, WT>(N, W, nct, nz, C);
+    if constexpr (WS::kAllReg) ssp_preds_regs<RG, WT, NW>(N, W, nct, nz, C);
     else ssp_preds<NW>(N, W, nct, nz, M);
     return true;
 }
@@ -1214,8 +1218,12 @@ hipError_t launch_scenarios(const SubNet &N, const SubIO &io, hipStream_t st) {
     const char *ev = getenv("SGUFP_SUB_WAVES");
     if (large && !(ev && atoi(ev) == 1)) {
         lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, kLargeWaves, kb);
-        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsLarge, int32_t, kLargeWaves, KT, false>),
-                           dim3((unsigned)io.n_paths * N.S), dim3(kWave * kLargeWaves), lds, st, N, io);
+        if (io.nct_cap <= kRegGroupsLarge * kLargeWaves * kWave && !N.preds_lds)
+            hipLaunchKernelGGL((k_sub_scenario<kRegGroupsLarge, int32_t, kLargeWaves, KT, true>),
+                               dim3((unsigned)io.n_paths * N.S), dim3(kWave * kLargeWaves), lds, st, N, io);
+        else
+            hipLaunchKernelGGL((k_sub_scenario<kRegGroupsLarge, int32_t, kLargeWaves, KT, false>),
+                               dim3((unsigned)io.n_paths * N.S), dim3(kWave * kLargeWaves), lds, st, N, io);
     } else if (io.nct_cap <= kRegGroupsSmall * kWave && !N.preds_lds) {
         // register groups hold key increments: 64-bit with 64-bit keys, 32-bit with 32-bit keys
         hipLaunchKernelGGL((k_sub_scenario<kRegGroupsSmall, KT, 1, KT, true>), dim3((unsigned)io.n_paths * N.S),
