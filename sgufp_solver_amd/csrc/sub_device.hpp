@@ -19,8 +19,9 @@ struct SubNet {
     int n, m, S, L, n_slots, nz;
     int64_t cost_bound;                  // bound on |residual costs| incl. big-M: 2 M with
                                          // M <= 1 + 2 sum_a |r_a| (max u + 1) (host)
-    int key32;                           // 32-bit Bellman-Ford keys suffice (host): no lower bound
-                                         // in any scenario, sum_a |r_a| < 2^18, n + 2 < 2^11
+    int key32;                           // 32-bit Bellman-Ford keys and 12-byte chain records (host):
+                                         // no lower bound and no negative upper bound in any
+                                         // scenario, sum_a |r_a| < 2^18, n + 2 < 2^11
     int preds_lds;                       // SGUFP_SUB_PREDS_LDS=1: predecessors from the LDS chain
                                          // records, not the register groups (A/B)
     const int32_t SGUFP_GBL *tail;       // [m]

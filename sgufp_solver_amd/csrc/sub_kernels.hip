@@ -34,6 +34,7 @@
 
 #include <climits>
 #include <cstdint>
+#include <type_traits>
 
 #include "sub_device.hpp"
 #define SGUFP_MULTI_WAVE_TU   // k_sub_scenario runs 1 or kLargeWaves (8) waves per workgroup
@@ -77,7 +78,25 @@ struct SubLds {
     LDS int16_t *dec;       // [m] decision at the head (out-arc id, -1 none, -2 head not V-bar);
                             //     phases 1-2 only (union), phase 5 reads dec_of from HBM
     LDS uint64_t *cta;      // [nct_cap] chains, in the topological order of their tails
-    LDS uint64_t *ctb;      // [nct_cap]
+    // ctb: the b words.  16-byte records (L:16 | U:16 | x:16 | first arc:16); with 32-bit keys
+    // (no lower bound anywhere, host) 12-byte records: U:16 | x:16 (L = 0; the first arc is
+    // re-derived from the path where it is needed) -- more scenarios fit the LDS of a CU
+    static constexpr bool kCompact = sizeof(KT) == 4;
+    using CBT = std::conditional_t<kCompact, uint32_t, uint64_t>;
+    LDS CBT *ctb;           // [nct_cap]
+    // read / write a b word in the 16-byte layout
+    __device__ __forceinline__ uint64_t rb(int k) const {
+        if constexpr (kCompact) {
+            const uint32_t v = ctb[k];
+            return (uint64_t)(v & 0xFFFFu) << 16 | (uint64_t)(v >> 16) << 32;
+        } else {
+            return ctb[k];
+        }
+    }
+    __device__ __forceinline__ void wb(int k, uint64_t b) const {
+        if constexpr (kCompact) ctb[k] = (uint32_t)((b >> 16) & 0xFFFFu) | (uint32_t)((b >> 32) & 0xFFFFu) << 16;
+        else ctb[k] = b;
+    }
     LDS int16_t *chosen;    // [m] in-arc that chose this out-arc of a V-bar node (phases 1-2;
                             //     aliases key / pred)
     LDS KT *key;            // [n+2] Bellman-Ford keys (cost << hop bits | hops); then alpha in place
@@ -135,7 +154,7 @@ constexpr int kSubLdsParts = 12;
 __host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int nz, int nw, size_t *off, int kbytes = 8) {
     size_t o = 0;
     off[1] = o; o = a16(o + (size_t)nct_cap * 8);
-    off[2] = o; o = a16(o + (size_t)nct_cap * 8);
+    off[2] = o; o = a16(o + (size_t)nct_cap * (kbytes == 4 ? 4 : 8));   // compact b words with 32-bit keys
     const size_t u0 = o;
     off[3] = o; o = a16(o + (size_t)(n + 2) * kbytes);   // key | chosen
     off[4] = o; o = a16(o + (size_t)(n + 2) * 4);   // pred
@@ -169,7 +188,7 @@ __device__ __forceinline__ uint64_t pack_b(int L, int U, int x, int first) {
 }
 // the flow field of chain k (lane 0 augments)
 template <class WS>
-__device__ __forceinline__ LDS int16_t *ch_xp(const WS &W, int k) { return (LDS int16_t *)&W.ctb[k] + 2; }
+__device__ __forceinline__ LDS int16_t *ch_xp(const WS &W, int k) { return (LDS int16_t *)&W.ctb[k] + (WS::kCompact ? 1 : 2); }
 
 __device__ __forceinline__ bool is_src(const SubNet &N, int v) { return N.in_off[v + 1] == N.in_off[v]; }
 __device__ __forceinline__ bool is_snk(const SubNet &N, int v) { return N.out_off[v + 1] == N.out_off[v]; }
@@ -194,7 +213,7 @@ __device__ __forceinline__ void for_residual(const SubNet &N, const WS &W, int n
     using B = Blk<NW>;
     // contracted arcs: code 2k (forward), 2k+1 (backward)
     for (int k = B::tid(); k < nct; k += B::T) {
-        const uint64_t ca = W.cta[k], cb = W.ctb[k];
+        const uint64_t ca = W.cta[k], cb = W.rb(k);
         const int t = ch_t(ca), h = ch_h(ca);
         if (t < 0 || h < 0) continue;
         const int64_t x = ch_x(cb), L = ch_L(cb), U = ch_U(cb), R = ch_R(ca);
@@ -284,7 +303,7 @@ __device__ __forceinline__ void load_chain_regs(const WS &W, int n, int nct, int
     for (int g = 0; g < RG; g++) {
         const int k = (g * NW + Blk<NW>::wid()) * kWave + lane();
         uint64_t ca = 0, cb = 0;
-        if (k < nct) { ca = W.cta[k]; cb = W.ctb[k]; }
+        if (k < nct) { ca = W.cta[k]; cb = W.rb(k); }
         const ChainArcs<KT> c = chain_arcs<KT>(ca, cb, k < nct, n, mode, M);
         C.th[g] = c.th;
         if constexpr (sizeof(WT) == sizeof(KT)) {   // key increments, formed once
@@ -348,7 +367,7 @@ __device__ __forceinline__ uint32_t bf_sweep(const SubNet &N, const WS &W, int n
         const int k = g * kWave + lane();
         ca = 0;
         cb = 0;
-        if (k < nct) { ca = W.cta[k]; cb = W.ctb[k]; }
+        if (k < nct) { ca = W.cta[k]; cb = W.rb(k); }
     };
     auto reg_w = [&](WT w) -> KT { return sizeof(WT) == sizeof(KT) ? (KT)w : (KT)(((int64_t)w << WS::kHop) + 1); };
     if constexpr (NW > 1) {
@@ -722,9 +741,9 @@ __device__ __forceinline__ int dec_of(const SubNet &N, const SubIO &io, int64_t 
 // in the order of the closed forms below (all integers: any summation order is exact).
 template <class WS>
 __device__ __forceinline__ ChainOut assemble_chain(const SubNet &N, const WS &W, const SubIO &io, int64_t poff, int64_t plen,
-                                   int k, int s, bool ray_mode, int ray_p, int ray_q, bool &ok) {
+                                   int k, int first, int s, bool ray_mode, int ray_p, int ray_q, bool &ok) {
     ChainOut o{0, 0};
-    const uint64_t ca = W.cta[k], cb = W.ctb[k];
+    const uint64_t ca = W.cta[k];
     const int t = ch_t(ca), h = ch_h(ca);
     const size_t so = (size_t)s * N.m;
     auto rew = [&](int a) -> int64_t { return ray_mode ? 0 : (int64_t)N.reward[a]; };
@@ -745,7 +764,6 @@ __device__ __forceinline__ ChainOut assemble_chain(const SubNet &N, const WS &W,
         o.rhs += v;
         add_coef(N, W, N.arc_layer[a], N.head[b], -v);
     };
-    const int first = ch_first(cb);
     // walk 1: length, sum r, first min-u / first max-l arc, sum_{i >= 1} (e_i - r_i)
     int len = 0, bmin = 0, bmax = 0;
     int64_t sumr = 0, dsum = 0, umin = 0, lmax = 0;
@@ -824,11 +842,50 @@ __device__ __forceinline__ ChainOut assemble_chain(const SubNet &N, const WS &W,
     return o;
 }
 
+// The chains in phase 2's numbering with their first arcs, re-derived from the path (after
+// phase 2 the matching arrays are gone): arc a starts a chain iff its tail is not V-bar or no
+// in-arc of the tail decided a; chains are numbered in arc_topo order.  visit(k, a) runs on the
+// lane of each start (the scan itself runs on every lane).
+template <int NW, class WS, class F>
+__device__ __forceinline__ void chain_starts(const SubNet &N, const WS &W, const SubIO &io, int64_t poff, int64_t plen,
+                                             F visit) {
+    using B = Blk<NW>;
+    int nct = 0;
+    for (int base = 0; base < N.m; base += B::T) {
+        const int a = base + B::tid() < N.m ? N.arc_topo[base + B::tid()] : -1;
+        bool st = false;
+        if (a >= 0) {
+            const int q = N.tail[a];
+            st = true;
+            if (N.vbar[q])
+                for (int e = N.in_off[q]; e < N.in_off[q + 1]; e++)
+                    if (dec_of(N, io, poff, plen, N.in_list[e]) == a) { st = false; break; }
+        }
+        const uint32_t incl = wave_scan_incl(st ? 1u : 0u);
+        uint32_t woff = 0, tot;
+        if constexpr (NW == 1) {
+            tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+        } else {
+            if (lane() == kWave - 1) W.red[B::wid()] = (int64_t)incl;
+            __syncthreads();
+            tot = 0;
+            for (int w = 0; w < NW; w++) {
+                const uint32_t c = (uint32_t)W.red[w];
+                woff += w < B::wid() ? c : 0u;
+                tot += c;
+            }
+            __syncthreads();
+        }
+        if (st) visit(nct + (int)(woff + incl) - 1, a);
+        nct += (int)tot;
+    }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
 template <int RG, typename WT, int NW, typename KT, bool ALLREG>
-__global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : 1) k_sub_scenario(SubNet N, SubIO io) {
+__global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : (sizeof(KT) == 4 ? 4 : 1)) k_sub_scenario(SubNet N, SubIO io) {
     using WS = SubLds<KT, ALLREG>;
     using B = Blk<NW>;
     const int tid = B::tid();
@@ -843,7 +900,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : 1) k_sub_scenario(Su
     WS W;
     W.dec = (LDS int16_t *)(smem + off[0]);
     W.cta = (LDS uint64_t *)(smem + off[1]);
-    W.ctb = (LDS uint64_t *)(smem + off[2]);
+    W.ctb = (LDS typename WS::CBT *)(smem + off[2]);
     W.chosen = (LDS int16_t *)(smem + off[3]);
     W.key = (LDS KT *)(smem + off[3]);
     W.alpha = W.key;
@@ -911,7 +968,10 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : 1) k_sub_scenario(Su
             __syncthreads();
         }
         const int pos = nct + (int)(woff + incl) - 1;
-        if (st && pos < io.nct_cap) W.ctb[pos] = pack_b(0, 0, 0, a);
+        if (st && pos < io.nct_cap) {   // the first arc, until the record is assembled below
+            if constexpr (WS::kCompact) W.cta[pos] = (uint64_t)(uint32_t)a;
+            else W.ctb[pos] = pack_b(0, 0, 0, a);
+        }
         nct += (int)tot;
     }
     if (nct > io.nct_cap) {   // more chains than the host counted: not a valid path
@@ -924,7 +984,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : 1) k_sub_scenario(Su
     for (int i = tid; i < nz; i += T) W.zlist[i] = N.zlist[i];
     int first_bad = INT_MAX;   // first chain (rank) that makes the scenario infeasible up front
     for (int k = tid; k < nct; k += T) {
-        int a = ch_first(W.ctb[k]);
+        int a = WS::kCompact ? (int)(uint32_t)W.cta[k] : ch_first(W.rb(k));
         const int first = a;
         const int t0 = N.tail[a];
         int L = N.lb[so + a], U = N.ub[so + a], R = N.reward[a];
@@ -942,7 +1002,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : 1) k_sub_scenario(Su
         }
         const int t = N.vbar[t0] ? -1 : t0;
         W.cta[k] = pack_a(t, h, R);
-        W.ctb[k] = pack_b(L, U, 0, first);
+        W.wb(k, pack_b(L, U, 0, first));   // compact: L = 0 (host), no first arc
         const bool complete = t >= 0 && h >= 0;
         if ((complete && L > U) || (!complete && L > 0)) first_bad = min(first_bad, k);
     }
@@ -963,7 +1023,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : 1) k_sub_scenario(Su
     for (int k = tid; k < nct; k += T) {
         const uint64_t ca = W.cta[k];
         if (ch_t(ca) >= 0 && ch_h(ca) >= 0) {
-            const int64_t R = ch_R(ca), U = ch_U(W.ctb[k]);
+            const int64_t R = ch_R(ca), U = ch_U(W.rb(k));
             M += 2 * (R < 0 ? -R : R) * (U + 1);
             max_aug += U > 0 ? U : 0;
         }
@@ -977,12 +1037,16 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : 1) k_sub_scenario(Su
     int err_site = 0;   // which check failed (an error scenario reports it as its dual: diagnostics)
     int64_t primal = 0;
 
-    if (first_bad != INT_MAX) {
+    if (WS::kCompact && first_bad != INT_MAX) {
+        // compact records come with no lower bound and ub >= 0 (host): cannot happen
+        status = kSubError;
+        err_site = 8;
+    } else if (first_bad != INT_MAX) {
         // (i) a chain fixed at 0 with a positive lower bound, or (ii) a chain with max l > min u
         status = kSubInfeasible;
         ray_chain = first_bad;
         const int k = first_bad;
-        int a = ch_first(W.ctb[k]);
+        int a = ch_first(W.rb(k));
         const bool complete = ch_t(W.cta[k]) >= 0 && ch_h(W.cta[k]) >= 0;
         int bp = a, bq = a;
         int64_t bl = N.lb[so + a], bu = N.ub[so + a];
@@ -1047,7 +1111,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : 1) k_sub_scenario(Su
             for (int i = tid; i < plen; i += T) {
                 const int code = W.plist[i];
                 if (code >= 2 * m) continue;   // Z arcs: uncapacitated
-                const uint64_t cb = W.ctb[code >> 1];
+                const uint64_t cb = W.rb(code >> 1);
                 const int64_t x = ch_x(cb), L = ch_L(cb), U = ch_U(cb);
                 const int64_t cap = (code & 1) ? (x > L ? x - L : x) : (x < L ? L - x : U - x);
                 delta = cap < delta ? cap : delta;
@@ -1058,7 +1122,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : 1) k_sub_scenario(Su
                 const int code = W.plist[i];
                 if (code >= 2 * m) continue;
                 const int k = code >> 1;
-                const uint64_t ca = W.cta[k], cb = W.ctb[k];
+                const uint64_t ca = W.cta[k], cb = W.rb(k);
                 const int64_t x = ch_x(cb), L = ch_L(cb), U = ch_U(cb);
                 const int64_t cap = (code & 1) ? (x > L ? x - L : x) : (x < L ? L - x : U - x);
                 *ch_xp(W, k) += (int16_t)((code & 1) ? -delta : delta);
@@ -1083,7 +1147,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : 1) k_sub_scenario(Su
         // lower bounds met?
         int unmet = 0;
         for (int k = tid; k < nct; k += T) {
-            const uint64_t ca = W.cta[k], cb = W.ctb[k];
+            const uint64_t ca = W.cta[k], cb = W.rb(k);
             if (ch_t(ca) >= 0 && ch_h(ca) >= 0) {
                 if (ch_x(cb) < ch_L(cb)) unmet = 1;
                 primal += (int64_t)ch_R(ca) * ch_x(cb);
@@ -1118,13 +1182,14 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : 1) k_sub_scenario(Su
     bool ok = true;
     if (status != kSubError) {
         const bool ray = status == kSubInfeasible;
-        for (int k = tid; k < nct; k += T) {
-            if (ray && ray_chain >= 0 && k != ray_chain) continue;   // (i)/(ii): only the bad chain
-            ChainOut c = assemble_chain(N, W, io, poff, plen, k, s, ray, (k == ray_chain) ? ray_p : -1,
+        // chains with their first arcs, in the numbering of phase 2 (re-derived from the path)
+        chain_starts<NW>(N, W, io, poff, plen, [&](int k, int a) {
+            if (k >= nct || (ray && ray_chain >= 0 && k != ray_chain)) return;   // (i)/(ii): only the bad chain
+            ChainOut c = assemble_chain(N, W, io, poff, plen, k, a, s, ray, (k == ray_chain) ? ray_p : -1,
                                         (k == ray_chain) ? ray_q : -1, ok);
             rhs += c.rhs;
             dual += c.obj;
-        }
+        });
         rhs = B::all(rhs, [](int64_t x, int64_t y) { return x + y; }, W.red);
         dual = B::all(dual, [](int64_t x, int64_t y) { return x + y; }, W.red);
         ok = B::any(ok ? 0u : 1u, W.red) == 0;
