@@ -95,6 +95,35 @@ def lib_sha256() -> str:
         return hashlib.sha256(fh.read()).hexdigest()
 
 
+# the sources of k_relax (its HBM traffic depends on them, not on the bits of one build)
+KERNEL_SOURCES = ("dd_kernels.hip", "dd_device.hpp", "wave.hpp")
+
+
+def kernel_src_sha256() -> str:
+    """sha256 over k_relax's sources and the hipcc flags (tools/kernel_src_sha256.py writes the
+    same value next to the PMC CSVs)."""
+    import hashlib
+    sys.path.insert(0, ROOT)
+    from sgufp_solver_amd.build import COMMON
+    h = hashlib.sha256(" ".join(f for f in COMMON if not f.startswith("-I")).encode())
+    for name in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, "sgufp_solver_amd", "csrc", name), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def profile_matches(d: str):
+    """'library' / 'sources' when the PMC profile directory d was collected with this very
+    libsgufp_hip.so / with k_relax built from these very sources, else None."""
+    for fname, want, what in (("lib.sha256", lib_sha256, "library"), ("src.sha256", kernel_src_sha256, "sources")):
+        path = os.path.join(d, fname)
+        if os.path.exists(path):
+            with open(path) as fh:
+                if fh.read().strip() == want():
+                    return what
+    return None
+
+
 # FETCH_SIZE correction on gfx950, measured by tools/calib (profiles/r02_fetch_calibration.json):
 # a coalesced 1 GiB stream of 4-, 8- or 16-byte loads per lane reports exactly 0.5 GiB of
 # FETCH_SIZE, and WRITE_SIZE reports stores of every width at 1.00 (1-byte stores 1.01).
@@ -112,14 +141,11 @@ def pmc_traffic(tag: str, workload: str, kernel: str = "k_relax"):
     only when they were collected with this very library (lib.sha256 next to the CSVs) on
     this very workload (workload.txt); otherwise (None, reason).  FETCH_SIZE x FETCH_CORRECTION + WRITE_SIZE; both count the
     L2's fabric-side requests (Infinity-Cache hits included), so this is L2-miss traffic."""
-    want = lib_sha256()
+    match = None
     for sub in ("pmc_fetch", "pmc_write"):
-        shafile = os.path.join(ROOT, "profiles", f"{tag}_{sub}", "lib.sha256")
-        if not os.path.exists(shafile):
-            return None, f"profiles/{tag}_{sub}/lib.sha256 missing"
-        with open(shafile) as fh:
-            if fh.read().strip() != want:
-                return None, f"profiles/{tag}_{sub} was collected with another build of libsgufp_hip.so"
+        match = profile_matches(os.path.join(ROOT, "profiles", f"{tag}_{sub}"))
+        if match is None:
+            return None, f"profiles/{tag}_{sub} was collected with another k_relax (library and source hashes differ)"
         wfile = os.path.join(ROOT, "profiles", f"{tag}_{sub}", "workload.txt")
         if not os.path.exists(wfile):
             return None, f"profiles/{tag}_{sub}/workload.txt missing"
@@ -143,8 +169,10 @@ def pmc_traffic(tag: str, workload: str, kernel: str = "k_relax"):
     w = load(f"{tag}_pmc_write/*counter_collection.csv", "WRITE_SIZE")
     if not f or not w:
         return None, f"no {kernel} rows in profiles/{tag}_pmc_*"
+    ident = (f"libsgufp_hip.so sha256 {lib_sha256()[:16]}" if match == "library"
+             else f"k_relax sources sha256 {kernel_src_sha256()[:16]}")
     src = (f"profiles/{tag}_pmc_fetch + {tag}_pmc_write (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of "
-           f"bench.py --steps 2, libsgufp_hip.so sha256 {want[:16]}); FETCH_SIZE x {FETCH_CORRECTION}")
+           f"bench.py --steps 2, {ident}); FETCH_SIZE x {FETCH_CORRECTION}")
     return (FETCH_CORRECTION * np.mean(f) + np.mean(w)) * 1024.0, src
 
 
@@ -153,11 +181,9 @@ def pmc_issue(tag: str, workload: str, kernel: str = "k_relax"):
     the HBM passes): per launch the wave-instructions issued and where the waves' cycles went.
     SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_ANY count quad-cycles and partition the
     waves' lifetime (MI355X_MICROARCH.md, rocprofv3 PMC slots)."""
-    want = lib_sha256()
     d = os.path.join(ROOT, "profiles", f"{tag}_pmc_issue")
     try:
-        if open(os.path.join(d, "lib.sha256")).read().strip() != want or \
-                open(os.path.join(d, "workload.txt")).read().strip() != workload:
+        if profile_matches(d) is None or open(os.path.join(d, "workload.txt")).read().strip() != workload:
             return None
     except OSError:
         return None

@@ -16,7 +16,8 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_write -o run -- python3 bench.py --steps 2 --warmup 1 $LEGS > gpurun_out/${TAG}_pmc_write.log 2>&1 || { tail gpurun_out/${TAG}_pmc_write.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d gpurun_out/${TAG}_pmc_issue -o run -- python3 bench.py --steps 2 --warmup 1 $LEGS > gpurun_out/${TAG}_pmc_issue.log 2>&1 || { tail gpurun_out/${TAG}_pmc_issue.log; exit 1; }
 sha256sum sgufp_solver_amd/lib/libsgufp_hip.so | cut -d' ' -f1 > gpurun_out/${TAG}_pmc_fetch/lib.sha256
-for d in pmc_write pmc_issue; do cp gpurun_out/${TAG}_pmc_fetch/lib.sha256 gpurun_out/${TAG}_$d/lib.sha256; done
+python3 tools/kernel_src_sha256.py > gpurun_out/${TAG}_pmc_fetch/src.sha256
+for d in pmc_write pmc_issue; do cp gpurun_out/${TAG}_pmc_fetch/lib.sha256 gpurun_out/${TAG}_pmc_fetch/src.sha256 gpurun_out/${TAG}_$d/; done
 for d in pmc_fetch pmc_write pmc_issue; do echo "C4:seed1:nodes8192:pool16F+64O" > gpurun_out/${TAG}_$d/workload.txt; cp -r gpurun_out/${TAG}_$d profiles/; done
 timeout -k 10 900 python3 bench.py --profile-tag ${TAG} > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { tail gpurun_out/bench_${TAG}.err; exit 1; }
 cat gpurun_out/bench_${TAG}.json
