@@ -259,3 +259,35 @@ def test_warm_bellman_ford_matches_cold(cfg, seed, S, n_paths, tmp_path):
         np.testing.assert_array_equal(a[k], b[k])
     for k in ("rhs", "rows", "obj_mean", "obj", "dual"):
         np.testing.assert_array_equal(a[k].view(np.uint64), b[k].view(np.uint64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,seed,S,n_paths", [("C3", 3, 16, 8), ("C5", 3, 2, 4)])
+def test_kernel_variants_agree(cfg, seed, S, n_paths, tmp_path):
+    """Launches without lower bounds run the 32-bit-key kernel with 12-byte chain records and
+    predecessors from the register groups (launch_subproblem).  The same algorithm with 64-bit
+    keys and 16-byte records (SGUFP_SUB_KEY64=1) and with the predecessors from the LDS chain
+    records (SGUFP_SUB_PREDS_LDS=1) must give bit-identical results: same augmenting paths
+    (the smallest tight arc code wins in every width), same duals, same cut rows."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    helper = os.path.join(here, "tests", "helpers", "sub_run.py")
+    res = {}
+    for name, extra in (("default", {}), ("key64", {"SGUFP_SUB_KEY64": "1"}),
+                        ("preds_lds", {"SGUFP_SUB_PREDS_LDS": "1"})):
+        env = dict(os.environ)
+        env.pop("SGUFP_LIB_PATH", None)
+        env.update(extra)
+        out = str(tmp_path / f"{name}.npz")
+        subprocess.run([sys.executable, helper, cfg, str(seed), str(S), str(n_paths), out], env=env,
+                       check=True, timeout=240)
+        res[name] = np.load(out)
+    a = res["default"]
+    assert (a["st"] == 0).all()
+    for name in ("key64", "preds_lds"):
+        b = res[name]
+        for k in ("typ", "st"):
+            np.testing.assert_array_equal(a[k], b[k], err_msg=name)
+        for k in ("rhs", "rows", "obj_mean", "obj", "dual"):
+            np.testing.assert_array_equal(a[k].view(np.uint64), b[k].view(np.uint64), err_msg=f"{name}: {k}")
