@@ -92,8 +92,21 @@ class Container {
 
   public:
     const cut_node_t *get() const { return head.load(std::memory_order_acquire); }
-    void add(cut_node_t *node);
-    ~Container();
+    // Container::add (Cut.h:461-465): push onto the list head with a release CAS; a reader that
+    // acquires the head sees every cut pushed before it, newest first
+    void add(cut_node_t *node) {
+        node->next = head.load(std::memory_order_relaxed);
+        while (!head.compare_exchange_weak(node->next, node, std::memory_order_release, std::memory_order_relaxed)) {
+        }
+    }
+    ~Container() {
+        cut_node_t *cur = head.load(std::memory_order_acquire);
+        while (cur) {
+            cut_node_t *nx = cur->next;
+            delete cur;
+            cur = nx;
+        }
+    }
 };
 
 struct OutObj {

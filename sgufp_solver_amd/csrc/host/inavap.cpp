@@ -34,20 +34,6 @@ double Cut::get(uint64_t key) const {
     return 0.0;
 }
 
-void Container::add(cut_node_t *node) {
-    node->next = head.load(std::memory_order_relaxed);
-    while (!head.compare_exchange_weak(node->next, node, std::memory_order_release, std::memory_order_relaxed)) {
-    }
-}
-
-Container::~Container() {
-    cut_node_t *cur = head.load(std::memory_order_acquire);
-    while (cur) {
-        cut_node_t *nx = cur->next;
-        delete cur;
-        cur = nx;
-    }
-}
 
 // ---- device handle -----------------------------------------------------------------------
 Device::Device(const Network &net, int max_batch) {

@@ -50,3 +50,26 @@ def test_host_api_solves_to_the_extensive_form_optimum(cfg, seed, S, seeding):
     assert "Optimal solution:" in r.stdout
     for k in ("ddsolver", "explorer", "sharded"):
         assert abs(got[k] - opt) <= 1e-5 * max(1.0, abs(opt)), (k, got, opt)
+
+
+def test_container_is_race_free_under_tsan(tmp_path):
+    """SURVEY.md §5 (race detection): Inavap::Container, the lock-free cut pool of the C++ host
+    API (include/sgufp/inavap.hpp; Cut.h:448-485 in the reference), under ThreadSanitizer with
+    concurrent writers and readers walking the list (tests/host/container_tsan.cpp)."""
+    import shutil
+    import subprocess
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("g++ missing")
+    exe = str(tmp_path / "container_tsan")
+    r = subprocess.run([cxx, "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-pthread",
+                        f"-I{os.path.join(here, 'include')}", os.path.join(here, "tests", "host", "container_tsan.cpp"),
+                        "-o", exe], capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.skip("ThreadSanitizer toolchain unavailable: " + r.stderr[-200:])
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:exitcode=66")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=120)
+    assert "ThreadSanitizer" not in r.stderr, r.stderr[-2000:]
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr[-500:])
+    assert "cuts 8000 (expected 8000)" in r.stdout
