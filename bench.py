@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--profile-tag", default="r03")
     ap.add_argument("--sub-paths", type=int, default=32, help="subproblem leg: random full-matching paths (0: skip)")
     ap.add_argument("--cpu-sub-seconds", type=float, default=8.0)
-    ap.add_argument("--c5-nodes", type=int, default=1024,
+    ap.add_argument("--c5-nodes", type=int, default=4096,
                     help="config-5 leg (5k arcs, 512 scenarios): open nodes relaxed per step (0: skip)")
     ap.add_argument("--c5-paths", type=int, default=4, help="config-5 leg: subproblem paths x 512 scenarios")
     ap.add_argument("--mode", choices=["relax", "bnb"], default="relax",
