@@ -76,6 +76,8 @@ def parse():
                          "incumbents / optimality cuts appear (with them most C3 paths are infeasible)")
     ap.add_argument("--round-seconds", type=float, default=5.0,
                     help="B&B: a round's exact-leaf refinement loops are deferred after this many seconds")
+    ap.add_argument("--bnb-streams", type=int, default=1,
+                    help="--mode bnb: frontier shards on the device (one context / stream / host thread each)")
     ap.add_argument("--bnb-heuristic", type=int, default=0,
                     help="--mode bnb: seed the incumbent with the restricted-DD heuristic of this width (0: none)")
     ap.add_argument("--bnb-seeded-width", type=int, default=128,
@@ -215,14 +217,16 @@ def pmc_issue(tag: str, workload: str, kernel: str = "k_relax"):
 
 
 def bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, work, device=0, progress=10.0, tag="bnb",
-            heuristic=0):
+            heuristic=0, streams=1):
     """The device DDSolver (sgufp_bnb_step rounds) from the root record Node{} with no
     incumbent, after a short warm-up search (kernels, allocations; its pool is cleared):
     relaxations = NodeExplorer::process calls, exact-leaf refinement loops with the device
     subproblem included; a round's loops stop after round_seconds (deferred, resumed later).
     heuristic > 0: the incumbent is seeded inside the timed region by the restricted-DD
     heuristic of that width on the root record (processX3's restricted half, restricted.py),
-    as the reference seeds it with a known value (main.cpp:75), so incumbent pruning acts."""
+    as the reference seeds it with a known value (main.cpp:75), so incumbent pruning acts.
+    streams > 1: that many frontier shards on the device, one context (HIP stream, scratch)
+    and one host thread each, exchanging as the multi-rank shards do (shards.LocalComm)."""
     from sgufp_solver_amd import instance
     from sgufp_solver_amd.pools import DOUBLE_MIN
     from sgufp_solver_amd.solver import DDSolver
@@ -232,25 +236,30 @@ def bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, work, device=
         inst.lb[:] = 0
     net = os.path.join(work, f"{tag}_{cfg_name}.txt")
     inst.write(net)
-    solver = DDSolver(net, device=device, max_batch=batch, verbose=False, time_budget=2.0, progress=progress,
-                      round_seconds=min(round_seconds, 2.0))
-    solver.start_solver(DOUBLE_MIN)                        # warm-up
-    solver.eng.clear_cuts()
-    solver.eng.set_timing(True)
-    solver.time_budget = budget
-    solver.round_seconds = round_seconds
-    solver.restricted_width = heuristic
+    from sgufp_solver_amd.shards import LocalComm, LocalGroup, run_local_shards
+    group = LocalGroup(streams) if streams > 1 else None
+    solvers = [DDSolver(net, device=device, max_batch=batch, verbose=False, time_budget=2.0, progress=progress,
+                        round_seconds=min(round_seconds, 2.0), comm=LocalComm(group, k) if group else None)
+               for k in range(streams)]
+    run_local_shards(solvers, lambda s: s.start_solver(DOUBLE_MIN))       # warm-up
+    for s in solvers:
+        s.eng.clear_cuts()
+        s.eng.set_timing(True)
+        s.time_budget = budget
+        s.round_seconds = round_seconds
+        s.restricted_width = heuristic
+    solver = solvers[0]
     import torch
-    if solver.shard_comm is not None:
+    if solver.shard_comm is not None and group is None:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    z = solver.start_solver(DOUBLE_MIN)
+    z = run_local_shards(solvers, lambda s: s.start_solver(DOUBLE_MIN))[0]
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    c = dict(solver.counters)
+    c = {k: sum(int(s.counters[k]) for s in solvers) for k in solver.counters}
     world = 1
-    if solver.shard_comm is not None:
+    if solver.shard_comm is not None and group is None:
         comm = solver.shard_comm
         world = comm.world
         keys = sorted(c)
@@ -261,18 +270,21 @@ def bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, work, device=
         "workload": f"{cfg_name}: {cfg.n_arcs}-arc layered network, {inst.scenarios} scenarios"
                     f"{' (lower bounds 0)' if lb_mode == 'zero' else ''}, root record, "
                     f"{f'incumbent seeded by the width-{heuristic} restricted-DD heuristic' if heuristic else 'no incumbent'}, "
+                    f"{f'{streams} frontier shards on the device (one stream and host thread each), ' if streams > 1 else ''}"
                     f"up to {batch} records per round, refinement loops deferred after {round_seconds} s per round",
         "instance_seed": seed, "total_layers": int(solver.eng.info.total_layers), "n_gpus": world,
         "relaxations_per_s": round(c["relaxed"] / elapsed, 2),
         "subproblems_per_s": round(c["subproblems"] / elapsed, 2),
         "scenario_lps_per_s": round(c["subproblems"] * inst.scenarios / elapsed, 1),
         "cuts_generated": int(c["new_feasibility_cuts"] + c["new_optimality_cuts"]),
-        "seconds": round(elapsed, 3), "rounds": solver.rounds, "complete": solver.complete, "incumbent": z,
+        "seconds": round(elapsed, 3), "rounds": solver.rounds, "complete": all(s.complete for s in solvers),
+        "incumbent": z, "streams": streams,
         "heuristic_incumbent": solver.heuristic_incumbent,
-        "frontier_left": solver.eng.frontier_size(),
+        "frontier_left": sum(s.eng.frontier_size() for s in solvers),
         "pool": [solver.eng.cuts_count(1), solver.eng.cuts_count(0)], "counters": c,
     }
-    solver.eng.close()
+    for s in solvers:
+        s.eng.close()
     return out
 
 
@@ -295,7 +307,7 @@ def bnb_main(args):
     heartbeat("bnb", 20.0)
     work = tempfile.mkdtemp(prefix=f"sgufp_bnb_r{rank}_")
     out = bnb_run(args.bnb_config, args.seed, args.bnb_lb, args.bnb_seconds, args.nodes, args.round_seconds, work,
-                  heuristic=args.bnb_heuristic,
+                  heuristic=args.bnb_heuristic, streams=args.bnb_streams,
                   device=local % max(1, torch.cuda.device_count()))
     line = {"metric": "device B&B: node relaxations/s (NodeExplorer::process incl. exact-leaf subproblems)",
             "value": out["relaxations_per_s"], "unit": "relaxations/s", "n_gpus": world,

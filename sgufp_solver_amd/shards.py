@@ -22,6 +22,7 @@ exchange by a collective on fixed-shape tensors (no pickled objects):
 """
 from __future__ import annotations
 
+import threading
 from typing import List, Sequence
 
 import numpy as np
@@ -190,3 +191,81 @@ class ShardComm:
                 eng.frontier_push(batch_slice(b, np.arange(lo, hi)))
                 got += hi - lo
         return got
+
+
+class LocalGroup:
+    """Shared state of `world` frontier shards that run as threads of one process."""
+
+    def __init__(self, world: int):
+        self.world = world
+        self.barrier = threading.Barrier(world)
+        self.slots = [None] * world
+
+
+class LocalComm(ShardComm):
+    """ShardComm's exchanges between threads of one process: several frontier shards on one
+    GPU, each with its own device context (its own HIP stream and scratch), so that while one
+    shard waits for the slowest record of its relaxation batch the others keep the GPU busy --
+    the reference's several worker threads per node, each with its own NodeExplorer
+    (DDSolver.cpp:684-760).  Same protocol as the multi-rank path: the collectives become a
+    slot write per shard between two barriers."""
+
+    def __init__(self, group: LocalGroup, rank: int):
+        self.torch = None
+        self.dist = None
+        self.group = group
+        self.world = group.world
+        self.rank = rank
+        self.dev = None
+        self.bytes = 0
+
+    def _exchange(self, value):
+        g = self.group
+        g.slots[self.rank] = value
+        g.barrier.wait()
+        out = list(g.slots)
+        g.barrier.wait()
+        return out
+
+    def allreduce_max(self, z: float) -> float:
+        self.bytes += 8
+        return max(self._exchange(float(z)))
+
+    def allgather_i64(self, vals: Sequence[int]) -> np.ndarray:
+        self.bytes += 8 * len(vals)
+        return np.stack([np.asarray(v, dtype=np.int64) for v in self._exchange([int(x) for x in vals])])
+
+    def allgather_rows(self, rows: np.ndarray) -> List[np.ndarray]:
+        rows = np.array(rows, dtype=np.float64, copy=True)
+        self.bytes += rows.nbytes
+        return self._exchange(rows)
+
+    def allgather_bytes(self, blob: np.ndarray) -> List[np.ndarray]:
+        blob = np.array(blob, dtype=np.uint8, copy=True)
+        self.bytes += blob.nbytes
+        return self._exchange(blob)
+
+
+def run_local_shards(solvers, fn):
+    """fn(solver) on every shard in its own thread (the library releases the GIL in its calls);
+    returns the results in shard order, re-raising the first exception."""
+    out = [None] * len(solvers)
+    err = []
+
+    def body(k):
+        try:
+            out[k] = fn(solvers[k])
+        except BaseException as e:   # noqa: BLE001 -- re-raised below
+            err.append(e)
+            for s in solvers:        # unblock the other shards' barriers
+                c = getattr(s, "comm", None)
+                if c is not None and hasattr(c, "group"):
+                    c.group.barrier.abort()
+    threads = [threading.Thread(target=body, args=(k,)) for k in range(len(solvers))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if err:
+        raise err[0]
+    return out

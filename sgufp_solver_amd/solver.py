@@ -42,7 +42,7 @@ class DDSolver:
                  max_batch: int = 4096, batch_nodes: int = 0, engine=None, group=None, verbose: bool = True,
                  progress: float = 0.0, max_rounds: int = 0, dive_batch: int = 64, time_budget: float = 0.0,
                  restricted_width: int = 0, round_seconds: float = 0.0, round_iters: int = 0,
-                 native_world: int = 0):
+                 native_world: int = 0, comm=None):
         """n_workers is accepted for API compatibility with the reference (threads there);
         the parallelism here is the batch of ``batch_nodes`` (<= max_batch) records per
         round and one rank per GPU."""
@@ -74,6 +74,9 @@ class DDSolver:
         # (sgufp_incumbent_allreduce / _cuts_exchange / _frontier_sizes / _frontier_balance,
         # shard.cpp: device buffers, no host staging); 0: torch.distributed (shards.py)
         self.native_world = native_world
+        # an explicit exchange object (shards.LocalComm: several shards as threads of one
+        # process, e.g. on one GPU); None: torch.distributed when initialised with > 1 rank
+        self.comm = comm
         # bound of one round's exact-leaf refinement loops (0: none; see Engine.bnb_set_limits)
         self.round_seconds = round_seconds
         self.round_iters = round_iters
@@ -100,7 +103,7 @@ class DDSolver:
     def start_solver(self, known_optimal: float) -> float:
         """DDSolver::startSolver (DDSolver.cpp:782-846): incumbent := known_optimal, the root
         record Node{} on the frontier (rank 0), rounds until every shard is empty."""
-        comm = None if self.native_world else self._comm()
+        comm = None if self.native_world else (self.comm if self.comm is not None else self._comm())
         self.shard_comm = comm
         rank = comm.rank if comm else 0
         eng = self.eng

@@ -241,3 +241,24 @@ def test_worker_stats_format():
     assert "Cuts (feasibility, optimality): 1 , 5" in lines
     assert "(1, 3, 0)  (0, 0, 2)  " in lines
     assert lines[-3] == "-" * 72 and lines[-2] == "" and lines[-1] == ""   # dash, endl, endl
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_in_process_shards_protocol(world):
+    """Several frontier shards as threads of one process (shards.LocalComm: one device context
+    each, e.g. on one GPU) run the same exchanges: every shard ends with the brute-force
+    optimum and the same global cut pool, every leaf is closed once, and every shard works."""
+    from sgufp_solver_amd.shards import LocalComm, LocalGroup, run_local_shards
+    group = LocalGroup(world)
+    engines = [ToyEngine() for _ in range(world)]
+    solvers = [DDSolver(engine=engines[r], batch_nodes=3, verbose=False, comm=LocalComm(group, r))
+               for r in range(world)]
+    zs = run_local_shards(solvers, lambda s: s.start_solver(-1.0))
+    opt = brute()
+    assert all(z == opt for z in zs), (zs, opt)
+    assert all(sorted(e.cuts[0]) == sorted(engines[0].cuts[0]) and sorted(e.cuts[1]) == sorted(engines[0].cuts[1])
+               for e in engines)
+    leaves = [t for e in engines for t in e.closed]
+    assert len(leaves) == len(set(leaves))
+    assert all(s.counters["relaxed"] > 0 for s in solvers)
+    assert all(s.complete for s in solvers)
