@@ -107,7 +107,6 @@ struct SubLds {
     LDS int32_t *zlist;     // [nz] free-supply / free-demand nodes: v | src << 30 | snk << 29
     LDS int32_t *misc;      // [8] flags
     LDS int64_t *red;       // [8] cross-wave reduction slots (multi-wave workgroups)
-    LDS uint16_t *anc2;     // [n+2] second ancestor buffer of invalidate_subtrees (multi-wave)
 #ifdef SGUFP_SUB_VERIFY
     LDS KT *vkey;           // [n+2] warm Bellman-Ford keys, compared with a cold run
 #endif
@@ -159,7 +158,6 @@ __host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int 
     off[3] = o; o = a16(o + (size_t)(n + 2) * kbytes);   // key | chosen
     off[4] = o; o = a16(o + (size_t)(n + 2) * 4);   // pred
     off[8] = o; o = a16(o + (size_t)(n + 2) * 2);   // plist
-    off[11] = o; o = a16(o + (nw > 1 ? (size_t)(n + 2) * 2 : 0));   // anc2
     off[0] = a16(u0 + (size_t)m * 2);               // dec, after chosen
     if (o < a16(off[0] + (size_t)m * 2)) o = a16(off[0] + (size_t)m * 2);
     off[5] = o;
@@ -625,58 +623,57 @@ __device__ __forceinline__ int64_t key_cost(typename WS::Key k) { return (int64_
 // tree path crosses one of them restarts at infinity, the others keep their keys.  Those are
 // still the shortest: the tree path survives, and SSP keys never decrease -- also in (cost,
 // hops) order, since a new path uses reverse arcs of the augmenting path, which come back
-// at equal cost with more hops.  Pointer jumping over the tree (ancestor in the path list's
-// space, dead = infinite key): a wave reads one group's entries before it writes them, and
-// later groups read after earlier ones wrote, so no lane sees a half-updated pair.
-// With several waves the rounds are double-buffered (every pointer of a round is read from
-// the previous round's buffer); a node killed in the same round as a descendant reads it is
-// caught one round later through the very ancestor that killed it.
+// at equal cost with more hops.  Pointer jumping over the tree: each 16-bit word holds an
+// ancestor anc(v) (15 bits) and a flag D(v) = "some node on the tree path v..anc(v), both
+// ends included, is dead (infinite key)".  A jump combines two words, (anc(a), D(v)|D(a))
+// with a = anc(v), which is again such a pair, so a lane may read any mix of this and the
+// previous round's words (other lanes and waves write concurrently; a 16-bit LDS word is read
+// and written whole): no double buffering, and each lane jumps kInvU nodes at once to overlap
+// their LDS round trips.  Once no pointer moves, every anc(v) is a root and D(v) covers the
+// whole path.
+#ifndef SGUFP_INV_U
+#define SGUFP_INV_U 4
+#endif
+constexpr int kInvU = SGUFP_INV_U;
 template <int NW, class WS>
 __device__ __forceinline__ void invalidate_subtrees(const SubNet &N, const WS &W) {
+    using B = Blk<NW>;
     constexpr auto kKInf = WS::kKInf;
     const int nn = N.n + 2;
-    if constexpr (NW > 1) {
-        using B = Blk<NW>;
-        LDS uint16_t *a_in = W.plist, *a_out = W.anc2;
-        for (int v = B::tid(); v < nn; v += B::T) {
-            const int32_t pr = W.pred[v];
-            a_in[v] = (uint16_t)(pr == kNoPred ? v : (pr & 0x7FFF));
-        }
-        __syncthreads();
-        for (int r = 0; r < 32; r++) {
-            uint32_t moved = 0;
-            for (int v = B::tid(); v < nn; v += B::T) {
-                const int a = a_in[v];
-                const int aa = a_in[a];
-                if (W.key[a] >= kKInf && W.key[v] < kKInf) W.key[v] = kKInf;
-                a_out[v] = (uint16_t)aa;
-                moved |= (aa != a) ? 1u : 0u;
-            }
-            LDS uint16_t *t = a_in;
-            a_in = a_out;
-            a_out = t;
-            if (!B::any(moved, W.red)) break;
-        }
-        return;
-    }
     LDS uint16_t *anc = W.plist;
-    for (int v = lane(); v < nn; v += kWave) {
+    for (int v = B::tid(); v < nn; v += B::T) {
         const int32_t pr = W.pred[v];
-        anc[v] = (uint16_t)(pr == kNoPred ? v : (pr & 0x7FFF));
+        const int a = pr == kNoPred ? v : (pr & 0x7FFF);
+        const bool dead = W.key[v] >= kKInf || W.key[a] >= kKInf;
+        anc[v] = (uint16_t)(a | (dead ? 0x8000 : 0));
     }
-    wave_lds_sync();
+    B::sync();
     for (int r = 0; r < 32; r++) {
         uint32_t moved = 0;
-        for (int v = lane(); v < nn; v += kWave) {
-            const int a = anc[v];
-            const int aa = anc[a];
-            const bool dead_a = W.key[a] >= kKInf, dead_v = W.key[v] >= kKInf;
-            if (dead_a && !dead_v) W.key[v] = kKInf;
-            if (aa != a) { anc[v] = (uint16_t)aa; moved = 1; }
+        for (int base = B::tid(); base < nn; base += kInvU * B::T) {
+            uint32_t w[kInvU], wa[kInvU];
+#pragma unroll
+            for (int k = 0; k < kInvU; k++) {
+                const int v = base + k * B::T;
+                w[k] = v < nn ? (uint32_t)anc[v] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < kInvU; k++) wa[k] = anc[w[k] & 0x7FFFu];
+#pragma unroll
+            for (int k = 0; k < kInvU; k++) {
+                const int v = base + k * B::T;
+                if (v < nn && (wa[k] & 0x7FFFu) != (w[k] & 0x7FFFu)) {
+                    anc[v] = (uint16_t)((wa[k] & 0x7FFFu) | ((w[k] | wa[k]) & 0x8000u));
+                    moved = 1;
+                }
+            }
         }
-        wave_lds_sync();
-        if (!wave_or(moved)) break;
+        B::sync();
+        if (!B::any(moved, W.red)) break;
     }
+    for (int v = B::tid(); v < nn; v += B::T)
+        if (anc[v] & 0x8000u) W.key[v] = kKInf;
+    B::sync();
 }
 
 // ---------------------------------------------------------------------------------------
@@ -910,7 +907,6 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : (sizeof(KT) == 4 ? 4
     W.zlist = (LDS int32_t *)(smem + off[6]);
     W.misc = (LDS int32_t *)(smem + off[7]);
     W.red = (LDS int64_t *)(smem + off[10]);
-    W.anc2 = (LDS uint16_t *)(smem + off[11]);
 #ifdef SGUFP_SUB_VERIFY
     W.vkey = (LDS KT *)(smem + off[9]);
 #endif
