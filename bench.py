@@ -87,6 +87,8 @@ def parse():
     ap.add_argument("--c5-bnb-seconds", type=float, default=30.0,
                     help="config-5 leg: seconds of the C5 / 512-scenario B&B with cut generation (0: skip)")
     ap.add_argument("--no-parity", action="store_true", help="skip the reference parity check of the timed batch")
+    ap.add_argument("--bnb-parity-rounds", type=int, default=6,
+                    help="rounds of the seeded device B&B checked against the reference under its own cuts (0: skip)")
     return ap.parse_args()
 
 
@@ -216,8 +218,22 @@ def pmc_issue(tag: str, workload: str, kernel: str = "k_relax"):
                                                                  c.get("SQ_INSTS_SALU", 0.0)), 2)}
 
 
+def _native_comm(eng, world, rank):
+    """The library's own RCCL communicator (shard.cpp) on this rank's context: the id made on
+    rank 0 reaches the others through a gloo side group (plain bytes)."""
+    import torch
+    import torch.distributed as dist
+    from sgufp_solver_amd import engine as E
+    side = dist.new_group(backend="gloo")
+    uid = torch.zeros(128, dtype=torch.uint8)
+    if rank == 0:
+        uid[:] = torch.frombuffer(bytearray(E.comm_unique_id()), dtype=torch.uint8)
+    dist.broadcast(uid, src=0, group=side)
+    eng.comm_init(world, rank, bytes(uid.numpy()))
+
+
 def bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, work, device=0, progress=10.0, tag="bnb",
-            heuristic=0, streams=1):
+            heuristic=0, streams=1, native=False):
     """The device DDSolver (sgufp_bnb_step rounds) from the root record Node{} with no
     incumbent, after a short warm-up search (kernels, allocations; its pool is cleared):
     relaxations = NodeExplorer::process calls, exact-leaf refinement loops with the device
@@ -226,7 +242,11 @@ def bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, work, device=
     heuristic of that width on the root record (processX3's restricted half, restricted.py),
     as the reference seeds it with a known value (main.cpp:75), so incumbent pruning acts.
     streams > 1: that many frontier shards on the device, one context (HIP stream, scratch)
-    and one host thread each, exchanging as the multi-rank shards do (shards.LocalComm)."""
+    and one host thread each, exchanging as the multi-rank shards do (shards.LocalComm).
+    With torch.distributed initialised (N ranks, one GPU each) the search is shared by the N
+    shards (strong scaling): native=True runs the round exchanges through the library's own
+    RCCL communicator (shard.cpp: incumbent all-reduce, cut-row all-gather, frontier sizes,
+    ncclSend / ncclRecv work sharing), else through shards.py over the torch group."""
     from sgufp_solver_amd import instance
     from sgufp_solver_amd.pools import DOUBLE_MIN
     from sgufp_solver_amd.solver import DDSolver
@@ -237,10 +257,17 @@ def bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, work, device=
     net = os.path.join(work, f"{tag}_{cfg_name}.txt")
     inst.write(net)
     from sgufp_solver_amd.shards import LocalComm, LocalGroup, run_local_shards
+    import torch
+    dist_world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
+    dist_rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
+    native = native and dist_world > 1
     group = LocalGroup(streams) if streams > 1 else None
     solvers = [DDSolver(net, device=device, max_batch=batch, verbose=False, time_budget=2.0, progress=progress,
-                        round_seconds=min(round_seconds, 2.0), comm=LocalComm(group, k) if group else None)
+                        round_seconds=min(round_seconds, 2.0), comm=LocalComm(group, k) if group else None,
+                        native_world=dist_world if native else 0)
                for k in range(streams)]
+    if native:
+        _native_comm(solvers[0].eng, dist_world, dist_rank)
     run_local_shards(solvers, lambda s: s.start_solver(DOUBLE_MIN))       # warm-up
     for s in solvers:
         s.eng.clear_cuts()
@@ -249,8 +276,10 @@ def bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, work, device=
         s.round_seconds = round_seconds
         s.restricted_width = heuristic
     solver = solvers[0]
-    import torch
-    if solver.shard_comm is not None and group is None:
+    if native:
+        solver.eng.cuts_exchange()      # the warm-up's marks: nothing left to send
+        solver.eng.incumbent_allreduce(0.0)   # a collective as a barrier on the library's stream
+    elif solver.shard_comm is not None and group is None:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -259,13 +288,24 @@ def bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, work, device=
     elapsed = time.perf_counter() - t0
     c = {k: sum(int(s.counters[k]) for s in solvers) for k in solver.counters}
     world = 1
-    if solver.shard_comm is not None and group is None:
+    keys = sorted(c)
+    if native:
+        world = dist_world
+        vals = [int(c[k]) for k in keys] + [int(elapsed * 1e6), int(solver.received)]
+        cols = [solver.eng.comm_allgather_i64(vals[i:i + 4], world) for i in range(0, len(vals), 4)]
+        g = np.concatenate(cols, axis=1)
+        c = {k: int(v) for k, v in zip(keys, g[:, :len(keys)].sum(axis=0))}
+        elapsed = float(g[:, len(keys)].max()) / 1e6
+        received = [int(x) for x in g[:, len(keys) + 1]]
+    elif solver.shard_comm is not None and group is None:
         comm = solver.shard_comm
         world = comm.world
-        keys = sorted(c)
-        g = comm.allgather_i64([int(c[k]) for k in keys] + [int(elapsed * 1e6)])
-        c = {k: int(v) for k, v in zip(keys, g[:, :-1].sum(axis=0))}
-        elapsed = float(g[:, -1].max()) / 1e6
+        g = comm.allgather_i64([int(c[k]) for k in keys] + [int(elapsed * 1e6), int(solver.received)])
+        c = {k: int(v) for k, v in zip(keys, g[:, :len(keys)].sum(axis=0))}
+        elapsed = float(g[:, len(keys)].max()) / 1e6
+        received = [int(x) for x in g[:, len(keys) + 1]]
+    else:
+        received = [int(s.received) for s in solvers]
     out = {
         "workload": f"{cfg_name}: {cfg.n_arcs}-arc layered network, {inst.scenarios} scenarios"
                     f"{' (lower bounds 0)' if lb_mode == 'zero' else ''}, root record, "
@@ -283,6 +323,10 @@ def bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, work, device=
         "frontier_left": sum(s.eng.frontier_size() for s in solvers),
         "pool": [solver.eng.cuts_count(1), solver.eng.cuts_count(0)], "counters": c,
     }
+    if world > 1:
+        out["exchange"] = ("library RCCL communicator (shard.cpp: ncclAllReduce / ncclAllGather / ncclSend+Recv)"
+                           if native else f"shards.py over torch.distributed ({torch.distributed.get_backend()})")
+        out["records_received_per_rank"] = received
     for s in solvers:
         s.eng.close()
     return out
@@ -523,12 +567,64 @@ def main():
             line["bnb_seeded"] = bnb_run(args.config, args.seed, "zero", args.bnb_leg_seconds, 1024,
                                          args.round_seconds, work, device=local, progress=0.0, tag="legs",
                                          heuristic=args.bnb_seeded_width)
+    if rank == 0 and world == 1 and args.bnb_parity_rounds > 0:
+        line["bnb_parity"] = bnb_parity_leg(args)
     if rank == 0 and world == 1 and args.config == "C4" and args.c5_nodes > 0:
         line["config5"] = config5_leg(args, work)
+    if world > 1 and args.bnb_leg_seconds > 0:
+        # BASELINE configs[3]: one search shared by the N frontier shards (strong scaling), the
+        # round exchanges over the library's own RCCL communicator -- beside the weak-scaling
+        # relaxation step above.  A watchdog prints the line without this leg should a shard
+        # stall in a collective.
+        stop = watchdog(args.bnb_leg_seconds + 240.0, line, rank)
+        try:
+            line["bnb_multi"] = bnb_run(args.config, args.seed, "zero", args.bnb_leg_seconds, 1024, args.round_seconds,
+                                        work, device=local % max(1, torch.cuda.device_count()), progress=0.0,
+                                        tag="multi", heuristic=args.bnb_seeded_width,
+                                        native=dist_backend(torch) == "nccl")
+        except Exception as e:     # noqa: BLE001 -- reported in the line, the headline stands
+            line["bnb_multi"] = {"error": f"{type(e).__name__}: {e}"}
+        stop.set()
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def watchdog(seconds, line, rank):
+    """After `seconds` without stop.set(): rank 0 prints the line built so far (the leg marked
+    as timed out) and every rank exits (a shard stuck in a collective cannot be unwound)."""
+    import threading
+    stop = threading.Event()
+
+    def run():
+        if not stop.wait(seconds):
+            if rank == 0:
+                line["bnb_multi"] = {"error": f"timed out after {seconds:.0f} s"}
+                print(json.dumps(line), flush=True)
+            sys.stdout.flush()
+            os._exit(0)
+
+    threading.Thread(target=run, daemon=True).start()
+    return stop
+
+
+def bnb_parity_leg(args):
+    """The device B&B under the cuts its own subproblem makes, checked round by round against
+    the reference (oracle/bnb_parity.check_search: the popped records vs ref_dd relaxp bit for
+    bit, bound pruning, cut tightness, closed-loop bounds vs the matchings' expected values and
+    HiGHS, one refinement loop vs ref_dd refine) on the bench network, seeded."""
+    from oracle import bnb_parity as bp
+    if not os.path.exists(bp.REF_BIN):
+        return None
+    rep = bp.check_search(args.config, args.seed, args.bnb_seeded_width, rounds=args.bnb_parity_rounds, batch=64,
+                          sample=24)
+    fails = rep.pop("failures")
+    rep["bit_exact"] = not fails and rep["mismatches"] == 0
+    rep["first_failures"] = fails[:5]
+    rep["against"] = ("oracle/_ref/ref_dd (the reference's RelaxedDDNew) relaxp / refine on the pools and "
+                      "frontiers of the running device search")
+    return rep
 
 
 def config5_leg(args, work):
@@ -705,7 +801,13 @@ def cpu_baseline(work, net, pool, batch, incumbent, args, gpu_sample=None):
     cuts = os.path.join(work, "cuts.txt")
     pools.write_nodes(nodes, E.batch_to_records(sample))
     pools.write_pool(cuts, pool)
-    threads = max(1, min(16, os.cpu_count() or 1))
+    # every host core (std::thread::hardware_concurrency()); the round-3 figure on
+    # 16 threads is reported beside it
+    threads = max(1, os.cpu_count() or 1)
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = threads
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as fh:
@@ -720,9 +822,16 @@ def cpu_baseline(work, net, pool, batch, incumbent, args, gpu_sample=None):
         if r.returncode == 0:
             out = json.loads(r.stdout.strip().splitlines()[-1])
             cb = {"value": round(out["relaxations"] / out["seconds"], 2), "unit": "relaxations/s", "cores": threads,
-                  "kind": "reference", "cpu": cpu_model,
+                  "kind": "reference", "cpu": cpu_model, "cpus_allowed": allowed,
                   "sample": f"the first {sample.n} open nodes of the timed frontier, same pool and incumbent, "
-                            f"{out['seconds']:.1f} s on {threads} threads"}
+                            f"{out['seconds']:.1f} s on {threads} threads (os.cpu_count())"}
+            if threads != 16:
+                r16 = subprocess.run([ref, "relaxp", net, cuts, nodes, incumbent.hex(), "16",
+                                      os.path.join(work, "ref_results16.txt")], capture_output=True, text=True,
+                                     timeout=600)
+                if r16.returncode == 0:
+                    o16 = json.loads(r16.stdout.strip().splitlines()[-1])
+                    cb["value_16_threads"] = round(o16["relaxations"] / o16["seconds"], 2)
             parity = None
             if gpu_sample is not None and not args.no_parity:
                 want = pools.read_results(out_path)

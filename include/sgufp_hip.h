@@ -198,6 +198,10 @@ int sgufp_frontier_push(sgufp_ctx *ctx, int n, const uint16_t *gl, const double 
 int sgufp_frontier_take_size(sgufp_ctx *ctx, int n, int from_bottom, int64_t *n_states, int64_t *n_sol);
 int sgufp_frontier_take(sgufp_ctx *ctx, int n, int from_bottom, uint16_t *gl, double *lb, double *ub,
                         int64_t *states_off, int16_t *states, int64_t *sol_off, int16_t *sol);
+/* Copy the n records at stack positions [first, first + n) (0 = bottom) without removing them. */
+int sgufp_frontier_peek_size(sgufp_ctx *ctx, int64_t first, int n, int64_t *n_states, int64_t *n_sol);
+int sgufp_frontier_peek(sgufp_ctx *ctx, int64_t first, int n, uint16_t *gl, double *lb, double *ub,
+                        int64_t *states_off, int16_t *states, int64_t *sol_off, int16_t *sol);
 int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_stats *stats);
 /* Bound the exact-leaf refinement loops of one sgufp_bnb_step: at most max_refine_iters
  * iterations (subproblem batches) and round_seconds of wall time (0: no limit).  Records
@@ -205,6 +209,21 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
  * again they rebuild, apply the pool (their own new cuts included) and resume the loop with
  * the paths it had seen (kept by the context until then; sgufp_frontier_clear drops them). */
 int sgufp_bnb_set_limits(sgufp_ctx *ctx, int max_refine_iters, double round_seconds);
+/* Round trace for tests and diagnostics (off by default).  With it on, every sgufp_bnb_step
+ * keeps what its round did, readable until the next step:
+ *   kind 0  popped records: record = index in the popped batch (0 = the deepest of the top b
+ *           stack entries), code = node status after the relaxation (SGUFP_PRUNED_BY_BOUND for
+ *           ub <= zOpt, DDSolver.cpp:707-711), value = the record's ub as popped, no path;
+ *   kind 1  scenario subproblems of the refinement loops, in the order they were solved
+ *           (NodeExplorer.cpp:957-969): record, code = cut type (0 optimality, 1 feasibility),
+ *           row = index of the appended cut in that list (sgufp_cuts_rows), value = sum_s obj_s / S,
+ *           path = the argmax path sent to the subproblem;
+ *   kind 2  closed loops (the argmax path repeated, {ub, ub}, NodeExplorer.cpp:948-956): record,
+ *           value = ub (the incumbent candidate), path = the repeated path.
+ * Any output pointer may be NULL; path_off has count + 1 entries. */
+int sgufp_bnb_set_trace(sgufp_ctx *ctx, int enabled);
+int sgufp_bnb_trace(sgufp_ctx *ctx, int kind, int64_t *count, int64_t *path_entries, int32_t *record, int32_t *code,
+                    int32_t *row, double *value, int64_t *path_off, int16_t *paths);
 /* Read back pool cuts [first, first + count) of one list (insertion order) as dense rows,
  * e.g. to all-gather the cuts a round produced to the other frontier shards. */
 int sgufp_cuts_rows(sgufp_ctx *ctx, int is_feasibility, int first, int count, double *rhs, double *rows);
@@ -234,6 +253,16 @@ int sgufp_frontier_sizes(sgufp_ctx *ctx, int64_t *sizes);
  * of >= 32, lf_queue::m_pop; half of fewer, the master's hand-out) and the idle shards
  * split each donor's records in contiguous chunks.  *received = records this shard got. */
 int sgufp_frontier_balance(sgufp_ctx *ctx, int64_t *received);
+/* The plan sgufp_frontier_balance follows, host only (no device is touched): from every
+ * shard's stack size, give[r] = records shard r gives (0 when no shard is idle), idle[0..ni)
+ * = the idle shards in rank order, and idle shard j gets records [chunk_lo[r * world + j],
+ * chunk_hi[r * world + j]) of donor r's bottom records (chunk arrays [world * world], may be
+ * NULL).  Returns ni (< 0: bad arguments). */
+int sgufp_balance_plan(int world, const int64_t *sizes, int64_t *give, int32_t *idle, int64_t *chunk_lo,
+                       int64_t *chunk_hi);
+/* all[world * k] := every shard's k (<= 4) int64 values (e.g. the per-shard counters that a
+ * sharded DDSolver prints on rank 0). */
+int sgufp_comm_allgather_i64(sgufp_ctx *ctx, const int64_t *mine, int k, int64_t *all);
 
 /* -- restricted decision diagram (replaces Inavap::RestrictedDDNew, DD.h:653-730 /
  *    DD.cpp:3090-3505, driven as in NodeExplorer::processX3, NodeExplorer.cpp:605-656) --

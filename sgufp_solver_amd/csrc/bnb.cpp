@@ -178,6 +178,34 @@ static double seconds_since(std::chrono::steady_clock::time_point t0) {
 
 extern "C" {
 
+int sgufp_bnb_set_trace(sgufp_ctx *ctx, int enabled) {
+    if (!ctx) return SGUFP_ERR_ARG;
+    ctx->trace = enabled != 0;
+    for (auto &t : ctx->trace_items) t.clear();
+    return SGUFP_OK;
+}
+
+int sgufp_bnb_trace(sgufp_ctx *ctx, int kind, int64_t *count, int64_t *path_entries, int32_t *record, int32_t *code,
+                    int32_t *row, double *value, int64_t *path_off, int16_t *paths) {
+    if (!ctx || kind < 0 || kind > 2) return SGUFP_ERR_ARG;
+    const auto &items = ctx->trace_items[kind];
+    int64_t pe = 0;
+    for (size_t i = 0; i < items.size(); i++) {
+        if (record) record[i] = items[i].record;
+        if (code) code[i] = items[i].code;
+        if (row) row[i] = items[i].row;
+        if (value) value[i] = items[i].value;
+        if (path_off) path_off[i] = pe;
+        if (paths && !items[i].path.empty())
+            std::memcpy(paths + pe, items[i].path.data(), items[i].path.size() * sizeof(int16_t));
+        pe += (int64_t)items[i].path.size();
+    }
+    if (path_off) path_off[items.size()] = pe;
+    if (count) *count = (int64_t)items.size();
+    if (path_entries) *path_entries = pe;
+    return SGUFP_OK;
+}
+
 int sgufp_bnb_set_limits(sgufp_ctx *ctx, int max_refine_iters, double round_seconds) {
     if (!ctx || max_refine_iters < 0 || !(round_seconds >= 0.0)) return SGUFP_ERR_ARG;
     ctx->bnb_max_iters = max_refine_iters;
@@ -192,16 +220,25 @@ void sgufp_ctx::make_record_key(uint16_t gl, uint32_t mask, const int16_t *sol, 
     if (len) std::memcpy(&key[6], sol, 2 * len);
 }
 
-bool sgufp_ctx::record_key(int64_t e, std::string &key) {
-    uint16_t gl = 0, len = 0;
-    uint32_t mask = 0;
-    int64_t so = 0;
-    if (!download(&gl, fr.gl + e, 1) || !download(&mask, fr.mask + e, 1) || !download(&len, fr.sol_len + e, 1) ||
-        !download(&so, fr.sol_off + e, 1) || !sync())
+bool sgufp_ctx::slice_keys(int64_t lo, int count, std::vector<std::string> &keys) {
+    keys.assign((size_t)count, std::string());
+    if (count <= 0) return true;
+    std::vector<uint16_t> gl(count), len(count);
+    std::vector<uint32_t> mask(count);
+    std::vector<int64_t> so(count);
+    if (!download(gl.data(), fr.gl + lo, count) || !download(mask.data(), fr.mask + lo, count) ||
+        !download(len.data(), fr.sol_len + lo, count) || !download(so.data(), fr.sol_off + lo, count) || !sync())
         return false;
-    std::vector<int16_t> sol(len);
-    if (len && (!download(sol.data(), fr.sol + so, len) || !sync())) return false;
-    make_record_key(gl, mask, sol.data(), len, key);
+    // solution offsets grow with the entry index: one span covers the slice
+    int64_t s_lo = so[0], s_hi = so[0];
+    for (int k = 0; k < count; k++) {
+        s_lo = std::min(s_lo, so[k]);
+        s_hi = std::max(s_hi, so[k] + (int64_t)len[k]);
+    }
+    std::vector<int16_t> arena((size_t)(s_hi - s_lo));
+    if (!arena.empty() && (!download(arena.data(), fr.sol + s_lo, arena.size()) || !sync())) return false;
+    for (int k = 0; k < count; k++)
+        make_record_key(gl[k], mask[k], arena.data() + (so[k] - s_lo), len[k], keys[k]);
     return true;
 }
 
@@ -241,9 +278,45 @@ int sgufp_frontier_push(sgufp_ctx *ctx, int n, const uint16_t *gl, const double 
     return SGUFP_OK;
 }
 
-int sgufp_frontier_take_size(sgufp_ctx *ctx, int n, int from_bottom, int64_t *n_states, int64_t *n_sol) {
-    if (!ctx || n < 0 || n > ctx->fr_n) return SGUFP_ERR_ARG;
-    const int64_t lo = from_bottom ? 0 : ctx->fr_n - n;
+// host copies of the frontier entries [lo, lo + n): records (states decoded, solutions
+// re-based to 0) and, when keys is given, their deferred-loop keys
+static int read_records(sgufp_ctx *ctx, int64_t lo, int n, uint16_t *gl, double *lb, double *ub, int64_t *states_off,
+                        int16_t *states, int64_t *sol_off, int16_t *sol, std::vector<std::string> *keys) {
+    FrontierDev &f = ctx->fr;
+    std::vector<uint16_t> g(n), len(n);
+    std::vector<double> l(n), u(n);
+    std::vector<uint32_t> mask(n);
+    std::vector<int64_t> so(n + 1);
+    if (!ctx->download(g.data(), f.gl + lo, n) || !ctx->download(l.data(), f.lb + lo, n) ||
+        !ctx->download(u.data(), f.ub + lo, n) || !ctx->download(mask.data(), f.mask + lo, n) ||
+        !ctx->download(len.data(), f.sol_len + lo, n) || !ctx->download(so.data(), f.sol_off + lo, n) || !ctx->sync())
+        return SGUFP_ERR_HIP;
+    // arena span of the records (offsets increase with the entry index)
+    int64_t s_hi = ctx->fr_sol_top;
+    if (lo + n < ctx->fr_n && (!ctx->download(&s_hi, f.sol_off + lo + n, 1) || !ctx->sync())) return SGUFP_ERR_HIP;
+    const int64_t s_lo = so[0];
+    std::vector<int16_t> arena((size_t)(s_hi - s_lo));
+    if (!ctx->download(arena.data(), f.sol + s_lo, arena.size()) || !ctx->sync()) return SGUFP_ERR_HIP;
+    if (gl) std::copy(g.begin(), g.end(), gl);
+    if (lb) std::copy(l.begin(), l.end(), lb);
+    if (ub) std::copy(u.begin(), u.end(), ub);
+    ctx->decode_states(g.data(), mask.data(), (size_t)n, states_off, states);
+    int64_t o = 0;
+    for (int k = 0; k < n; k++) {
+        if (sol_off) sol_off[k] = o;
+        if (sol) std::memcpy(sol + o, arena.data() + (so[k] - s_lo), len[k] * sizeof(int16_t));
+        o += len[k];
+    }
+    if (sol_off) sol_off[n] = o;
+    if (keys) {
+        keys->assign((size_t)n, std::string());
+        for (int k = 0; k < n; k++)
+            sgufp_ctx::make_record_key(g[k], mask[k], arena.data() + (so[k] - s_lo), len[k], (*keys)[k]);
+    }
+    return SGUFP_OK;
+}
+
+static int records_size(sgufp_ctx *ctx, int64_t lo, int n, int64_t *n_states, int64_t *n_sol) {
     std::vector<uint32_t> mask(n);
     std::vector<uint16_t> len(n);
     if (!ctx->download(mask.data(), ctx->fr.mask + lo, n) || !ctx->download(len.data(), ctx->fr.sol_len + lo, n) ||
@@ -259,6 +332,27 @@ int sgufp_frontier_take_size(sgufp_ctx *ctx, int n, int from_bottom, int64_t *n_
     return SGUFP_OK;
 }
 
+int sgufp_frontier_take_size(sgufp_ctx *ctx, int n, int from_bottom, int64_t *n_states, int64_t *n_sol) {
+    if (!ctx || n < 0 || n > ctx->fr_n) return SGUFP_ERR_ARG;
+    return records_size(ctx, from_bottom ? 0 : ctx->fr_n - n, n, n_states, n_sol);
+}
+
+int sgufp_frontier_peek_size(sgufp_ctx *ctx, int64_t first, int n, int64_t *n_states, int64_t *n_sol) {
+    if (!ctx || n < 0 || first < 0 || first + n > ctx->fr_n) return SGUFP_ERR_ARG;
+    return records_size(ctx, first, n, n_states, n_sol);
+}
+
+int sgufp_frontier_peek(sgufp_ctx *ctx, int64_t first, int n, uint16_t *gl, double *lb, double *ub,
+                        int64_t *states_off, int16_t *states, int64_t *sol_off, int16_t *sol) {
+    if (!ctx || n < 0 || first < 0 || first + n > ctx->fr_n) return SGUFP_ERR_ARG;
+    if (n == 0) {
+        if (states_off) states_off[0] = 0;
+        if (sol_off) sol_off[0] = 0;
+        return SGUFP_OK;
+    }
+    return read_records(ctx, first, n, gl, lb, ub, states_off, states, sol_off, sol, nullptr);
+}
+
 int sgufp_frontier_take(sgufp_ctx *ctx, int n, int from_bottom, uint16_t *gl, double *lb, double *ub,
                         int64_t *states_off, int16_t *states, int64_t *sol_off, int16_t *sol) {
     if (!ctx || n < 0 || n > ctx->fr_n) return SGUFP_ERR_ARG;
@@ -267,37 +361,19 @@ int sgufp_frontier_take(sgufp_ctx *ctx, int n, int from_bottom, uint16_t *gl, do
         if (sol_off) sol_off[0] = 0;
         return SGUFP_OK;
     }
-    FrontierDev &f = ctx->fr;
     const int64_t total = ctx->fr_n;
     const int64_t lo = from_bottom ? 0 : total - n;
-    std::vector<uint16_t> g(n), len(n);
-    std::vector<double> l(n), u(n);
-    std::vector<uint32_t> mask(n);
-    std::vector<int64_t> so(n + 1);
-    if (!ctx->download(g.data(), f.gl + lo, n) || !ctx->download(l.data(), f.lb + lo, n) ||
-        !ctx->download(u.data(), f.ub + lo, n) || !ctx->download(mask.data(), f.mask + lo, n) ||
-        !ctx->download(len.data(), f.sol_len + lo, n) || !ctx->download(so.data(), f.sol_off + lo, n) || !ctx->sync())
-        return SGUFP_ERR_HIP;
-    // arena span of the taken records (offsets increase with the entry index)
-    int64_t s_hi = ctx->fr_sol_top;
-    if (from_bottom && n < total) {
-        if (!ctx->download(&s_hi, f.sol_off + n, 1) || !ctx->sync()) return SGUFP_ERR_HIP;
-    }
-    const int64_t s_lo = so[0];
-    std::vector<int16_t> arena((size_t)(s_hi - s_lo));
-    if (!ctx->download(arena.data(), f.sol + s_lo, arena.size()) || !ctx->sync()) return SGUFP_ERR_HIP;
-    if (gl) std::copy(g.begin(), g.end(), gl);
-    if (lb) std::copy(l.begin(), l.end(), lb);
-    if (ub) std::copy(u.begin(), u.end(), ub);
-    ctx->decode_states(g.data(), mask.data(), (size_t)n, states_off, states);
-    int64_t o = 0;
-    for (int k = 0; k < n; k++) {
-        if (sol_off) sol_off[k] = o;
-        if (sol) std::memcpy(sol + o, arena.data() + (so[k] - s_lo), len[k] * sizeof(int16_t));
-        o += len[k];
-    }
-    if (sol_off) sol_off[n] = o;
+    std::vector<std::string> keys;
+    const int rc = read_records(ctx, lo, n, gl, lb, ub, states_off, states, sol_off, sol,
+                                ctx->deferred_seen.empty() ? nullptr : &keys);
+    if (rc != SGUFP_OK) return rc;
+    // a taken record leaves this context (another shard, or the caller): its deferred loop's
+    // seen list goes no further (the receiver restarts the loop; re-solving a path only
+    // re-adds a valid cut)
+    for (auto &k : keys) ctx->deferred_seen.erase(k);
     if (!from_bottom || n == total) {
+        int64_t s_lo = 0;
+        if (!ctx->download(&s_lo, ctx->fr.sol_off + lo, 1) || !ctx->sync()) return SGUFP_ERR_HIP;
         ctx->fr_n -= n;
         ctx->fr_sol_top = ctx->fr_n ? s_lo : 0;
         return SGUFP_OK;
@@ -352,6 +428,16 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
     const int64_t base = T - b;
     S.popped = b;
 
+    for (auto &t : ctx->trace_items) t.clear();
+    // deferred loops: keys of the popped records (resumed below, or dropped when pruned)
+    std::vector<std::string> keys;
+    if (!ctx->deferred_seen.empty() && !ctx->slice_keys(base, b, keys)) return SGUFP_ERR_HIP;
+    std::vector<double> ub_in;
+    if (ctx->trace) {
+        ub_in.resize(b);
+        if (!ctx->download(ub_in.data(), ctx->fr.ub + base, b) || !ctx->sync()) return SGUFP_ERR_HIP;
+    }
+
     // 1-3: relax the top of the stack in place
     ctx->n = b;
     ctx->cur = ctx->frontier_slice(base, b);
@@ -395,6 +481,19 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
         S.sweeps += sw[k];
     }
     S.exact = (int64_t)act.size();
+    if (ctx->trace)
+        for (int k = 0; k < b; k++) {
+            ctx->trace_items[0].emplace_back();
+            auto &t = ctx->trace_items[0].back();
+            t.record = k;
+            t.code = st[k];
+            t.value = ub_in[k];
+        }
+    // a popped record that left its deferred loop without re-entering it (pruned by bound
+    // or by a cut of the grown pool) drops its seen list
+    if (!keys.empty())
+        for (int k = 0; k < b; k++)
+            if (st[k] != SGUFP_NEEDS_SUBPROBLEM) ctx->deferred_seen.erase(keys[k]);
 
     // 4: refinement loop of the exact DDs (NodeExplorer.cpp:946-969), device-resident: per
     // iteration k_loop_check (argmax path seen? -> {ub, ub}; else fresh), one synchronisation,
@@ -414,11 +513,9 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
         if (!ctx->loop_reserve(b, 64)) return SGUFP_ERR_HIP;
         std::vector<int32_t> nseen(b, 0);
         if (!ctx->hip_ok(hipMemsetAsync(ctx->seen.n, 0, (size_t)b * 4, ctx->stream), "memset")) return SGUFP_ERR_HIP;
-        if (!ctx->deferred_seen.empty()) {
+        if (!keys.empty()) {
             for (int k : act) {
-                std::string key;
-                if (!ctx->record_key(base + k, key)) return SGUFP_ERR_HIP;
-                auto it = ctx->deferred_seen.find(key);
+                auto it = ctx->deferred_seen.find(keys[k]);
                 if (it == ctx->deferred_seen.end()) continue;
                 const int cnt = (int)it->second.size();
                 if (!ctx->loop_reserve(b, cnt + 1)) return SGUFP_ERR_HIP;
@@ -434,9 +531,15 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
         std::vector<double> pub;
         std::vector<int> prev;            // fresh records of the previous iteration (rows filed below)
         int prev_first = 0;
+        std::vector<double> pobj;         // trace: the previous iteration's sum_s obj_s / S
+        std::vector<size_t> prev_trace;   // trace: items of the previous iteration's subproblems
         auto file_rows = [&]() -> bool {  // Container::add: feasibility list, optimality list
             for (size_t i = 0; i < prev.size(); i++) {
                 if (ptype[i] < 0) {
+                    // the rows of that launch leave the pool again (they were appended and
+                    // applied on the device before the host saw the type); the batch's results
+                    // are not used past the error
+                    ctx->n_rows = prev_first;
                     ctx->err = "scenario subproblem failed (invalid path or numerical failure)";
                     return false;
                 }
@@ -445,13 +548,27 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
             for (int want = 1; want >= 0; want--)
                 for (size_t i = 0; i < prev.size(); i++) {
                     if (ptype[i] != want) continue;
-                    (want ? ctx->f_rows : ctx->o_rows).push_back(prev_first + (int)i);
+                    auto &list = want ? ctx->f_rows : ctx->o_rows;
+                    if (ctx->trace) {
+                        auto &t = ctx->trace_items[1][prev_trace[i]];
+                        t.code = want;
+                        t.row = (int32_t)list.size();
+                        t.value = pobj[i];
+                    }
+                    list.push_back(prev_first + (int)i);
                     ctx->row_ub[(size_t)prev_first + i] = pub[i];
                     (want ? S.new_feasibility_cuts : S.new_optimality_cuts)++;
                 }
             ctx->order_dirty = true;
             prev.clear();
             return true;
+        };
+        // trace: the argmax path of batch slot k as the loop check saw it
+        std::vector<uint16_t> tlen;
+        std::vector<int16_t> tpath;
+        const size_t Lc = (size_t)ctx->sc.Lcap;
+        auto slot_path = [&](int k) {
+            return std::vector<int16_t>(tpath.begin() + (long)(k * Lc), tpath.begin() + (long)(k * Lc + tlen[k]));
         };
         while (na > 0) {
             if (!ctx->hip_ok(launch_loop_check(o, ctx->seen, ctx->d_lact, na, ctx->net.m, ctx->d_lflag, ctx->d_lchain,
@@ -461,12 +578,21 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
             chains.resize(na);
             ptype.resize(prev.size());
             pub.resize(prev.size());
+            pobj.resize(prev.size());
             if (!ctx->download(flag.data(), ctx->d_lflag, (size_t)na) ||
                 !ctx->download(chains.data(), ctx->d_lchain, (size_t)na) ||
                 !ctx->download(ptype.data(), ctx->sio.cut_type, prev.size()) ||
-                !ctx->download(pub.data(), ctx->d_lrowub, prev.size()) || !ctx->sync())   // the one sync
+                !ctx->download(pub.data(), ctx->d_lrowub, prev.size()) ||
+                (ctx->trace && !ctx->download(pobj.data(), ctx->sio.obj_mean, prev.size())) || !ctx->sync())   // the one sync
                 return SGUFP_ERR_HIP;
             if (!file_rows()) return SGUFP_ERR_STATE;
+            if (ctx->trace) {
+                tlen.resize((size_t)b);
+                tpath.resize((size_t)b * Lc);
+                if (!ctx->download(tlen.data(), o.path_len, (size_t)b) || !ctx->download(tpath.data(), o.path, tpath.size()) ||
+                    !ctx->sync())
+                    return SGUFP_ERR_HIP;
+            }
             std::vector<int> fresh;
             int nct = 1;
             for (int a = 0; a < na; a++) {
@@ -474,6 +600,11 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
                 if (flag[a] == 1) {                 // {ub, ub, {}, SUCCESS}
                     closed.push_back(k);
                     S.exact_closed++;
+                    if (ctx->trace) {
+                        ctx->trace_items[2].emplace_back();
+                        ctx->trace_items[2].back().record = k;
+                        ctx->trace_items[2].back().path = slot_path(k);
+                    }
                 } else if (flag[a] == 2) {
                     fresh.push_back(k);
                     nct = std::max(nct, chains[a]);
@@ -485,7 +616,9 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
             }
             if (fresh.empty()) break;
             if ((ctx->bnb_max_iters > 0 && S.refine_iters >= ctx->bnb_max_iters) ||
-                (ctx->bnb_seconds > 0 && seconds_since(t_round) >= ctx->bnb_seconds)) {
+                (ctx->bnb_seconds > 0 && S.refine_iters > 0 && seconds_since(t_round) >= ctx->bnb_seconds)) {
+                // (every round runs at least one iteration: a batch whose relaxation alone
+                // outlasts round_seconds still makes progress)
                 deferred.swap(fresh);    // their current path is unseen: solved when resumed
                 break;
             }
@@ -536,6 +669,17 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
             S.subproblems += nf;
             prev = fresh;
             prev_first = first;
+            if (ctx->trace) {
+                prev_trace.clear();
+                for (int i = 0; i < nf; i++) {
+                    prev_trace.push_back(ctx->trace_items[1].size());
+                    ctx->trace_items[1].emplace_back();
+                    auto &t = ctx->trace_items[1].back();
+                    t.record = fresh[i];
+                    t.code = -1;
+                    t.path = slot_path(fresh[i]);
+                }
+            }
             act = fresh;
             act.insert(act.end(), rest.begin(), rest.end());
             na = (int)act.size();
@@ -544,8 +688,10 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
         if (!prev.empty()) {
             ptype.resize(prev.size());
             pub.resize(prev.size());
+            pobj.resize(prev.size());
             if (!ctx->download(ptype.data(), ctx->sio.cut_type, prev.size()) ||
-                !ctx->download(pub.data(), ctx->d_lrowub, prev.size()) || !ctx->sync())
+                !ctx->download(pub.data(), ctx->d_lrowub, prev.size()) ||
+                (ctx->trace && !ctx->download(pobj.data(), ctx->sio.obj_mean, prev.size())) || !ctx->sync())
                 return SGUFP_ERR_HIP;
             if (!file_rows()) return SGUFP_ERR_STATE;
         }
@@ -553,6 +699,7 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
         // deferred records' bound
         if (!ctx->download(ub.data(), o.ub, b) || !ctx->sync()) return SGUFP_ERR_HIP;
         for (int k : closed) lbv[k] = ub[k];
+        for (auto &t : ctx->trace_items[2]) t.value = ub[t.record];
         for (int k : deferred) {
             seen_host.emplace_back();
             if (!ctx->seen_download(k, nseen[k], seen_host.back())) return SGUFP_ERR_HIP;

@@ -709,6 +709,7 @@ int sgufp_cuts_clear(sgufp_ctx *ctx) {
     ctx->o_rows.clear();
     ctx->n_rows = 0;
     ctx->order_dirty = true;
+    ctx->shared[0] = ctx->shared[1] = 0;   // frontier shards: nothing of the new pool exchanged yet
     return SGUFP_OK;
 }
 

@@ -111,7 +111,16 @@ struct sgufp_ctx {
     // record (gl, state mask, solution): restored when the record is popped again
     std::unordered_map<std::string, std::vector<std::vector<int16_t>>> deferred_seen;
     static void make_record_key(uint16_t gl, uint32_t mask, const int16_t *sol, size_t len, std::string &key);
-    bool record_key(int64_t entry, std::string &key);
+    // keys of the frontier entries [lo, lo + count) (bulk downloads, one synchronisation)
+    bool slice_keys(int64_t lo, int count, std::vector<std::string> &keys);
+    // round trace (sgufp_bnb_set_trace): what the last sgufp_bnb_step did, for tests
+    bool trace = false;
+    struct TraceItem {
+        int32_t record = -1, code = 0, row = -1;
+        double value = 0.0;
+        std::vector<int16_t> path;
+    };
+    std::vector<TraceItem> trace_items[3];    // 0 popped, 1 subproblems, 2 closed loops
     // device-resident refinement loop (bnb.cpp, bnb_kernels.hip): seen-path lists per batch
     // slot and the per-iteration index / flag arrays
     SeenLists seen{};

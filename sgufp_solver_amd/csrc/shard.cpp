@@ -47,6 +47,30 @@ int64_t give_count(int64_t size) {
     return 0;
 }
 
+// The work-sharing plan every shard computes from the all-gathered stack sizes (identical on
+// every rank): give[r] records from the bottom of shard r, the idle shards in rank order, and
+// idle shard j receiving records [give[r] * j / ni, give[r] * (j + 1) / ni) of every donor r.
+// Returns the number of idle shards (0: nothing moves).
+int balance_plan(int world, const int64_t *sizes, int64_t *give, int32_t *idle) {
+    int ni = 0;
+    bool any = false;
+    for (int r = 0; r < world; r++) {
+        if (sizes[r] == 0) idle[ni++] = r;
+        give[r] = sizes[r] > 0 ? give_count(sizes[r]) : 0;
+        any = any || give[r] > 0;
+    }
+    if (ni == 0 || !any) {
+        std::fill(give, give + world, 0);
+        return 0;
+    }
+    return ni;
+}
+
+void chunk_of(int64_t give, int j, int ni, int64_t &lo, int64_t &hi) {
+    lo = give * j / ni;
+    hi = give * (j + 1) / ni;
+}
+
 bool nccl_ok(sgufp_ctx *ctx, ncclResult_t r, const char *what) {
     if (r == ncclSuccess) return true;
     ctx->err = std::string(what) + ": " + ncclGetErrorString(r);
@@ -231,21 +255,18 @@ int sgufp_frontier_balance(sgufp_ctx *ctx, int64_t *received) {
     std::vector<int64_t> sizes;
     const int64_t mine = ctx->fr_n;
     if (!allgather_i64(ctx, &mine, 1, sizes)) return SGUFP_ERR_HIP;
-    std::vector<int> idle;
-    for (int r = 0; r < W; r++)
-        if (sizes[r] == 0) idle.push_back(r);
     std::vector<int64_t> give(W, 0);
-    bool any = false;
-    for (int r = 0; r < W; r++) {
-        give[r] = sizes[r] > 0 ? give_count(sizes[r]) : 0;
-        any = any || give[r] > 0;
+    std::vector<int32_t> idle(W, -1);
+    const int ni = balance_plan(W, sizes.data(), give.data(), idle.data());
+    if (ni == 0) return SGUFP_OK;
+    idle.resize(ni);
+    auto chunk = [&](int r, int j, int64_t &lo, int64_t &hi) { chunk_of(give[r], j, ni, lo, hi); };
+    // the given records leave this context: their deferred loops' seen lists go no further
+    if (give[me] > 0 && !ctx->deferred_seen.empty()) {
+        std::vector<std::string> keys;
+        if (!ctx->slice_keys(0, (int)give[me], keys)) return SGUFP_ERR_HIP;
+        for (auto &k : keys) ctx->deferred_seen.erase(k);
     }
-    if (idle.empty() || !any) return SGUFP_OK;
-    const int ni = (int)idle.size();
-    auto chunk = [&](int r, int j, int64_t &lo, int64_t &hi) {
-        lo = give[r] * j / ni;
-        hi = give[r] * (j + 1) / ni;
-    };
     // solution spans of this shard's chunks: [sol_lo, sol_hi) per idle shard
     std::vector<int64_t> span((size_t)2 * ni, 0);
     if (give[me] > 0) {
@@ -340,6 +361,34 @@ int sgufp_frontier_balance(sgufp_ctx *ctx, int64_t *received) {
     }
     if (give[me] > 0 && !ctx->frontier_drop_bottom(give[me])) return SGUFP_ERR_HIP;
     if (received) *received = got;
+    return SGUFP_OK;
+}
+
+int sgufp_balance_plan(int world, const int64_t *sizes, int64_t *give, int32_t *idle, int64_t *chunk_lo,
+                       int64_t *chunk_hi) {
+    if (world < 1 || !sizes || !give || !idle) return -1;
+    for (int r = 0; r < world; r++)
+        if (sizes[r] < 0) return -1;
+    const int ni = balance_plan(world, sizes, give, idle);
+    for (int r = 0; r < world; r++)
+        for (int j = 0; j < ni; j++) {
+            int64_t lo, hi;
+            chunk_of(give[r], j, ni, lo, hi);
+            if (chunk_lo) chunk_lo[(size_t)r * world + j] = lo;
+            if (chunk_hi) chunk_hi[(size_t)r * world + j] = hi;
+        }
+    return ni;
+}
+
+int sgufp_comm_allgather_i64(sgufp_ctx *ctx, const int64_t *mine, int k, int64_t *all) {
+    if (!ctx || k < 0 || k > 4 || (k && (!mine || !all))) return SGUFP_ERR_ARG;
+    if (!ctx->comm) {
+        std::copy(mine, mine + k, all);
+        return SGUFP_OK;
+    }
+    std::vector<int64_t> v;
+    if (!allgather_i64(ctx, mine, k, v)) return SGUFP_ERR_HIP;
+    std::copy(v.begin(), v.end(), all);
     return SGUFP_OK;
 }
 

@@ -33,7 +33,8 @@ EXPORTS = [
     "sgufp_restricted_relax", "sgufp_restricted_results", "sgufp_restricted_paths", "sgufp_restricted_cutset_size",
     "sgufp_restricted_cutset", "sgufp_bnb_set_limits", "sgufp_comm_unique_id", "sgufp_comm_init",
     "sgufp_comm_info", "sgufp_comm_destroy", "sgufp_incumbent_allreduce", "sgufp_cuts_exchange",
-    "sgufp_frontier_sizes", "sgufp_frontier_balance",
+    "sgufp_frontier_sizes", "sgufp_frontier_balance", "sgufp_bnb_set_trace", "sgufp_bnb_trace",
+    "sgufp_frontier_peek_size", "sgufp_frontier_peek", "sgufp_balance_plan", "sgufp_comm_allgather_i64",
 ]
 
 
@@ -67,6 +68,22 @@ def comm_unique_id() -> bytes:
     if lib.sgufp_comm_unique_id(buf, 128) != 0:
         raise RuntimeError("sgufp_comm_unique_id failed")
     return bytes(buf)
+
+
+def balance_plan(sizes):
+    """sgufp_balance_plan (host only): (give[world], idle ranks, chunk_lo / chunk_hi [world,
+    world]) of the work sharing sgufp_frontier_balance does for these stack sizes."""
+    lib = load_library()
+    w = len(sizes)
+    sz = np.asarray(sizes, dtype=np.int64)
+    give = np.zeros(w, dtype=np.int64)
+    idle = np.zeros(w, dtype=np.int32)
+    lo = np.zeros((w, w), dtype=np.int64)
+    hi = np.zeros((w, w), dtype=np.int64)
+    ni = lib.sgufp_balance_plan(w, _ptr(sz), _ptr(give), _ptr(idle), _ptr(lo), _ptr(hi))
+    if ni < 0:
+        raise ValueError("sgufp_balance_plan: bad sizes")
+    return give, [int(x) for x in idle[:ni]], lo[:, :ni], hi[:, :ni]
 
 
 def load_library(path: str = LIB_PATH) -> C.CDLL:
@@ -114,7 +131,13 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.sgufp_frontier_take_size.argtypes = [P, C.c_int, C.c_int, P, P]
     lib.sgufp_frontier_take.argtypes = [P, C.c_int, C.c_int, P, P, P, P, P, P, P]
     lib.sgufp_bnb_step.argtypes = [P, C.c_int, P, P]
+    lib.sgufp_balance_plan.argtypes = [C.c_int, P, P, P, P, P]
+    lib.sgufp_comm_allgather_i64.argtypes = [P, P, C.c_int, P]
+    lib.sgufp_frontier_peek_size.argtypes = [P, C.c_int64, C.c_int, P, P]
+    lib.sgufp_frontier_peek.argtypes = [P, C.c_int64, C.c_int, P, P, P, P, P, P, P]
     lib.sgufp_bnb_set_limits.argtypes = [P, C.c_int, C.c_double]
+    lib.sgufp_bnb_set_trace.argtypes = [P, C.c_int]
+    lib.sgufp_bnb_trace.argtypes = [P, C.c_int, P, P, P, P, P, P, P, P]
     lib.sgufp_comm_unique_id.argtypes = [P, C.c_int]
     lib.sgufp_comm_init.argtypes = [P, C.c_int, C.c_int, P]
     lib.sgufp_comm_info.argtypes = [P, P, P]
@@ -505,6 +528,21 @@ class Engine:
                                                  _ptr(states), _ptr(poff), _ptr(sol)))
         return batch_from_arrays(gl[:n], lb[:n], ub[:n], soff, states[:ns.value], poff, sol[:nl.value])
 
+    def frontier_peek(self, first: int, n: int) -> BatchArrays:
+        """Copies of the records at stack positions [first, first + n) (0 = bottom), left in place."""
+        ns, nl = C.c_int64(0), C.c_int64(0)
+        self._check(self.lib.sgufp_frontier_peek_size(self.ctx, int(first), n, C.byref(ns), C.byref(nl)))
+        gl = np.zeros(max(n, 1), dtype=np.uint16)
+        lb = np.zeros(max(n, 1), dtype=np.float64)
+        ub = np.zeros(max(n, 1), dtype=np.float64)
+        soff = np.zeros(n + 1, dtype=np.int64)
+        states = np.zeros(max(ns.value, 1), dtype=np.int16)
+        poff = np.zeros(n + 1, dtype=np.int64)
+        sol = np.zeros(max(nl.value, 1), dtype=np.int16)
+        self._check(self.lib.sgufp_frontier_peek(self.ctx, int(first), n, _ptr(gl), _ptr(lb), _ptr(ub), _ptr(soff),
+                                                 _ptr(states), _ptr(poff), _ptr(sol)))
+        return batch_from_arrays(gl[:n], lb[:n], ub[:n], soff, states[:ns.value], poff, sol[:nl.value])
+
     def bnb_step(self, incumbent: float, max_nodes: int = 0) -> Tuple[float, BnbStats]:
         """One batched B&B round; returns the new incumbent and the round's counters."""
         z = C.c_double(incumbent)
@@ -516,6 +554,28 @@ class Engine:
         """Bound the refinement loops of one bnb_step (0: no limit); unfinished exact
         records go back on top of the frontier."""
         self._check(self.lib.sgufp_bnb_set_limits(self.ctx, int(max_refine_iters), C.c_double(round_seconds)))
+
+    def bnb_set_trace(self, on: bool = True):
+        """Keep what each bnb_step round did (sgufp_bnb_set_trace) for bnb_trace()."""
+        self._check(self.lib.sgufp_bnb_set_trace(self.ctx, 1 if on else 0))
+
+    def bnb_trace(self, kind: int):
+        """The last round's trace of one kind (0 popped records, 1 subproblems, 2 closed
+        loops; include/sgufp_hip.h): a list of (record, code, row, value, path)."""
+        n, pe = C.c_int64(0), C.c_int64(0)
+        self._check(self.lib.sgufp_bnb_trace(self.ctx, int(kind), C.byref(n), C.byref(pe), None, None, None, None,
+                                             None, None))
+        k = n.value
+        rec = np.zeros(max(k, 1), dtype=np.int32)
+        code = np.zeros(max(k, 1), dtype=np.int32)
+        row = np.zeros(max(k, 1), dtype=np.int32)
+        val = np.zeros(max(k, 1), dtype=np.float64)
+        off = np.zeros(k + 1, dtype=np.int64)
+        paths = np.zeros(max(pe.value, 1), dtype=np.int16)
+        self._check(self.lib.sgufp_bnb_trace(self.ctx, int(kind), C.byref(n), C.byref(pe), _ptr(rec), _ptr(code),
+                                             _ptr(row), _ptr(val), _ptr(off), _ptr(paths)))
+        return [(int(rec[i]), int(code[i]), int(row[i]), float(val[i]), [int(x) for x in paths[off[i]:off[i + 1]]])
+                for i in range(k)]
 
     # -- frontier shards over RCCL (shard.cpp) --------------------------------------
     def comm_init(self, world: int, rank: int, uid: bytes):
@@ -536,6 +596,13 @@ class Engine:
         a = (C.c_int64 * max(world, 1))()
         self._check(self.lib.sgufp_frontier_sizes(self.ctx, a))
         return [int(x) for x in a]
+
+    def comm_allgather_i64(self, vals: Sequence[int], world: int) -> np.ndarray:
+        """[world, len(vals)] (len <= 4) over the context's communicator (sgufp_comm_allgather_i64)."""
+        v = np.asarray(list(vals), dtype=np.int64)
+        out = np.zeros(max(world * len(v), 1), dtype=np.int64)
+        self._check(self.lib.sgufp_comm_allgather_i64(self.ctx, _ptr(v), len(v), _ptr(out)))
+        return out[:world * len(v)].reshape(world, len(v))
 
     def frontier_balance(self) -> int:
         n = C.c_int64(0)

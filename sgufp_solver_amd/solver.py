@@ -202,12 +202,25 @@ class DDSolver:
         explored = self.counters.get("children", 0)
         comm = self.shard_comm
         per_rank = [dict(self.counters)]
+        keys = sorted(self.counters)
+        first = True
         if comm is not None:
-            keys = sorted(self.counters)
             g = comm.allgather_i64([int(self.counters[k]) for k in keys])
             per_rank = [{k: int(v) for k, v in zip(keys, row)} for row in g]
             explored = sum(c.get("children", 0) for c in per_rank)
-        first = comm is None or comm.rank == 0
+            first = comm.rank == 0
+        elif self.native_world > 1:
+            # the library's own communicator (shard.cpp): counters gathered four at a time
+            import ctypes
+            w, r = ctypes.c_int(0), ctypes.c_int(0)
+            self.eng._check(self.eng.lib.sgufp_comm_info(self.eng.ctx, ctypes.byref(w), ctypes.byref(r)))
+            cols = []
+            for i in range(0, len(keys), 4):
+                cols.append(self.eng.comm_allgather_i64([int(self.counters[k]) for k in keys[i:i + 4]], w.value))
+            g = np.concatenate(cols, axis=1)
+            per_rank = [{k: int(v) for k, v in zip(keys, row)} for row in g]
+            explored = sum(c.get("children", 0) for c in per_rank)
+            first = r.value == 0
         if self.verbose and solver_counters and first:
             print(worker_stats_text(per_rank, self.eng.cuts_count(1), self.eng.cuts_count(0)), end="")
         if self.verbose and first:
@@ -225,7 +238,7 @@ def worker_stats_text(per_worker, n_feas_cuts: int, n_opt_cuts: int) -> str:
     dash = "-" * 72
     processed = [float(c.get("relaxed", 0)) for c in per_worker]
     mean = sum(processed) / len(processed) if processed else 0.0
-    absdev = sum(abs(p - mean) for p in processed) / len(processed) if processed else 0.0
+    absdev = 0.0      # the reference's stats_absdev is a stub returning 0 (statistics.h:31-33)
     lines = [dash, "Processed: " + "".join(f"{int(p)}  " for p in processed),
              f"Total: {_g(sum(processed))}\t Mean: {_g(mean)}\t Deviation: {_g(absdev)}\t "
              f"Min: {_g(min(processed) if processed else 0.0)}\t Max: {_g(max(processed) if processed else 0.0)}",

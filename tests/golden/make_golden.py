@@ -83,6 +83,9 @@ def add_refine():
             os.remove(tmp)
             runs.append({"incumbent": inc.hex(), "file": f"refine_{k}.txt.gz"})
         entries[name] = runs
+    with open(os.path.join(HERE, "refine_manifest.json")) as fh:
+        old = json.load(fh)
+    entries.update({k: v for k, v in old.items() if k.startswith("bnb_")})
     with open(os.path.join(HERE, "refine_manifest.json"), "w") as fh:
         json.dump(entries, fh, indent=1)
 
@@ -125,6 +128,9 @@ def main():
         manifest.append({"name": name, "config": cfg, "seed": seed, "scenarios": S, "n_feas": nf, "n_opt": no,
                          "frontier": mode, "nodes": len(nodes), "runs": outs})
         print(name, len(nodes), "nodes")
+    # cases made elsewhere (make_bnb_golden.py: the device B&B's own pools) stay listed
+    with open(os.path.join(HERE, "manifest.json")) as fh:
+        manifest += [c for c in json.load(fh) if "source" in c]
     with open(os.path.join(HERE, "manifest.json"), "w") as fh:
         json.dump(manifest, fh, indent=1)
     add_refine()

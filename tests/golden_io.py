@@ -22,6 +22,24 @@ def case_dir(name: str) -> str:
     return os.path.join(GOLDEN, name)
 
 
+_PLAIN = {}
+
+
+def golden_file(d: str, fname: str) -> str:
+    """Path of a plain-text fixture file of case directory d: the file itself, or -- for the
+    large pools of the device-B&B cases, stored as <fname>.gz -- a decompressed copy."""
+    path = os.path.join(d, fname)
+    if os.path.exists(path):
+        return path
+    if path not in _PLAIN:
+        import tempfile
+        out = os.path.join(tempfile.mkdtemp(prefix="sgufp_golden_"), fname)
+        with gzip.open(path + ".gz", "rb") as fi, open(out, "wb") as fo:
+            fo.write(fi.read())
+        _PLAIN[path] = out
+    return _PLAIN[path]
+
+
 def read_golden(name: str, fname: str) -> str:
     with gzip.open(os.path.join(case_dir(name), fname), "rb") as fh:
         return fh.read().decode()

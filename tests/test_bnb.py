@@ -97,6 +97,20 @@ def test_bnb_deferred_refinement_keeps_the_optimum(iters, batch):
     assert solver.counters["deferred"] > 0
 
 
+def test_tiny_round_deadline_still_progresses():
+    """A round deadline shorter than the relaxation itself (sgufp_bnb_set_limits with 1 us):
+    every round still runs one refinement iteration, so deferred loops advance and the search
+    ends at the extensive-form optimum instead of re-popping the same records forever."""
+    inst, path = _inst("T4", 3, 3)
+    opt = ef.solve(inst)
+    solver = DDSolver(path, max_batch=256, batch_nodes=16, max_rounds=200000, verbose=False, round_seconds=1e-6)
+    sol, _ = solver.start(DOUBLE_MIN)
+    solver.eng.close()
+    assert solver.complete
+    assert abs(sol - opt) <= TOL * max(1.0, abs(opt))
+    assert solver.counters["subproblems"] > 0
+
+
 def test_native_shard_calls_single_rank():
     """The library's own RCCL exchanges (shard.cpp) on a one-rank communicator: the search
     runs them after every round (incumbent all-reduce, cut exchange, frontier sizes, work

@@ -1,0 +1,75 @@
+"""The device B&B against the reference under the cuts the B&B itself makes.
+
+Every cut the reference's search applies comes from GuroSolver::solveSubProblem
+(NodeExplorer.cpp:957-969, grb.cpp:236-281); here it comes from k_sub_scenario.  Such rows
+have integral / dyadic coefficients, so equal state values and signed zeros are common --
+where the strict-`>` argmax (DD.cpp:3834), first-match back-tracking (DD.cpp:3808) and the
+std::max / std::min tie rules decide.  Round by round the tests below run the device search
+(sgufp_bnb_step with its round trace, include/sgufp_hip.h) and check:
+
+* parity of the round's relaxation: the records the round pops, relaxed under the pool and
+  incumbent the round sees, against the reference's own RelaxedDDNew (oracle/_ref/ref_dd
+  relaxp): status, exact flag, lb / ub bits, argmax path, cutset children, DD sizes; and the
+  round's own k_relax statuses (trace) equal those results;
+* bound pruning: a popped record is skipped unprocessed iff ub <= zOpt (DDSolver.cpp:707-711);
+* every optimality cut is tight at the path it was generated for (RHS + coef . y-bar ==
+  sum_s obj_s / S), every feasibility cut cuts its path off;
+* every closed loop's bound (the incumbent candidate, NodeExplorer.cpp:948-956) equals the
+  expected scenario value of the matching that closed it, and the incumbent is the best of
+  them -- for the incumbent's matching also against HiGHS on the reference's dual LP
+  restated (all S scenarios);
+* one refinement loop per round replayed step by step on the device (sgufp_batch_refine with
+  the subproblem's cuts) against ``ref_dd refine`` fed with the same cuts.
+
+BASELINE configs[2] (C3: 1k arcs, 64 scenarios, incumbent pruning -- seeded by the
+restricted-DD heuristic, and unseeded), configs[3]'s network (C4, 256 scenarios) and
+configs[4] (C5: 5k arcs, 512 scenarios, cut generation in the loop) are run for a bounded
+number of rounds: none of them closes.
+"""
+import pytest
+
+from oracle import bnb_parity as bp
+
+pytestmark = pytest.mark.gpu
+
+
+def _search_rounds(*args, **kw):
+    rep = bp.check_search(*args, **kw)
+    assert not rep["failures"], "\n".join(rep["failures"][:10])
+    return rep
+
+
+def test_bnb_parity_c3_seeded():
+    """BASELINE configs[2]: C3 / 64 scenarios with incumbent pruning, the incumbent seeded by
+    the width-64 restricted-DD heuristic (processX3's restricted half); two refinement
+    iterations per round keep the pool small enough for the reference's CPU sweeps."""
+    seen = _search_rounds("C3", 1, 64, rounds=80, batch=64, sample=32, min_subproblems=1, round_iters=2)
+    assert seen["checked"] > 0 and seen["subproblems"] > 0 and seen["opt_cuts"] > 0
+    assert seen["replayed"] > 0
+
+
+def test_bnb_parity_c3_unseeded():
+    """configs[2] from the root with no incumbent: the first exact leaves come from the search."""
+    seen = _search_rounds("C3", 2, 0, rounds=80, batch=64, sample=32, min_subproblems=1, round_iters=2)
+    assert seen["subproblems"] > 0
+
+
+def test_bnb_parity_m1_loops_close():
+    """A 64-scenario network small enough for the refinement loops to close (M1: 60 arcs, 13
+    V-bar nodes): unbounded loops, closed bounds == the matchings' expected values, the
+    incumbent == the best of them and == HiGHS on the reference's dual LP (64 scenarios)."""
+    seen = _search_rounds("M1", 1, 0, rounds=200, batch=64, sample=48, min_closed=4)
+    assert seen["closed"] >= 4 and seen["highs_checked"] == 64 and seen["replayed"] > 0
+
+
+def test_bnb_parity_c4():
+    """The headline network (C4: 1k arcs, 256 scenarios), seeded."""
+    seen = _search_rounds("C4", 1, 128, rounds=80, batch=64, sample=24, min_subproblems=1, round_iters=2)
+    assert seen["subproblems"] > 0
+
+
+def test_bnb_parity_c5():
+    """BASELINE configs[4]: 5k arcs, 512 scenarios, cut generation in the loop."""
+    seen = _search_rounds("C5", 1, 0, rounds=80, batch=32, sample=8, round_seconds=3.0, replay=False,
+                          min_subproblems=1, rounds_after=1, round_iters=1)
+    assert seen["relaxed"] > 0 and seen["subproblems"] > 0

@@ -21,7 +21,7 @@ CASES = [(c["name"], r) for c in golden_io.manifest() for r in c["runs"]]
 def test_oracle_matches_reference_fixture(oracle_bin, tmp_path, name, run):
     d = golden_io.case_dir(name)
     out = tmp_path / "o.txt"
-    subprocess.run([oracle_bin, "relax", f"{d}/net.txt", f"{d}/cuts.txt", f"{d}/nodes.txt", run["incumbent"], str(out)],
+    subprocess.run([oracle_bin, "relax", f"{d}/net.txt", golden_io.golden_file(d, "cuts.txt"), f"{d}/nodes.txt", run["incumbent"], str(out)],
                    check=True)
     want = golden_io.read_golden(name, run["file"])
     got = out.read_text()
@@ -37,7 +37,7 @@ REFINE = golden_io.refine_manifest()
 def test_oracle_refinement_loop_matches_reference(oracle_bin, tmp_path, name, run):
     d = golden_io.case_dir(name)
     out = tmp_path / "o.txt"
-    subprocess.run([oracle_bin, "refine", f"{d}/net.txt", f"{d}/cuts.txt", f"{d}/nodes.txt", run["incumbent"],
+    subprocess.run([oracle_bin, "refine", f"{d}/net.txt", golden_io.golden_file(d, "cuts.txt"), f"{d}/nodes.txt", run["incumbent"],
                     f"{d}/extra_cuts.txt", str(out)], check=True)
     assert out.read_text() == golden_io.read_golden(name, run["file"])
 
@@ -198,7 +198,7 @@ def test_oracle_clean_under_sanitizers(tmp_path, name):
     run = case["runs"][0]
     out = tmp_path / "o.txt"
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1")
-    p = subprocess.run([exe, "relax", f"{d}/net.txt", f"{d}/cuts.txt", f"{d}/nodes.txt", run["incumbent"], str(out)],
+    p = subprocess.run([exe, "relax", f"{d}/net.txt", golden_io.golden_file(d, "cuts.txt"), f"{d}/nodes.txt", run["incumbent"], str(out)],
                        capture_output=True, text=True, env=env, timeout=600)
     assert p.returncode == 0, p.stderr[-2000:]
     assert "runtime error" not in p.stderr and "AddressSanitizer" not in p.stderr

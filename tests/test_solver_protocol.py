@@ -199,6 +199,31 @@ def test_work_sharing_plan():
     assert plan([0, 100, 3, 0]) == ([(1, 40), (2, 1)], [0, 3])
 
 
+def test_native_balance_plan_matches_shards_plan():
+    """The C ABI's work-sharing plan (shard.cpp balance_plan / chunk_of, behind
+    sgufp_frontier_balance's RCCL sends) == shards.plan and ShardComm.rebalance's chunking on
+    random stack-size vectors (host only: no device is touched)."""
+    from sgufp_solver_amd.engine import balance_plan
+    from sgufp_solver_amd.shards import plan
+    rng = np.random.default_rng(7)
+    cases = [[0], [5], [0, 0], [1, 0], [0, 100, 3, 0], [5, 7], [31, 0, 32, 0, 0, 1]]
+    for _ in range(300):
+        w = int(rng.integers(1, 9))
+        sizes = [int(x) if rng.random() > 0.35 else 0 for x in rng.integers(0, 5000, size=w)]
+        if rng.random() < 0.3:
+            sizes = [int(x) for x in rng.integers(0, 40, size=w)]
+        cases.append(sizes)
+    for sizes in cases:
+        give, idle, lo, hi = balance_plan(sizes)
+        donors, idle_py = plan(sizes)
+        assert idle == (idle_py if donors else []), sizes
+        assert {r: int(g) for r, g in enumerate(give) if g > 0} == dict(donors), sizes
+        for r, g in donors:
+            for j in range(len(idle)):
+                assert (lo[r, j], hi[r, j]) == (g * j // len(idle), g * (j + 1) // len(idle)), (sizes, r, j)
+            assert hi[r, len(idle) - 1] == g          # the chunks cover the donor's records
+
+
 def test_record_pack_roundtrip():
     from sgufp_solver_amd.shards import pack_batch, unpack_batch
     recs = [NodeRecord(3, -1.5, 7.25, [1, 4], [2, -1, 5]), NodeRecord(0, -1e300, 1e300, [], []),
@@ -237,7 +262,7 @@ def test_worker_stats_format():
     lines = txt.split("\n")
     assert lines[0] == "-" * 72
     assert lines[1] == "Processed: 10  14  "
-    assert lines[2] == "Total: 24\t Mean: 12\t Deviation: 2\t Min: 10\t Max: 14"
+    assert lines[2] == "Total: 24\t Mean: 12\t Deviation: 0\t Min: 10\t Max: 14"   # statistics.h:31-33 stub
     assert "Cuts (feasibility, optimality): 1 , 5" in lines
     assert "(1, 3, 0)  (0, 0, 2)  " in lines
     assert lines[-3] == "-" * 72 and lines[-2] == "" and lines[-1] == ""   # dash, endl, endl
