@@ -219,7 +219,10 @@ int sgufp_bnb_set_limits(sgufp_ctx *ctx, int max_refine_iters, double round_seco
  *           row = index of the appended cut in that list (sgufp_cuts_rows), value = sum_s obj_s / S,
  *           path = the argmax path sent to the subproblem;
  *   kind 2  closed loops (the argmax path repeated, {ub, ub}, NodeExplorer.cpp:948-956): record,
- *           value = ub (the incumbent candidate), path = the repeated path.
+ *           value = ub (the incumbent candidate), path = the repeated path;
+ *   kind 3  the popped records' k_relax waves: record, code = exact single-cut redos, row = cuts
+ *           swept, value = the wave's wall_clock64 ticks (100 MHz; 0 unless the profiling
+ *           build lib_prof/ stamps them).
  * Any output pointer may be NULL; path_off has count + 1 entries. */
 int sgufp_bnb_set_trace(sgufp_ctx *ctx, int enabled);
 int sgufp_bnb_trace(sgufp_ctx *ctx, int kind, int64_t *count, int64_t *path_entries, int32_t *record, int32_t *code,

@@ -28,8 +28,8 @@ ARCH = "gfx950"
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
           f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}"]
 
-HIP_SOURCES = ["dd_kernels.hip", "sub_kernels.hip", "bnb_kernels.hip", "rdd_kernels.hip", "capi.cpp", "bnb.cpp",
-               "network.cpp", "shard.cpp"]
+HIP_SOURCES = ["dd_kernels.hip", "sub_kernels.hip", "bnb_kernels.hip", "rdd_kernels.hip", "exact_kernels.hip", "capi.cpp",
+               "bnb.cpp", "network.cpp", "shard.cpp"]
 LINK = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]   # frontier shards (shard.cpp)
 HOST_SOURCES = ["host/inavap.cpp"]
 

@@ -187,7 +187,7 @@ int sgufp_bnb_set_trace(sgufp_ctx *ctx, int enabled) {
 
 int sgufp_bnb_trace(sgufp_ctx *ctx, int kind, int64_t *count, int64_t *path_entries, int32_t *record, int32_t *code,
                     int32_t *row, double *value, int64_t *path_off, int16_t *paths) {
-    if (!ctx || kind < 0 || kind > 2) return SGUFP_ERR_ARG;
+    if (!ctx || kind < 0 || kind > 3) return SGUFP_ERR_ARG;
     const auto &items = ctx->trace_items[kind];
     int64_t pe = 0;
     for (size_t i = 0; i < items.size(); i++) {
@@ -481,14 +481,26 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
         S.sweeps += sw[k];
     }
     S.exact = (int64_t)act.size();
-    if (ctx->trace)
+    if (ctx->trace) {
+        std::vector<uint64_t> ticks(b);
+        std::vector<uint32_t> redo(b);
+        if (!ctx->download(ticks.data(), o.ticks, b) || !ctx->download(redo.data(), o.redo, b) || !ctx->sync())
+            return SGUFP_ERR_HIP;
+        const bool stamped = relax_has_phases();
         for (int k = 0; k < b; k++) {
             ctx->trace_items[0].emplace_back();
             auto &t = ctx->trace_items[0].back();
             t.record = k;
             t.code = st[k];
             t.value = ub_in[k];
+            ctx->trace_items[3].emplace_back();
+            auto &u = ctx->trace_items[3].back();
+            u.record = k;
+            u.code = (int32_t)(redo[k] & 0xFF);
+            u.row = (int32_t)sw[k];
+            u.value = stamped ? (double)ticks[k] : 0.0;
         }
+    }
     // a popped record that left its deferred loop without re-entering it (pruned by bound
     // or by a cut of the grown pool) drops its seen list
     if (!keys.empty())

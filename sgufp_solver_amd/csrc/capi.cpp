@@ -101,6 +101,12 @@ bool sgufp_ctx::init() {
     if (cb != 1 && cb != 4 && cb != 8 && cb != 16) cb = 4;
     nscreen = cb;
     if (const char *e = getenv("SGUFP_SCREEN")) nscreen = std::max(0, atoi(e));
+    if (const char *e = getenv("SGUFP_EXACT_FAST")) exact_fast = atoi(e) != 0;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+            cus = prop.multiProcessorCount;
+    }
     int64_t acap = std::max<int64_t>(1, (int64_t)std::max(0, L - 4) * (kRelaxedMaxWidth - 1) * maxU);
     if (ncap > (int64_t)kParentMask || acap > (int64_t)0x7FFFFFFF) { err = "DD capacity beyond 22-bit indices"; return false; }
     sc.Ncap = (int)ncap;
@@ -259,14 +265,57 @@ bool sgufp_ctx::relax_order(BatchIn &in) {
     return true;
 }
 
+// The cut-minor copy of the optimality rows (coefO, column j = o_rows[j]) grows with the
+// pool: new columns are transposed on the device before a relaxation; the root-fold buffer
+// holds one column per O cut for every batch slot.  The pending counters start at zero.
+bool sgufp_ctx::exact_prepare() {
+    const int no = (int)o_rows.size();
+    ex.enabled = (exact_fast && no > 0) ? 1 : 0;
+    ex.no = no;
+    if (!ex.enabled) return true;
+    const size_t rows_c = (size_t)net.n_slots + 2;
+    if (no > ocap) {
+        const int cap = std::max(no, std::max(2 * ocap, 256));
+        double *c = nullptr, *r = nullptr;
+        if (!alloc(c, rows_c * cap, "exact coefO")) return false;
+        if (o_built && !hip_ok(hipMemcpy2DAsync(c, (size_t)cap * 8, d_coefO, (size_t)ocap * 8, (size_t)o_built * 8, rows_c,
+                                                hipMemcpyDeviceToDevice, stream), "D2D 2D"))
+            return false;
+        if (d_R) release(d_R);
+        if (!alloc(r, (size_t)max_batch * cap, "exact root folds")) return false;
+        if (!sync()) return false;
+        if (d_coefO) release(d_coefO);
+        d_coefO = c;
+        d_R = r;
+        ocap = cap;
+    }
+    if (!d_pslot && (!alloc(d_pslot, (size_t)max_batch, "exact pending") || !alloc(d_pbase, (size_t)max_batch, "exact pending") ||
+                     !alloc(d_ectr, 4, "exact pending")))
+        return false;
+    if (o_built < no) {
+        if (!hip_ok(launch_exact_cols(d_rows, d_rhs, d_oorder, no, o_built, net.n_slots + 1, net.n_slots, ocap, d_coefO,
+                                      stream), "k_exact_cols"))
+            return false;
+        o_built = no;
+    }
+    if (!hip_ok(hipMemsetAsync(d_ectr, 0, 4 * sizeof(unsigned long long), stream), "memset")) return false;
+    ex.ostride = ocap;
+    ex.coefO = d_coefO;
+    ex.R = d_R;
+    ex.pend_slot = d_pslot;
+    ex.pend_base = d_pbase;
+    ex.ctr = d_ectr;
+    return true;
+}
+
 bool sgufp_ctx::relax_current(double optimal_lb) {
-    if (!push_orders()) return false;
+    if (!push_orders() || !exact_prepare()) return false;
     BatchIn in = cur;
     if (!relax_order(in)) return false;
     const Pool p = pool();
     hipStream_t st = stream;
     if (timing) hipEventRecord(ev[0], st);
-    if (!hip_ok(launch_relax(nd, sc, in, p, out, optimal_lb, cb, st), "k_relax")) return false;
+    if (!hip_ok(launch_relax(nd, sc, in, p, out, optimal_lb, cb, ex, cus, st), "k_relax")) return false;
     if (timing) hipEventRecord(ev[1], st);
     if (in.n > 0 && !hip_ok(launch_scan(out.nchild, out.sol_need, in.n, d_coff, d_soff, st), "k_scan2")) return false;
     uint64_t tot[2] = {0, 0};
@@ -709,6 +758,7 @@ int sgufp_cuts_clear(sgufp_ctx *ctx) {
     ctx->o_rows.clear();
     ctx->n_rows = 0;
     ctx->order_dirty = true;
+    ctx->o_built = 0;
     ctx->shared[0] = ctx->shared[1] = 0;   // frontier shards: nothing of the new pool exchanged yet
     return SGUFP_OK;
 }

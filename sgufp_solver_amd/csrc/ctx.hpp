@@ -26,7 +26,10 @@ size_t relax_lds_bytes(int Tcap, int Lcap, int cb, int us);
 size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw, int kbytes = 8);
 hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st);
 hipError_t launch_relax(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &, double, int,
-                        hipStream_t);
+                        const ExactIO &, int, hipStream_t);
+// exact_kernels.hip
+hipError_t launch_exact_cols(const double *rows, const double *rhs, const int32_t *o_order, int no, int first,
+                             int stride, int n_slots, int ostride, double *coefO, hipStream_t st);
 hipError_t launch_scan(const uint32_t *, const uint32_t *, int, uint64_t *, uint64_t *, hipStream_t);
 hipError_t launch_emit(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &,
                        const ChildOut &, hipStream_t);
@@ -120,7 +123,7 @@ struct sgufp_ctx {
         double value = 0.0;
         std::vector<int16_t> path;
     };
-    std::vector<TraceItem> trace_items[3];    // 0 popped, 1 subproblems, 2 closed loops
+    std::vector<TraceItem> trace_items[4];    // 0 popped, 1 subproblems, 2 closed loops, 3 k_relax waves
     // device-resident refinement loop (bnb.cpp, bnb_kernels.hip): seen-path lists per batch
     // slot and the per-iteration index / flag arrays
     SeenLists seen{};
@@ -201,6 +204,17 @@ struct sgufp_ctx {
     double *d_rowbuf = nullptr;               // sgufp_cuts_rows gather buffer
     int32_t *d_rowids = nullptr;
     size_t rowbuf_cap = 0, rowids_cap = 0;
+
+    // cut-parallel optimality phase of exact DDs (exact_kernels.hip; SGUFP_EXACT_FAST=0: off)
+    bool exact_fast = true;
+    int cus = 256;                            // compute units (persistent grids)
+    ExactIO ex{};
+    double *d_coefO = nullptr, *d_R = nullptr;
+    int ocap = 0, o_built = 0;                // columns of coefO allocated / filled
+    int32_t *d_pslot = nullptr;
+    uint32_t *d_pbase = nullptr;
+    unsigned long long *d_ectr = nullptr;
+    bool exact_prepare();
 
     bool timing = false;
     hipEvent_t ev[4] = {};

@@ -167,6 +167,35 @@ struct ChildOut {
     int16_t SGUFP_GBL *sol;
 };
 
+// Optimality phase of exact DDs (exact_kernels.hip).  An exact DD is a tree: every leaf is
+// one path, applyOptimalityCut makes no edit on it (DD.cpp:3986-4022 run only for non-exact
+// DDs), and its terminal weight ends as min over the O cuts of the path's value (a running
+// std::min, DD.cpp:3975-3984).  The outcome is therefore the same for any processing order
+// of the cuts: PRUNED_BY_OPTIMALITY_CUT iff max over leaves of that minimum <= optimalLB (the
+// running maximum only decreases), else ub = that maximum and the argmax path.  k_relax
+// hands such records over after the feasibility phase and screening (status
+// kExactPending); the leaf kernel computes the minima with lanes = cuts (all lanes walk the
+// same tree), a workgroup per pass of kLeafPass leaves of one record, every cut column read
+// once per pass from a cut-minor copy of the O rows.
+constexpr int32_t kExactPending = 5;
+constexpr int kExactMaxT = 16;         // DD layers (root included) the hand-off takes
+constexpr int kExactMaxEntries = 64;   // (T - 1) * ustride coefficient rows staged per cut block
+constexpr int kLeafWaves = 8;          // waves per leaf-kernel workgroup
+constexpr int kLeavesPerWave = 32;
+constexpr int kLeafPass = kLeafWaves * kLeavesPerWave;
+
+struct ExactIO {
+    int enabled;
+    int no;                               // optimality cuts in the pool at launch
+    int ostride;                          // column capacity of coefO / R
+    const double SGUFP_GBL *coefO;        // [n_slots + 2][ostride]: column j = O cut o_rows[j] (oldest
+                                          // first); row n_slots = 0 (absent key), row n_slots + 1 = RHS
+    double SGUFP_GBL *R;                  // [max_batch][ostride]: root folds, pending index x newest-first position
+    int32_t SGUFP_GBL *pend_slot;         // [max_batch] batch slot of pending record i
+    uint32_t SGUFP_GBL *pend_base;        // [max_batch] first leaf pass of pending record i
+    unsigned long long SGUFP_GBL *ctr;    // [4]: (pending << 32 | leaf passes), root work, leaf work
+};
+
 // Seen-path lists of the exact DDs' refinement loops (bnb_kernels.hip), per batch slot.
 struct SeenLists {
     int16_t SGUFP_GBL *paths;   // [slots][cap][Lcap]

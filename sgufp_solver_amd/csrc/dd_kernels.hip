@@ -1819,14 +1819,18 @@ struct LoopState {
 #endif
 };
 
-// one cut at a time from pool position s onwards
-__device__ __forceinline__ void cut_loop_single(const NetDev &net, DD &d, const Pool &pool, double incumbent, int s, LoopState &st) {
+// one cut at a time from pool position s onwards; efast: an exact DD leaves at the first
+// optimality cut for the cut-parallel kernels (kExactPending, exact_kernels.hip)
+__device__ __forceinline__ void cut_loop_single(const NetDev &net, DD &d, const Pool &pool, double incumbent, int s, LoopState &st,
+                                                bool efast = false) {
     const int total = pool.nf + pool.no;
+    if (efast && s >= pool.nf) { st.status = kExactPending; return; }
     for (int s0 = s; s0 < total; s0 += kWave) {
         double rv = root_fold_seq(pool, d, s0, total);
         int cnt = min(kWave, total - s0);
         for (int j = 0; j < cnt; j++) {
             const int seq = s0 + j;
+            if (efast && seq >= pool.nf) { st.status = kExactPending; return; }
             const int id = seq_id(pool, seq);
             const GBL double *row = pool.rows + (size_t)id * pool.stride;
             dd_sweep(net, d, row, lane_get(rv, j));
@@ -2140,12 +2144,12 @@ __device__ __forceinline__ bool screen_opt(const NetDev &net, DD &d, BatchView &
 
 template <int CB>
 __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const Scratch &sc, BatchView &bv, const Pool &pool,
-                                 double incumbent, LoopState &st) {
+                                 double incumbent, LoopState &st, bool efast) {
     const int total = pool.nf + pool.no;
     const int last = d.T - 1;
     bv.gbase = uni(d.noff[d.kg]);
     if (d.T < 2 || uni(d.noff[last]) + uni(d.nn[last]) - bv.gbase > (uint32_t)sc.tail_cap) {
-        cut_loop_single(net, d, pool, incumbent, 0, st);
+        cut_loop_single(net, d, pool, incumbent, 0, st, efast);
         return;
     }
     int s = 0;
@@ -2158,6 +2162,7 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
             st.stamp(6);
             if (pruned) { st.status = kPrunedOptimality; return; }
         }
+        if (!feas && efast) { st.status = kExactPending; return; }
         const int nb = min(CB, (feas ? pool.nf : total) - s);
         if (lane() < nb) bv.ids[lane()] = seq_id(pool, s + lane());
         for (int k = lane(); k < d.T; k += kWave) bv.w1[k] = ((d.nalive[k]) == 1) ? 1 : 0;
@@ -2274,7 +2279,7 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
 // Kernel 1: build + pool sweeps + finish, one wave per open node.
 template <int CB>
 __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, BatchIn in, Pool pool, BatchOut out,
-                                                double incumbent) {
+                                                double incumbent, ExactIO ex) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
     if ((int)blockIdx.x >= in.n) return;
@@ -2301,6 +2306,7 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
 #endif
     double lb = DMIN;
     uint32_t nchild = 0, n_nodes = 0, n_arcs = 0, n_merged = 0;
+    bool efast = false;
     d.T = 1; d.exact = 1;
 
     if (!in.valid[slot] || d.len > d.g || d.g > net.L || d.len > sc.Lcap) {
@@ -2330,6 +2336,8 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
         goto done;
     }
     st.stamp(0);
+    // exact DDs whose optimality phase the cut-parallel kernels can take (exact_kernels.hip)
+    efast = ex.enabled && d.exact && pool.no > 0 && d.T <= kExactMaxT && (d.T - 1) * sc.us <= kExactMaxEntries;
     if (CB > 1 && d.aligned) {
         LdsCarve cv = lds_carve(sc.Tcap, sc.Lcap, CB, sc.us);
         d.tmir = sc.tmir + (size_t)slot * sc.tmir_cap;
@@ -2354,16 +2362,31 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
         bv.sm = sc.sm + (size_t)slot * sc.Tcap * CB;
         bv.xm = sc.xm + (size_t)slot * sc.Tcap * CB;
         build_stream(d, n_merged, CB * pool.ustride);   // tmir_cap = Ncap + Acap >= Nn + Amir
-        if (d.stream) cut_loop_batched<CB>(net, d, sc, bv, pool, incumbent, st);
-        else cut_loop_single(net, d, pool, incumbent, 0, st);
+        if (d.stream) cut_loop_batched<CB>(net, d, sc, bv, pool, incumbent, st, efast);
+        else cut_loop_single(net, d, pool, incumbent, 0, st, efast);
 #if defined(SGUFP_PROF) && defined(SGUFP_PHASES)
         st.ph[6] += bv.prof[0];
         st.ph[7] += bv.prof[1];
 #endif
     } else {
-        cut_loop_single(net, d, pool, incumbent, 0, st);
+        cut_loop_single(net, d, pool, incumbent, 0, st, efast);
     }
     st.stamp(6);
+    if (st.status == kExactPending) {
+        // hand-off: the root solution's slots for k_exact_root, then one pending entry and
+        // this record's leaf passes (a single 64-bit atomic keeps the pass bases ascending
+        // with the entry index, which k_exact_leaf's item search relies on)
+        GBL int32_t *rs = sc.rslot + (size_t)slot * sc.Lcap;
+        for (int t = lane(); t < d.len; t += kWave) rs[t] = (int32_t)d.rslot[t];
+        if (lane() == 0) {
+            const uint32_t leaves = uni(d.nn[d.T - 1]);
+            const unsigned long long passes = (leaves + (uint32_t)kLeafPass - 1) / (uint32_t)kLeafPass;
+            const unsigned long long old = atomicAdd(ex.ctr, (1ull << 32) | passes);
+            const int i = (int)(old >> 32);
+            ex.pend_slot[i] = slot;
+            ex.pend_base[i] = (uint32_t)(old & 0xFFFFFFFFull);
+        }
+    }
     if (st.status == kSuccess) {
         const GBL double *lrow = st.last_cut >= 0 ? pool.rows + (size_t)st.last_cut * pool.stride : nullptr;
         if (d.exact) {
@@ -2549,6 +2572,52 @@ __global__ void __launch_bounds__(kWave) k_refine(NetDev net, Scratch sc, BatchI
 }
 
 // ------------------------------------------------------------------------------------
+// Kernel 4: end of the cut-parallel optimality phase of exact DDs (exact_kernels.hip):
+// the terminal weights are final, so applyOptimalityCut's outcome is read off them --
+// terminal state = first maximum over the alive leaves (DD.cpp:3975-3984); <= optimalLB:
+// PRUNED_BY_OPTIMALITY_CUT, else ub = it and the argmax path (getSolution) -- and the DD is
+// left as the reference's last cut (the oldest optimality cut) leaves it for k_refine.
+__global__ void __launch_bounds__(kWave) k_exact_fin(NetDev net, Scratch sc, BatchIn in, Pool pool, BatchOut out,
+                                                     ExactIO ex, double incumbent) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
+    const int i = blockIdx.x;
+    if (i >= (int)(ex.ctr[0] >> 32)) return;
+    const int slot = ex.pend_slot[i];
+    DD d;
+    dd_bind(d, smem, sc, slot);
+    load_meta_layers(d, sc, slot);
+    const int last = d.T - 1;
+    const uint32_t lo = uni(d.noff[last]), ln = uni(d.nn[last]);
+    VP best{0.0, INT_MIN};
+    for (uint32_t base = 0; base < ln; base += kWave) {
+        const uint32_t k = base + lane();
+        if (k < ln && (d.nflag[lo + k] & kAlive)) best = vp_pick(best, VP{d.tw[lo + k], prio_old((int)k)});
+    }
+    best = wave_vp(best);
+    const double term = (best.p == INT_MIN) ? DMIN : smax(DMIN, best.v);
+    const int last_cut = pool.o_order[pool.no - 1];
+    int status = kNeedsSubproblem;
+    double ub = term;
+    if (term <= incumbent) {
+        status = kPrunedOptimality;
+        ub = DMIN;
+    } else {
+        const GBL int16_t *rsol = in.sol + in.sol_off[slot];
+        const int plen = dd_solution_path(net, d, pool.rows + (size_t)last_cut * pool.stride,
+                                          out.path + (size_t)slot * sc.Lcap, rsol);
+        if (lane() == 0) out.path_len[slot] = (uint16_t)plen;
+    }
+    if (lane() == 0) {
+        out.status[slot] = status;
+        out.lb[slot] = DMIN;
+        out.ub[slot] = ub;
+        out.sweeps[slot] += (uint32_t)pool.no;
+    }
+    store_meta_layers(d, sc, slot, last_cut, status, 0, ub);
+}
+
+// ------------------------------------------------------------------------------------
 // Exclusive scan of two u32 arrays into u64 offsets (n+1 entries), one 1024-thread block.
 __global__ void __launch_bounds__(1024) k_scan2(const uint32_t *a, const uint32_t *b, int n, uint64_t *oa,
                                                uint64_t *ob) {
@@ -2578,16 +2647,25 @@ __global__ void __launch_bounds__(1024) k_scan2(const uint32_t *a, const uint32_
 // host-side launchers (called from capi.cpp)
 size_t relax_lds_bytes(int Tcap, int Lcap, int cb, int us) { return lds_carve(Tcap, Lcap, cb, us).bytes; }
 
+hipError_t launch_exact(const NetDev &net, const Scratch &sc, const ExactIO &ex, double incumbent, int cus,
+                        hipStream_t st);
+
 hipError_t launch_relax(const NetDev &net, const Scratch &sc, const BatchIn &in, const Pool &pool,
-                        const BatchOut &out, double incumbent, int cb, hipStream_t st) {
+                        const BatchOut &out, double incumbent, int cb, const ExactIO &ex, int cus, hipStream_t st) {
     if (in.n <= 0) return hipSuccess;
     size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, cb, sc.us);
     switch (cb) {
-        case 4: hipLaunchKernelGGL(k_relax<4>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent); break;
-        case 8: hipLaunchKernelGGL(k_relax<8>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent); break;
-        case 16: hipLaunchKernelGGL(k_relax<16>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent); break;
-        default: hipLaunchKernelGGL(k_relax<1>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent); break;
+        case 4: hipLaunchKernelGGL(k_relax<4>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent, ex); break;
+        case 8: hipLaunchKernelGGL(k_relax<8>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent, ex); break;
+        case 16: hipLaunchKernelGGL(k_relax<16>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent, ex); break;
+        default: hipLaunchKernelGGL(k_relax<1>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent, ex); break;
     }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !ex.enabled || ex.no <= 0) return e;
+    // exact DDs handed off by k_relax: root folds, terminal weights, outcome
+    if ((e = launch_exact(net, sc, ex, incumbent, cus, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_exact_fin, dim3(in.n), dim3(kWave), relax_lds_bytes(sc.Tcap, sc.Lcap, 1, sc.us), st, net, sc, in,
+                       pool, out, ex, incumbent);
     return hipGetLastError();
 }
 

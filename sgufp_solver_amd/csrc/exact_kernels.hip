@@ -1,0 +1,325 @@
+// Optimality phase of exact DDs, cut-parallel (see ExactIO in dd_device.hpp).
+//
+// An exact DD below a deep B&B record is a small tree (at 1k arcs: ~7 layers, ~6.8k nodes,
+// ~5k leaves) swept by every optimality cut of a pool that grows to tens of thousands of
+// rows.  k_relax sweeps one cut (or a batch of four) at a time with the lanes over the
+// nodes of a layer; for these records that costs ~20 us per cut and a 1 024-record B&B
+// launch lasts as long as its slowest record.  Here the lanes are the
+// cuts instead: every lane walks the same tree with its own cut's values, so there is no
+// cross-lane traffic until the very end, the coefficient of a node is one conflict-free
+// LDS read, and the records split into independent (record, leaf pass) work items that
+// persistent workgroups pull from a counter -- no record can hold a launch up.
+//
+//   k_exact_cols  new optimality rows -> the cut-minor copy coefO (row n_slots + 1 = RHS)
+//   k_exact_root  the root prefix (DD.cpp:3938-3949: RHS, then + coef per decision of the
+//                 record's solution, in order) of every (pending record, cut): lanes = cuts
+//   k_exact_leaf  per (record, pass of kLeafPass leaves): 8 waves x 32 leaves, lanes = cuts
+//                 of a 64-cut block staged in LDS; per leaf the lane keeps the running
+//                 std::min of its cuts' path values (DD.cpp:3975-3984) in a register; a
+//                 pass stops early once every leaf is <= optimalLB (the outcome no longer
+//                 changes); at the end a wave-min per leaf is the terminal weight
+//
+// Bit-exactness: every path value is the reference's fold, in its order -- the root
+// prefix left to right, then parent + coefficient layer by layer (no add for a -1
+// decision, DMIN below a dead in-arc) -- and each lane meets its cuts in pool order, so
+// its running min keeps the first of equal values like std::min.  Across lanes equal
+// minima can differ only in the sign of zero; a leaf whose minimum is zero and above
+// optimalLB (so that the value can still be the DD's maximum) is re-scanned in pool order
+// for the first cut that reaches it (first_zero).  The file is compiled with
+// -ffp-contract=off like the rest.
+#define SGUFP_MULTI_WAVE_TU 1
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "dd_device.hpp"
+#include "wave.hpp"
+
+namespace sgufp {
+
+#define EDMIN (-__DBL_MAX__)
+#define EDMAX (__DBL_MAX__)
+
+__device__ __forceinline__ int wid() { return (int)(threadIdx.x >> 6); }
+
+// Coefficient slot of state rank r at DD layer k of a record (rank_slot in dd_kernels.hip):
+// structural layer g + k - 1, coefficient layer len + k - 1 (they differ only for records
+// whose solution vector is shorter than their global layer).  -1: no slot (coefficient 0).
+__device__ __forceinline__ int slot_of(const NetDev &net, int g, int len, int aligned, int k, int r) {
+    const int ls = g + k - 1;
+    if (aligned) return net.slot_tab[ls * kMaxU + r];
+    const int u = net.layer_universe[ls];
+    if (u < 0 || r >= net.set_len[u]) return -1;
+    const int dec = net.set_val[net.set_off[u] + r];
+    if (dec < 0) return -1;
+    const int lc = len + k - 1;
+    const int j = net.arc_head[dec];
+    for (int s = net.slot_off[lc]; s < net.slot_off[lc + 1]; s++)
+        if (net.slot_head[s] == j) return s;
+    return net.n_slots;
+}
+
+// ---- k_exact_cols: columns [first, no) of coefO from the pool rows ------------------------
+__global__ void __launch_bounds__(256) k_exact_cols(const double *rows, const double *rhs, const int32_t *o_order,
+                                                    int no, int first, int stride, int n_slots, int ostride,
+                                                    double *coefO) {
+    const int j = first + (int)blockIdx.x;      // oldest-first position
+    if (j >= no) return;
+    const int row = o_order[no - 1 - j];        // o_order is newest first
+    const double *src = rows + (size_t)row * stride;
+    for (int s = threadIdx.x; s < n_slots; s += blockDim.x) coefO[(size_t)s * ostride + j] = src[s];
+    if (threadIdx.x == 0) {
+        coefO[(size_t)n_slots * ostride + j] = 0.0;
+        coefO[(size_t)(n_slots + 1) * ostride + j] = rhs[row];
+    }
+}
+
+// ---- k_exact_root: R[i][s] = root prefix of pending record i under O cut s (newest first) --
+constexpr int kFold = 16;
+__global__ void __launch_bounds__(256) k_exact_root(NetDev net, Scratch sc, ExactIO ex) {
+    __shared__ int32_t item_s[4];
+    const int w = wid();
+    const unsigned long long packed = ex.ctr[0];
+    const int npend = (int)(packed >> 32);
+    const int nblk = (ex.no + kWave - 1) / kWave;
+    const long long total = (long long)npend * nblk;
+    const int ns = net.n_slots;
+    for (;;) {
+        if (lane() == 0) item_s[w] = (int32_t)atomicAdd(&ex.ctr[1], 1ull);
+        __builtin_amdgcn_wave_barrier();
+        const long long item = (long long)uni(item_s[w]);
+        __builtin_amdgcn_wave_barrier();
+        if (item >= total) break;
+        const int i = (int)(item / nblk), b = (int)(item % nblk);
+        const int slot = ex.pend_slot[i];
+        const int len = sc.meta[(size_t)slot * 8 + 1];
+        const GBL int32_t *rs = sc.rslot + (size_t)slot * sc.Lcap;
+        const int s = b * kWave + lane();
+        const bool vc = s < ex.no;
+        const int oidx = vc ? ex.no - 1 - s : 0;
+        double v = ex.coefO[(size_t)(ns + 1) * ex.ostride + oidx];
+        for (int t0 = 0; t0 < len; t0 += kFold) {
+            double x[kFold];
+            bool ok[kFold];
+#pragma unroll
+            for (int j = 0; j < kFold; j++) {
+                const int t = t0 + j;
+                const int sl = t < len ? uni(rs[t]) : -1;
+                ok[j] = sl >= 0;
+                x[j] = ex.coefO[(size_t)(ok[j] ? sl : ns) * ex.ostride + oidx];
+            }
+            sched_fence();
+#pragma unroll
+            for (int j = 0; j < kFold; j++)
+                if (ok[j]) v = v + x[j];
+        }
+        if (vc) ex.R[(size_t)i * ex.ostride + s] = v;
+    }
+}
+
+// ---- k_exact_leaf ------------------------------------------------------------------------
+// Per-wave tables of one pass: for leaf j of the wave and DD layer k (1 .. T-1) the rank of
+// the decision into its ancestor at layer k (bits 0-5) and that node's in-arc alive flag
+// (bit 7); dv[j] = the first layer where leaf j's ancestors differ from leaf j-1's.
+struct LeafWave {
+    uint8_t info[kLeavesPerWave][kExactMaxT];
+    uint8_t dv[kLeavesPerWave];
+};
+
+struct LeafShared {
+    double C[kExactMaxEntries][kWave];   // staged coefficients of a 64-cut block, row = (k-1)*us + r
+    int32_t stab[kExactMaxEntries];      // their slots (-1: no coefficient)
+    LeafWave lw[kLeafWaves];
+    double vb[kLeafWaves][kExactMaxT][kWave];   // ancestor values of the current leaf, per wave
+    int32_t item, flags[kLeafWaves];
+};
+
+// running min of a lane's cuts meeting a path value (std::min(w, v): keeps w on ties)
+__device__ __forceinline__ double rmin(double w, double v) { return (v < w) ? v : w; }
+
+// ancestors of leaf j (wave-local) from layer dj down to the leaf's parent, values in vb;
+// returns the parent value
+__device__ __forceinline__ double walk_down(LeafShared &S, int w, int j, int dj, int T, int us, double root) {
+    double prev = (dj <= 1) ? root : S.vb[w][dj - 1][lane()];
+    for (int k = dj; k < T - 1; k++) {
+        const uint32_t b = uni((uint32_t)S.lw[w].info[j][k]);
+        const uint32_t r = b & 63u;
+        const double x = !(b & 128u) ? EDMIN : (r ? prev + S.C[(k - 1) * us + r][lane()] : prev);
+        S.vb[w][k][lane()] = x;
+        prev = x;
+    }
+    return prev;
+}
+
+// the first cut in pool order whose value at the leaf equals the leaf's minimum zero: its
+// bits (the sign std::min's sequential fold keeps).  Coefficients straight from coefO.
+__device__ double first_zero(const NetDev &net, const ExactIO &ex, LeafShared &S, int w, int j, int T, int us, int i) {
+    const int nblk = (ex.no + kWave - 1) / kWave;
+    for (int b = 0; b < nblk; b++) {
+        const int s = b * kWave + lane();
+        const bool vc = s < ex.no;
+        const int oidx = vc ? ex.no - 1 - s : 0;
+        double v = vc ? ex.R[(size_t)i * ex.ostride + s] : 1.0;
+        for (int k = 1; k < T; k++) {
+            const uint32_t bb = uni((uint32_t)S.lw[w].info[j][k]);
+            const uint32_t r = bb & 63u;
+            const int sl = S.stab[(k - 1) * us + (int)r];
+            const double c = (sl >= 0 && vc) ? ex.coefO[(size_t)sl * ex.ostride + oidx] : 0.0;
+            v = !(bb & 128u) ? EDMIN : (r ? v + c : v);
+        }
+        const uint64_t hit = __ballot(vc && v == 0.0);
+        if (hit) return lane_get(v, (int)(__ffsll((unsigned long long)hit) - 1));
+    }
+    return 0.0;
+}
+
+__global__ void __launch_bounds__(kLeafWaves * kWave) k_exact_leaf(NetDev net, Scratch sc, ExactIO ex, double incumbent) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    LeafShared &S = *(LeafShared *)smem_raw;
+    const int w = wid();
+    const int tid = (int)threadIdx.x;
+    const unsigned long long packed = ex.ctr[0];
+    const int npend = (int)(packed >> 32);
+    const uint32_t total = (uint32_t)(packed & 0xFFFFFFFFull);
+    const int nblk = (ex.no + kWave - 1) / kWave;
+    const int us = sc.us;
+    for (;;) {
+        if (tid == 0) S.item = (int32_t)atomicAdd(&ex.ctr[2], 1ull);
+        __syncthreads();
+        const uint32_t item = (uint32_t)uni(S.item);
+        __syncthreads();
+        if (item >= total) break;
+        // record of the item: the last pending record whose first pass is <= item
+        int lo = 0, hi = npend - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (ex.pend_base[mid] <= item) lo = mid;
+            else hi = mid - 1;
+        }
+        const int i = lo;
+        const int slot = ex.pend_slot[i];
+        const int pass = (int)(item - ex.pend_base[i]);
+        const GBL int32_t *meta = sc.meta + (size_t)slot * 8;
+        const int g = uni(meta[0]), len = uni(meta[1]), T = uni(meta[2]), aligned = uni(meta[4]);
+        const GBL uint32_t *lay = sc.lay + (size_t)slot * sc.Tcap * 5;
+        const uint32_t lnoff = uni(lay[T - 1]), lnn = uni(lay[sc.Tcap + T - 1]);
+        const size_t N = (size_t)slot * sc.Ncap;
+        const int E = (T - 1) * us;
+        for (int e = tid; e < E; e += kLeafWaves * kWave) {
+            const int k = e / us + 1, r = e % us;
+            S.stab[e] = r == 0 ? -1 : slot_of(net, g, len, aligned, k, r);
+        }
+        // this wave's leaves: ancestry tables and alive mask
+        const int j0 = pass * kLeafPass + w * kLeavesPerWave;
+        const int cnt = max(0, min(kLeavesPerWave, (int)lnn - j0));
+        uint32_t alive = 0;
+        {
+            const int j = lane();
+            bool al = false;
+            uint32_t anc[kExactMaxT];
+            if (j < cnt) {
+                uint32_t node = lnoff + (uint32_t)(j0 + j);
+                al = (sc.nflag[N + node] & kAlive) != 0;
+#pragma unroll
+                for (int k = kExactMaxT - 1; k >= 1; k--) {
+                    if (k < T) {
+                        const uint32_t t = sc.ntopo[N + node];
+                        const uint8_t f = sc.nflag[N + node];
+                        S.lw[w].info[j][k] = (uint8_t)(((t >> kRankShift) & 63u) | ((f & kInAlive) ? 128u : 0u));
+                        anc[k] = node;
+                        node = lay[k - 1] + (t & kParentMask);
+                    }
+                }
+            }
+            // first layer where this leaf's ancestors leave the previous leaf's
+            int dv = 1;
+#pragma unroll
+            for (int k = 1; k < kExactMaxT; k++) {
+                if (k < T - 1) {
+                    const uint32_t prev = (uint32_t)__shfl_up((int)anc[k], 1, kWave);
+                    if (j > 0 && j < cnt && prev == anc[k] && dv == k) dv = k + 1;
+                }
+            }
+            if (j < cnt) S.lw[w].dv[j] = (uint8_t)((j == 0) ? 1 : dv);
+            alive = (uint32_t)__ballot(j < cnt && al);
+        }
+        double m[kLeavesPerWave];
+#pragma unroll
+        for (int j = 0; j < kLeavesPerWave; j++) m[j] = EDMAX;
+        uint32_t done = 0;
+        __syncthreads();
+        for (int b = 0; b < nblk; b++) {
+            // stage the block's coefficients: row e = (layer, rank), lane = cut
+            for (int x = tid; x < E * kWave; x += kLeafWaves * kWave) {
+                const int e = x >> 6, l = x & (kWave - 1);
+                const int s = b * kWave + l;
+                const int sl = S.stab[e];
+                S.C[e][l] = (sl >= 0 && s < ex.no) ? ex.coefO[(size_t)sl * ex.ostride + (ex.no - 1 - s)] : 0.0;
+            }
+            __syncthreads();
+            const int s = b * kWave + lane();
+            const bool vc = s < ex.no;
+            if (cnt > 0 && (done & alive) != alive) {
+                const double root = vc ? ex.R[(size_t)i * ex.ostride + s] : 0.0;
+                double par = root;
+#pragma unroll
+                for (int j = 0; j < kLeavesPerWave; j++) {
+                    if (j < cnt) {
+                        const int dj = (int)uni((uint32_t)S.lw[w].dv[j]);
+                        if (dj < T - 1 || j == 0) par = walk_down(S, w, j, dj, T, us, root);
+                        if (((alive & ~done) >> j) & 1u) {
+                            const uint32_t bb = uni((uint32_t)S.lw[w].info[j][T - 1]);
+                            const uint32_t r = bb & 63u;
+                            const double v = !(bb & 128u) ? EDMIN : (r ? par + S.C[(T - 2) * us + r][lane()] : par);
+                            if (vc) m[j] = rmin(m[j], v);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < kLeavesPerWave; j++)
+                    if (((alive & ~done) >> j) & 1u)
+                        if (__ballot(vc && m[j] <= incumbent)) done |= 1u << j;
+            }
+            if (lane() == 0) S.flags[w] = ((done & alive) == alive) ? 1 : 0;
+            __syncthreads();
+            int all = 1;
+#pragma unroll
+            for (int q = 0; q < kLeafWaves; q++) all &= S.flags[q];
+            __syncthreads();
+            if (all) break;
+        }
+        // terminal weights: min over the lanes
+#pragma unroll
+        for (int j = 0; j < kLeavesPerWave; j++) {
+            if ((alive >> j) & 1u) {
+                double v = lane_reduce<1>(m[j], [](double a, double b) { return rmin(a, b); });
+                if (v == 0.0 && v > incumbent && !((done >> j) & 1u)) v = first_zero(net, ex, S, w, j, T, us, i);
+                if (lane() == 0) sc.tw[N + lnoff + (uint32_t)(j0 + j)] = v;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+size_t exact_leaf_lds_bytes() { return sizeof(LeafShared); }
+
+hipError_t launch_exact_cols(const double *rows, const double *rhs, const int32_t *o_order, int no, int first,
+                             int stride, int n_slots, int ostride, double *coefO, hipStream_t st) {
+    if (no <= first) return hipSuccess;
+    hipLaunchKernelGGL(k_exact_cols, dim3(no - first), dim3(256), 0, st, rows, rhs, o_order, no, first, stride, n_slots,
+                       ostride, coefO);
+    return hipGetLastError();
+}
+
+// the pending records' root folds and terminal weights; k_exact_fin (dd_kernels.hip) ends them
+hipError_t launch_exact(const NetDev &net, const Scratch &sc, const ExactIO &ex, double incumbent, int cus,
+                        hipStream_t st) {
+    hipLaunchKernelGGL(k_exact_root, dim3(4 * cus), dim3(256), 0, st, net, sc, ex);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_exact_leaf, dim3(2 * cus), dim3(kLeafWaves * kWave), sizeof(LeafShared), st, net, sc, ex,
+                       incumbent);
+    return hipGetLastError();
+}
+
+}  // namespace sgufp

@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Where the device B&B's round time goes (GPU; profiling library for per-wave ticks).
+
+    SGUFP_LIB_PATH=sgufp_solver_amd/lib_prof/libsgufp_hip.so python tools/bnb_tail_diag.py --config C3 --seconds 20
+
+Runs the seeded search (restricted-DD heuristic of --width on the root, as bench.py's
+bnb_seeded leg) and, per round: wall time, k_relax launch time (hipEvents), the popped
+records' wave times (wall_clock64 ticks, 100 MHz) by status, cuts swept, and how full the
+launch kept the GPU (sum of wave times / (launch time x resident wave slots)).
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--width", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--seconds", type=float, default=20.0)
+    ap.add_argument("--round-seconds", type=float, default=5.0)
+    ap.add_argument("--slots", type=int, default=2048, help="resident k_relax waves (2 per SIMD x 1024 SIMDs)")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    from sgufp_solver_amd import engine as E
+    from sgufp_solver_amd import instance
+    from sgufp_solver_amd.pools import DOUBLE_MAX, DOUBLE_MIN, NodeRecord
+    from sgufp_solver_amd.restricted import RestrictedExplorer
+    inst = instance.generate(instance.CONFIGS[a.config], a.seed)
+    inst.lb[:] = 0
+    d = tempfile.mkdtemp()
+    net = os.path.join(d, "net.txt")
+    inst.write(net)
+    eng = E.Engine(net, 0, a.batch)
+    eng.set_timing(True)
+    eng.bnb_set_trace(True)
+    root = NodeRecord(0, DOUBLE_MIN, DOUBLE_MAX, [], [])
+    z = RestrictedExplorer(eng, a.width).incumbent([root], DOUBLE_MIN) if a.width else DOUBLE_MIN
+    eng.frontier_clear()
+    eng.frontier_push([root])
+    t0 = time.perf_counter()
+    rows = []
+    diving = True
+    while time.perf_counter() - t0 < a.seconds and eng.frontier_size():
+        eng.bnb_set_limits(0, a.round_seconds)
+        b = 64 if diving else a.batch
+        tr = time.perf_counter()
+        z, st = eng.bnb_step(z, b)
+        wall = time.perf_counter() - tr
+        if st.exact:
+            diving = False
+        n = int(st.popped)
+        waves = eng.bnb_trace(3)
+        popped = eng.bnb_trace(0)
+        ticks = np.array([w[3] for w in waves])
+        sw = np.array([w[2] for w in waves])
+        stt = np.array([p[1] for p in popped])
+        ms = ticks / 1e5
+        launch = float(st.ms_relax)
+        fill = float(ms.sum() / max(1e-9, launch * min(a.slots, max(n, 1)))) if launch else 0.0
+        by = {}
+        for s in np.unique(stt):
+            m = stt == s
+            by[int(s)] = {"n": int(m.sum()), "wave_ms_mean": round(float(ms[m].mean()), 3),
+                          "wave_ms_max": round(float(ms[m].max()), 3), "sweeps_mean": round(float(sw[m].mean()), 1)}
+        rows.append({"round": len(rows), "popped": n, "wall_ms": round(wall * 1e3, 2), "k_relax_ms": round(launch, 2),
+                     "wave_ms_max": round(float(ms.max()), 3) if n else 0.0,
+                     "wave_ms_mean": round(float(ms.mean()), 3) if n else 0.0,
+                     "fill": round(fill, 3), "subproblems": int(st.subproblems), "iters": int(st.refine_iters),
+                     "pool": eng.cuts_count(0) + eng.cuts_count(1), "by_status": by})
+        print(json.dumps(rows[-1]), flush=True)
+    tot = {k: sum(r[k] for r in rows) for k in ("wall_ms", "k_relax_ms", "popped", "subproblems")}
+    tot["relaxations_per_s"] = round(tot["popped"] / (tot["wall_ms"] / 1e3), 1)
+    tot["k_relax_share"] = round(tot["k_relax_ms"] / tot["wall_ms"], 3)
+    print(json.dumps({"total": tot}))
+    if a.out:
+        with open(a.out, "w") as fh:
+            json.dump({"rounds": rows, "total": tot}, fh)
+
+
+if __name__ == "__main__":
+    main()
