@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--c5-nodes", type=int, default=4096,
                     help="config-5 leg (5k arcs, 512 scenarios): open nodes relaxed per step (0: skip)")
     ap.add_argument("--c5-paths", type=int, default=4, help="config-5 leg: subproblem paths x 512 scenarios")
+    ap.add_argument("--c5-parity", type=int, default=256,
+                    help="config-5 leg: records of the timed step checked against the reference (0: none)")
     ap.add_argument("--mode", choices=["relax", "bnb"], default="relax",
                     help="relax: the headline batch relaxation; bnb: the device B&B (config C3) for --bnb-seconds")
     ap.add_argument("--bnb-config", default="C3")
@@ -665,11 +667,29 @@ def config5_leg(args, work):
     wall = time.perf_counter() - t0
     st, ex, lb, ub, nc = eng.results_arrays()
     dn, da, dl, sw = eng.stats()
+    parity = None
+    if not args.no_parity and args.c5_parity > 0:
+        # the last timed step's first records against the reference's RelaxedDDNew
+        k = min(args.c5_parity, fr.n)
+        got = eng._collect()[:k]
+        sample = E.batch_slice(fr, np.arange(k))
+        nodes, cuts, outp = (os.path.join(work, f) for f in ("c5_nodes.txt", "c5_cuts.txt", "c5_ref.txt"))
+        pools.write_nodes(nodes, E.batch_to_records(sample))
+        pools.write_pool(cuts, pool)
+        ref = os.path.join(ROOT, "oracle", "_ref", "ref_dd")
+        if os.path.exists(ref):
+            r = subprocess.run([ref, "relaxp", net, cuts, nodes, inc.hex(), "16", outp], capture_output=True, text=True,
+                               timeout=900)
+            if r.returncode == 0:
+                bad, msgs = compare_results(got, pools.read_results(outp))
+                parity = {"checked": k, "mismatches": bad, "bit_exact": bad == 0, "first_mismatches": msgs,
+                          "against": "oracle/_ref/ref_dd relaxp (the reference's RelaxedDDNew), same records, pool "
+                                     "and incumbent", "ref_seconds": json.loads(r.stdout.strip().splitlines()[-1])["seconds"]}
     out = {"workload": f"C5: {cfg.n_arcs}-arc layered network, {inst.scenarios} scenarios, {args.n_feas}F+{args.n_opt}O "
                        f"pool, BFS frontier of {fr.n} open nodes", "instance_seed": args.seed, "incumbent": inc,
            "relaxations_per_s": round(fr.n * steps / wall, 2), "k_relax_ms": round(float(np.mean(ms)), 4),
            "status_counts": {str(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
-           "avg_dd_nodes": float(np.mean(dn)), "avg_sweeps": float(np.mean(sw))}
+           "avg_dd_nodes": float(np.mean(dn)), "avg_sweeps": float(np.mean(sw)), "parity": parity}
     if args.c5_paths > 0:
         _, la, _ = E.probe_network(net)
         rng = np.random.default_rng(args.seed + 7)

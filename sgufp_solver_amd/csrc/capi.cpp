@@ -1,5 +1,7 @@
 // C ABI of libsgufp_hip.so (declared in include/sgufp_hip.h): context, device
 // memory, cut-pool densification, batch staging and result retrieval.
+#include <cstdio>
+
 #include "ctx.hpp"
 #include <algorithm>
 #include <cstdlib>
@@ -102,6 +104,7 @@ bool sgufp_ctx::init() {
     nscreen = cb;
     if (const char *e = getenv("SGUFP_SCREEN")) nscreen = std::max(0, atoi(e));
     if (const char *e = getenv("SGUFP_EXACT_FAST")) exact_fast = atoi(e) != 0;
+    if (const char *e = getenv("SGUFP_EXACT_SCREEN")) exact_screen = std::max(0, std::min(kExactScreen, atoi(e)));
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -294,10 +297,22 @@ bool sgufp_ctx::exact_prepare() {
         return false;
     if (o_built < no) {
         if (!hip_ok(launch_exact_cols(d_rows, d_rhs, d_oorder, no, o_built, net.n_slots + 1, net.n_slots, ocap, d_coefO,
-                                      stream), "k_exact_cols"))
+                                      1, stream), "k_exact_cols"))
             return false;
         o_built = no;
     }
+    // screening columns: the strongest optimality cuts (push_orders' o_rank), rebuilt per launch
+    ex.nsc = std::min(no, exact_screen);
+    if (ex.nsc > 0) {
+        if (!d_coefS && (!alloc(d_coefS, rows_c * kExactScreen, "exact screen") ||
+                         !alloc(d_RS, (size_t)max_batch * kExactScreen, "exact screen")))
+            return false;
+        if (!hip_ok(launch_exact_cols(d_rows, d_rhs, d_orank, ex.nsc, 0, net.n_slots + 1, net.n_slots, kExactScreen,
+                                      d_coefS, 0, stream), "k_exact_cols"))
+            return false;
+    }
+    ex.coefS = d_coefS;
+    ex.RS = d_RS;
     if (!hip_ok(hipMemsetAsync(d_ectr, 0, 4 * sizeof(unsigned long long), stream), "memset")) return false;
     ex.ostride = ocap;
     ex.coefO = d_coefO;
@@ -323,6 +338,18 @@ bool sgufp_ctx::relax_current(double optimal_lb) {
         if (!download(&tot[0], d_coff + in.n, 1) || !download(&tot[1], d_soff + in.n, 1)) return false;
     }
     if (!sync()) return false;
+    static const bool estats = [] {
+        const char *e = std::getenv("SGUFP_EXACT_STATS");
+        return e && e[0] == '1';
+    }();
+    if (estats && ex.enabled) {
+        unsigned long long c[4];
+        if (download(c, d_ectr, 4) && sync())
+            std::fprintf(stderr, "[exact] pending %llu passes %llu blocks swept %llu of %llu (no %d, screen %d)\n",
+                         c[0] >> 32, c[0] & 0xFFFFFFFFull, c[3],
+                         (c[0] & 0xFFFFFFFFull) * (unsigned long long)((ex.no + 63) / 64 + (ex.nsc + 63) / 64), ex.no,
+                         ex.nsc);
+    }
     total_children = (int64_t)tot[0];
     total_csol = (int64_t)tot[1];
     if (!grow_children((size_t)tot[0], (size_t)tot[1])) return false;

@@ -29,7 +29,7 @@ hipError_t launch_relax(const NetDev &, const Scratch &, const BatchIn &, const 
                         const ExactIO &, int, hipStream_t);
 // exact_kernels.hip
 hipError_t launch_exact_cols(const double *rows, const double *rhs, const int32_t *o_order, int no, int first,
-                             int stride, int n_slots, int ostride, double *coefO, hipStream_t st);
+                             int stride, int n_slots, int ostride, double *coefO, int reverse, hipStream_t st);
 hipError_t launch_scan(const uint32_t *, const uint32_t *, int, uint64_t *, uint64_t *, hipStream_t);
 hipError_t launch_emit(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &,
                        const ChildOut &, hipStream_t);
@@ -209,7 +209,8 @@ struct sgufp_ctx {
     bool exact_fast = true;
     int cus = 256;                            // compute units (persistent grids)
     ExactIO ex{};
-    double *d_coefO = nullptr, *d_R = nullptr;
+    double *d_coefO = nullptr, *d_R = nullptr, *d_coefS = nullptr, *d_RS = nullptr;
+    int exact_screen = 0;                     // screening columns (SGUFP_EXACT_SCREEN; measured no gain)
     int ocap = 0, o_built = 0;                // columns of coefO allocated / filled
     int32_t *d_pslot = nullptr;
     uint32_t *d_pbase = nullptr;

@@ -194,7 +194,14 @@ struct ExactIO {
     int32_t SGUFP_GBL *pend_slot;         // [max_batch] batch slot of pending record i
     uint32_t SGUFP_GBL *pend_base;        // [max_batch] first leaf pass of pending record i
     unsigned long long SGUFP_GBL *ctr;    // [4]: (pending << 32 | leaf passes), root work, leaf work
+    // screening columns swept first (any order gives the same terminal minima; these -- the
+    // strongest O cuts by their node-independent bound, Pool::o_rank -- end pruned records
+    // early): nsc of them, kExactScreen columns allocated
+    int nsc;
+    const double SGUFP_GBL *coefS;        // [n_slots + 2][kExactScreen]
+    double SGUFP_GBL *RS;                 // [max_batch][kExactScreen]
 };
+constexpr int kExactScreen = 256;
 
 // Seen-path lists of the exact DDs' refinement loops (bnb_kernels.hip), per batch slot.
 struct SeenLists {

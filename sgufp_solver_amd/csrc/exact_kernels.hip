@@ -60,12 +60,13 @@ __device__ __forceinline__ int slot_of(const NetDev &net, int g, int len, int al
 }
 
 // ---- k_exact_cols: columns [first, no) of coefO from the pool rows ------------------------
+// (reverse = 1: column j = o_order[no - 1 - j], o_order newest first; 0: column j = o_order[j])
 __global__ void __launch_bounds__(256) k_exact_cols(const double *rows, const double *rhs, const int32_t *o_order,
                                                     int no, int first, int stride, int n_slots, int ostride,
-                                                    double *coefO) {
-    const int j = first + (int)blockIdx.x;      // oldest-first position
+                                                    double *coefO, int reverse) {
+    const int j = first + (int)blockIdx.x;
     if (j >= no) return;
-    const int row = o_order[no - 1 - j];        // o_order is newest first
+    const int row = reverse ? o_order[no - 1 - j] : o_order[j];
     const double *src = rows + (size_t)row * stride;
     for (int s = threadIdx.x; s < n_slots; s += blockDim.x) coefO[(size_t)s * ostride + j] = src[s];
     if (threadIdx.x == 0) {
@@ -81,7 +82,8 @@ __global__ void __launch_bounds__(256) k_exact_root(NetDev net, Scratch sc, Exac
     const int w = wid();
     const unsigned long long packed = ex.ctr[0];
     const int npend = (int)(packed >> 32);
-    const int nblk = (ex.no + kWave - 1) / kWave;
+    const int nbs = (ex.nsc + kWave - 1) / kWave;              // screening blocks
+    const int nblk = nbs + (ex.no + kWave - 1) / kWave;        // + pool blocks
     const long long total = (long long)npend * nblk;
     const int ns = net.n_slots;
     for (;;) {
@@ -90,14 +92,18 @@ __global__ void __launch_bounds__(256) k_exact_root(NetDev net, Scratch sc, Exac
         const long long item = (long long)uni(item_s[w]);
         __builtin_amdgcn_wave_barrier();
         if (item >= total) break;
-        const int i = (int)(item / nblk), b = (int)(item % nblk);
+        const int i = (int)(item / nblk), bb = (int)(item % nblk);
         const int slot = ex.pend_slot[i];
         const int len = sc.meta[(size_t)slot * 8 + 1];
         const GBL int32_t *rs = sc.rslot + (size_t)slot * sc.Lcap;
+        const bool scr = bb < nbs;
+        const int b = scr ? bb : bb - nbs;
         const int s = b * kWave + lane();
-        const bool vc = s < ex.no;
-        const int oidx = vc ? ex.no - 1 - s : 0;
-        double v = ex.coefO[(size_t)(ns + 1) * ex.ostride + oidx];
+        const bool vc = s < (scr ? ex.nsc : ex.no);
+        const int col = vc ? (scr ? s : ex.no - 1 - s) : 0;
+        const GBL double *cm = scr ? ex.coefS : ex.coefO;
+        const size_t cs = scr ? (size_t)kExactScreen : (size_t)ex.ostride;
+        double v = cm[(size_t)(ns + 1) * cs + col];
         for (int t0 = 0; t0 < len; t0 += kFold) {
             double x[kFold];
             bool ok[kFold];
@@ -106,14 +112,17 @@ __global__ void __launch_bounds__(256) k_exact_root(NetDev net, Scratch sc, Exac
                 const int t = t0 + j;
                 const int sl = t < len ? uni(rs[t]) : -1;
                 ok[j] = sl >= 0;
-                x[j] = ex.coefO[(size_t)(ok[j] ? sl : ns) * ex.ostride + oidx];
+                x[j] = cm[(size_t)(ok[j] ? sl : ns) * cs + col];
             }
             sched_fence();
 #pragma unroll
             for (int j = 0; j < kFold; j++)
                 if (ok[j]) v = v + x[j];
         }
-        if (vc) ex.R[(size_t)i * ex.ostride + s] = v;
+        if (vc) {
+            if (scr) ex.RS[(size_t)i * kExactScreen + s] = v;
+            else ex.R[(size_t)i * ex.ostride + s] = v;
+        }
     }
 }
 
@@ -152,7 +161,8 @@ __device__ __forceinline__ double walk_down(LeafShared &S, int w, int j, int dj,
 }
 
 // the first cut in pool order whose value at the leaf equals the leaf's minimum zero: its
-// bits (the sign std::min's sequential fold keeps).  Coefficients straight from coefO.
+// bits (the sign std::min's sequential fold keeps; the screening columns repeat pool cuts,
+// so they add no value of their own).  Coefficients straight from coefO.
 __device__ double first_zero(const NetDev &net, const ExactIO &ex, LeafShared &S, int w, int j, int T, int us, int i) {
     const int nblk = (ex.no + kWave - 1) / kWave;
     for (int b = 0; b < nblk; b++) {
@@ -181,7 +191,8 @@ __global__ void __launch_bounds__(kLeafWaves * kWave) k_exact_leaf(NetDev net, S
     const unsigned long long packed = ex.ctr[0];
     const int npend = (int)(packed >> 32);
     const uint32_t total = (uint32_t)(packed & 0xFFFFFFFFull);
-    const int nblk = (ex.no + kWave - 1) / kWave;
+    const int nbs = (ex.nsc + kWave - 1) / kWave;              // screening blocks first
+    const int nblk = nbs + (ex.no + kWave - 1) / kWave;
     const int us = sc.us;
     for (;;) {
         if (tid == 0) S.item = (int32_t)atomicAdd(&ex.ctr[2], 1ull);
@@ -243,42 +254,68 @@ __global__ void __launch_bounds__(kLeafWaves * kWave) k_exact_leaf(NetDev net, S
             if (j < cnt) S.lw[w].dv[j] = (uint8_t)((j == 0) ? 1 : dv);
             alive = (uint32_t)__ballot(j < cnt && al);
         }
+        __syncthreads();
+        // per leaf, in scalar registers for the whole pass: 16 bits = the LDS row of its
+        // last-layer coefficient (bits 0-6; kRowNoAdd: a -1 decision, kRowDead: in-arc dead) |
+        // dv << 8 (the first layer to recompute for it)
+        // (lane j holds leaf j's word; the leaf loop reads it with v_readlane)
+        constexpr uint32_t kRowNoAdd = 127u, kRowDead = 126u;
+        uint32_t lp = 0;
+        if (lane() < kLeavesPerWave) {
+            const uint32_t b = S.lw[w].info[lane()][T - 1];
+            const uint32_t r = b & 63u;
+            const uint32_t row = !(b & 128u) ? kRowDead : (r ? (uint32_t)((T - 2) * us) + r : kRowNoAdd);
+            lp = row | (uint32_t)S.lw[w].dv[lane()] << 8;
+        }
         double m[kLeavesPerWave];
 #pragma unroll
         for (int j = 0; j < kLeavesPerWave; j++) m[j] = EDMAX;
         uint32_t done = 0;
-        __syncthreads();
-        for (int b = 0; b < nblk; b++) {
+        int nb_done = 0;
+        for (int bb = 0; bb < nblk; bb++) {
+            nb_done = bb + 1;
+            const bool scr = bb < nbs;
+            const int b = scr ? bb : bb - nbs;
+            const int ncut = scr ? ex.nsc : ex.no;
+            const GBL double *cm = scr ? ex.coefS : ex.coefO;
+            const size_t cs = scr ? (size_t)kExactScreen : (size_t)ex.ostride;
             // stage the block's coefficients: row e = (layer, rank), lane = cut
             for (int x = tid; x < E * kWave; x += kLeafWaves * kWave) {
                 const int e = x >> 6, l = x & (kWave - 1);
                 const int s = b * kWave + l;
                 const int sl = S.stab[e];
-                S.C[e][l] = (sl >= 0 && s < ex.no) ? ex.coefO[(size_t)sl * ex.ostride + (ex.no - 1 - s)] : 0.0;
+                S.C[e][l] = (sl >= 0 && s < ncut) ? cm[(size_t)sl * cs + (scr ? s : ncut - 1 - s)] : 0.0;
             }
             __syncthreads();
             const int s = b * kWave + lane();
-            const bool vc = s < ex.no;
+            const bool vc = s < ncut;
             if (cnt > 0 && (done & alive) != alive) {
-                const double root = vc ? ex.R[(size_t)i * ex.ostride + s] : 0.0;
+                const double root = vc ? (scr ? ex.RS[(size_t)i * kExactScreen + s] : ex.R[(size_t)i * ex.ostride + s]) : 0.0;
+                const uint32_t open = alive & ~done;
                 double par = root;
 #pragma unroll
                 for (int j = 0; j < kLeavesPerWave; j++) {
                     if (j < cnt) {
-                        const int dj = (int)uni((uint32_t)S.lw[w].dv[j]);
+                        const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)lp, j);
+                        const int dj = (int)(x >> 8);
                         if (dj < T - 1 || j == 0) par = walk_down(S, w, j, dj, T, us, root);
-                        if (((alive & ~done) >> j) & 1u) {
-                            const uint32_t bb = uni((uint32_t)S.lw[w].info[j][T - 1]);
-                            const uint32_t r = bb & 63u;
-                            const double v = !(bb & 128u) ? EDMIN : (r ? par + S.C[(T - 2) * us + r][lane()] : par);
+                        if ((open >> j) & 1u) {
+                            const uint32_t row = x & 0x7Fu;
+                            double v;
+                            if (row == kRowDead) v = EDMIN;
+                            else if (row == kRowNoAdd) v = par;
+                            else v = par + S.C[row][lane()];
                             if (vc) m[j] = rmin(m[j], v);
                         }
                     }
                 }
+                // every fourth block (and the last): leaves some lane already took to <= optimalLB
+                if ((bb & 3) == 3 || bb == nblk - 1) {
 #pragma unroll
-                for (int j = 0; j < kLeavesPerWave; j++)
-                    if (((alive & ~done) >> j) & 1u)
-                        if (__ballot(vc && m[j] <= incumbent)) done |= 1u << j;
+                    for (int j = 0; j < kLeavesPerWave; j++)
+                        if ((open >> j) & 1u)
+                            if (__ballot(vc && m[j] <= incumbent)) done |= 1u << j;
+                }
             }
             if (lane() == 0) S.flags[w] = ((done & alive) == alive) ? 1 : 0;
             __syncthreads();
@@ -288,6 +325,7 @@ __global__ void __launch_bounds__(kLeafWaves * kWave) k_exact_leaf(NetDev net, S
             __syncthreads();
             if (all) break;
         }
+        if (tid == 0) atomicAdd(&ex.ctr[3], (unsigned long long)nb_done);   // diagnostics: cut blocks swept
         // terminal weights: min over the lanes
 #pragma unroll
         for (int j = 0; j < kLeavesPerWave; j++) {
@@ -304,10 +342,10 @@ __global__ void __launch_bounds__(kLeafWaves * kWave) k_exact_leaf(NetDev net, S
 size_t exact_leaf_lds_bytes() { return sizeof(LeafShared); }
 
 hipError_t launch_exact_cols(const double *rows, const double *rhs, const int32_t *o_order, int no, int first,
-                             int stride, int n_slots, int ostride, double *coefO, hipStream_t st) {
+                             int stride, int n_slots, int ostride, double *coefO, int reverse, hipStream_t st) {
     if (no <= first) return hipSuccess;
     hipLaunchKernelGGL(k_exact_cols, dim3(no - first), dim3(256), 0, st, rows, rhs, o_order, no, first, stride, n_slots,
-                       ostride, coefO);
+                       ostride, coefO, reverse);
     return hipGetLastError();
 }
 

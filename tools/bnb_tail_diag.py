@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=20.0)
     ap.add_argument("--round-seconds", type=float, default=5.0)
     ap.add_argument("--slots", type=int, default=2048, help="resident k_relax waves (2 per SIMD x 1024 SIMDs)")
+    ap.add_argument("--round-iters", type=int, default=0)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     from sgufp_solver_amd import engine as E
@@ -50,9 +51,11 @@ def main():
     eng.frontier_push([root])
     t0 = time.perf_counter()
     rows = []
+    seen_paths = {}
+    dup = 0
     diving = True
     while time.perf_counter() - t0 < a.seconds and eng.frontier_size():
-        eng.bnb_set_limits(0, a.round_seconds)
+        eng.bnb_set_limits(a.round_iters, a.round_seconds)
         b = 64 if diving else a.batch
         tr = time.perf_counter()
         z, st = eng.bnb_step(z, b)
@@ -62,7 +65,12 @@ def main():
         n = int(st.popped)
         waves = eng.bnb_trace(3)
         popped = eng.bnb_trace(0)
+        for sub in eng.bnb_trace(1):
+            key = hash(tuple(sub[4]))
+            dup += 1 if key in seen_paths else 0
+            seen_paths[key] = 1
         ticks = np.array([w[3] for w in waves])
+        redo = np.array([w[1] for w in waves])
         sw = np.array([w[2] for w in waves])
         stt = np.array([p[1] for p in popped])
         ms = ticks / 1e5
@@ -72,7 +80,8 @@ def main():
         for s in np.unique(stt):
             m = stt == s
             by[int(s)] = {"n": int(m.sum()), "wave_ms_mean": round(float(ms[m].mean()), 3),
-                          "wave_ms_max": round(float(ms[m].max()), 3), "sweeps_mean": round(float(sw[m].mean()), 1)}
+                          "wave_ms_max": round(float(ms[m].max()), 3), "sweeps_mean": round(float(sw[m].mean()), 1),
+                          "redo_mean": round(float(redo[m].mean()), 2), "redo_frac": round(float((redo[m] > 0).mean()), 3)}
         rows.append({"round": len(rows), "popped": n, "wall_ms": round(wall * 1e3, 2), "k_relax_ms": round(launch, 2),
                      "wave_ms_max": round(float(ms.max()), 3) if n else 0.0,
                      "wave_ms_mean": round(float(ms.mean()), 3) if n else 0.0,
@@ -82,6 +91,8 @@ def main():
     tot = {k: sum(r[k] for r in rows) for k in ("wall_ms", "k_relax_ms", "popped", "subproblems")}
     tot["relaxations_per_s"] = round(tot["popped"] / (tot["wall_ms"] / 1e3), 1)
     tot["k_relax_share"] = round(tot["k_relax_ms"] / tot["wall_ms"], 3)
+    tot["duplicate_subproblem_paths"] = dup
+    tot["round_iters"] = a.round_iters
     print(json.dumps({"total": tot}))
     if a.out:
         with open(a.out, "w") as fh:
