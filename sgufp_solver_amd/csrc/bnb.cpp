@@ -675,7 +675,7 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
                                                 ctx->d_lrowub, ctx->d_rcuts, ctx->d_rfeas, ctx->stream),
                              "k_append_cuts") ||
                 !ctx->hip_ok(launch_refine(ctx->nd, ctx->sc, ctx->batch(), ctx->pool(), o, ctx->d_lact, ctx->d_rcuts,
-                                           ctx->d_rfeas, nf, z, ctx->stream), "k_refine"))
+                                           ctx->d_rfeas, nf, z, ctx->ex, ctx->stream), "k_refine"))
                 return SGUFP_ERR_HIP;
             ctx->n_rows += nf;
             S.subproblems += nf;

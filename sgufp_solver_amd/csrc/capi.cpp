@@ -105,6 +105,7 @@ bool sgufp_ctx::init() {
     if (const char *e = getenv("SGUFP_SCREEN")) nscreen = std::max(0, atoi(e));
     if (const char *e = getenv("SGUFP_EXACT_FAST")) exact_fast = atoi(e) != 0;
     if (const char *e = getenv("SGUFP_EXACT_SCREEN")) exact_screen = std::max(0, std::min(kExactScreen, atoi(e)));
+    if (const char *e = getenv("SGUFP_EXACT_LAZY")) exact_lazy = std::max(0, atoi(e));
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -293,7 +294,7 @@ bool sgufp_ctx::exact_prepare() {
         ocap = cap;
     }
     if (!d_pslot && (!alloc(d_pslot, (size_t)max_batch, "exact pending") || !alloc(d_pbase, (size_t)max_batch, "exact pending") ||
-                     !alloc(d_ectr, 4, "exact pending")))
+                     !alloc(d_ectr, 6, "exact pending") || !alloc(d_pidx, (size_t)max_batch, "exact pending")))
         return false;
     if (o_built < no) {
         if (!hip_ok(launch_exact_cols(d_rows, d_rhs, d_oorder, no, o_built, net.n_slots + 1, net.n_slots, ocap, d_coefO,
@@ -313,7 +314,11 @@ bool sgufp_ctx::exact_prepare() {
     }
     ex.coefS = d_coefS;
     ex.RS = d_RS;
-    if (!hip_ok(hipMemsetAsync(d_ectr, 0, 4 * sizeof(unsigned long long), stream), "memset")) return false;
+    if (!hip_ok(hipMemsetAsync(d_ectr, 0, 6 * sizeof(unsigned long long), stream), "memset") ||
+        !hip_ok(hipMemsetAsync(d_pidx, 0xFF, (size_t)max_batch * sizeof(int32_t), stream), "memset"))
+        return false;
+    ex.lazy = ex.nsc == 0 ? exact_lazy : 0;
+    ex.pidx = d_pidx;
     ex.ostride = ocap;
     ex.coefO = d_coefO;
     ex.R = d_R;
@@ -343,12 +348,14 @@ bool sgufp_ctx::relax_current(double optimal_lb) {
         return e && e[0] == '1';
     }();
     if (estats && ex.enabled) {
-        unsigned long long c[4];
-        if (download(c, d_ectr, 4) && sync())
-            std::fprintf(stderr, "[exact] pending %llu passes %llu blocks swept %llu of %llu (no %d, screen %d)\n",
+        unsigned long long c[6];
+        if (download(c, d_ectr, 6) && sync())
+            std::fprintf(stderr,
+                         "[exact] pending %llu passes %llu blocks swept %llu of %llu (no %d, screen %d, lazy %d: "
+                         "%llu resolves, %llu blocks)\n",
                          c[0] >> 32, c[0] & 0xFFFFFFFFull, c[3],
                          (c[0] & 0xFFFFFFFFull) * (unsigned long long)((ex.no + 63) / 64 + (ex.nsc + 63) / 64), ex.no,
-                         ex.nsc);
+                         ex.nsc, ex.lazy, c[4], c[5]);
     }
     total_children = (int64_t)tot[0];
     total_csol = (int64_t)tot[1];
@@ -959,7 +966,7 @@ int sgufp_batch_refine(sgufp_ctx *ctx, int n, const int32_t *node_idx, const uin
         !ctx->upload(ctx->d_rfeas, is_feasibility, n))
         return SGUFP_ERR_HIP;
     if (!ctx->hip_ok(launch_refine(ctx->nd, ctx->sc, ctx->batch(), ctx->pool(), ctx->out, ctx->d_rslots, ctx->d_rcuts,
-                                   ctx->d_rfeas, n, optimal_lb, ctx->stream),
+                                   ctx->d_rfeas, n, optimal_lb, ctx->ex, ctx->stream),
                      "k_refine"))
         return SGUFP_ERR_HIP;
     return ctx->sync() ? SGUFP_OK : SGUFP_ERR_HIP;

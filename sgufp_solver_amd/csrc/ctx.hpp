@@ -34,7 +34,7 @@ hipError_t launch_scan(const uint32_t *, const uint32_t *, int, uint64_t *, uint
 hipError_t launch_emit(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &,
                        const ChildOut &, hipStream_t);
 hipError_t launch_refine(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &,
-                         const int32_t *, const int32_t *, const uint8_t *, int, double, hipStream_t);
+                         const int32_t *, const int32_t *, const uint8_t *, int, double, const ExactIO &, hipStream_t);
 hipError_t launch_gather_paths(const BatchOut &, int Lcap, const int32_t *idx, const int64_t *off, int n,
                                int16_t *dst, hipStream_t);
 hipError_t launch_push_children(const ChildOut &, const BatchOut &, const int32_t *parents, const int64_t *dst_child,
@@ -215,6 +215,8 @@ struct sgufp_ctx {
     int32_t *d_pslot = nullptr;
     uint32_t *d_pbase = nullptr;
     unsigned long long *d_ectr = nullptr;
+    int32_t *d_pidx = nullptr;
+    int exact_lazy = 0;                       // ExactIO::lazy (SGUFP_EXACT_LAZY)
     bool exact_prepare();
 
     bool timing = false;

@@ -37,6 +37,7 @@ enum NodeStatus : int32_t {
 constexpr uint8_t kAlive = 1;      // node is in tree[layer] (not deleted)
 constexpr uint8_t kInAlive = 2;    // its (single, exact-layer) incoming arc is alive
 constexpr uint8_t kKill = 4;       // scheduled for deletion in the current cascade
+constexpr uint8_t kLazy = 8;       // exact DD leaf: tw is an upper bound (ExactIO::lazy), see exact_resolve
 
 // topology word: parent index inside the previous layer (22 bits) | decision rank (6 bits)
 constexpr uint32_t kParentMask = (1u << 22) - 1;
@@ -193,7 +194,15 @@ struct ExactIO {
     double SGUFP_GBL *R;                  // [max_batch][ostride]: root folds, pending index x newest-first position
     int32_t SGUFP_GBL *pend_slot;         // [max_batch] batch slot of pending record i
     uint32_t SGUFP_GBL *pend_base;        // [max_batch] first leaf pass of pending record i
-    unsigned long long SGUFP_GBL *ctr;    // [4]: (pending << 32 | leaf passes), root work, leaf work
+    unsigned long long SGUFP_GBL *ctr;    // [6]: (pending << 32 | leaf passes), root work, leaf work,
+                                          // blocks swept, lazy resolves, blocks they swept
+    // Lazy terminal weights: a leaf pass sweeps at most `lazy` cut blocks (the newest 64 x lazy
+    // O cuts); when that leaves some leaf above optimalLB the pass's leaves keep the partial
+    // minimum (an upper bound of the terminal weight) flagged kLazy, and the argmax scans
+    // (k_exact_fin, k_refine) complete a flagged leaf over the remaining blocks only when it
+    // is the maximum (exact_resolve).  0: every pass sweeps the whole pool.
+    int lazy;
+    int32_t SGUFP_GBL *pidx;              // [max_batch] batch slot -> pending index (-1: none)
     // screening columns swept first (any order gives the same terminal minima; these -- the
     // strongest O cuts by their node-independent bound, Pool::o_rank -- end pruned records
     // early): nsc of them, kExactScreen columns allocated

@@ -2385,6 +2385,7 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
             const int i = (int)(old >> 32);
             ex.pend_slot[i] = slot;
             ex.pend_base[i] = (uint32_t)(old & 0xFFFFFFFFull);
+            ex.pidx[slot] = i;
         }
     }
     if (st.status == kSuccess) {
@@ -2515,11 +2516,117 @@ __global__ void __launch_bounds__(kWave) k_emit_children(NetDev net, Scratch sc,
 }
 
 // ------------------------------------------------------------------------------------
+// Lazy terminal weights of exact DDs (ExactIO::lazy).  A flagged leaf's tw is the running
+// min over the newest 64 x lazy O cuts of the exact phase (then over any refinement cuts
+// since): an upper bound of its terminal weight.  The maximum over leaves only needs the
+// exact value of the leaf that attains it: exact_argmax takes the first maximum, completes
+// it over the remaining O cuts when it is flagged (exact_resolve), and repeats until the
+// first maximum is exact -- every other leaf's true weight is <= its bound <= that value,
+// and the ones before it are strictly below, so it is the reference's first maximum
+// (DD.cpp:3975-3984).  Flagged leaves <= optimalLB are never completed: they cannot become
+// the maximum of an unpruned DD (the incumbent only rises).
+
+// Lanes = cuts of the blocks [ex.lazy, nblk) (newest-first positions), the leaf's path
+// folded exactly as k_exact_leaf does; per lane a running min, then the wave min.  Zero
+// bits: when the result is a zero above optimalLB, the first zero of the sequential order
+// (the exact phase's cuts, newest first, then the refinement cuts tw has seen) decides.
+__device__ void exact_resolve(const NetDev &net, DD &d, const ExactIO &ex, int i, uint32_t node, double incumbent) {
+    const int T = d.T;
+    // lane k holds layer k's (rank | in-alive << 7) and coefficient slot
+    uint32_t info = 0;
+    int slot = -1;
+    {
+        uint32_t nd = node;
+        for (int k = T - 1; k >= 1; k--) {
+            const uint32_t t = d.ntopo[nd];
+            const uint32_t r = (t >> kRankShift) & 63u;
+            const uint32_t b = r | ((d.nflag[nd] & kInAlive) ? 128u : 0u);
+            if (lane() == k) {
+                info = b;
+                slot = r == 0 ? -1 : rank_slot(net, d, k, (int)r);
+            }
+            nd = uni(d.noff[k - 1]) + (t & kParentMask);
+        }
+    }
+    const int nblk = (ex.no + kWave - 1) / kWave;
+    const size_t os = (size_t)ex.ostride;
+    auto value = [&](int s) -> double {
+        const bool vc = s < ex.no;
+        const int col = vc ? ex.no - 1 - s : 0;
+        double c[kExactMaxT];
+#pragma unroll
+        for (int k = 1; k < kExactMaxT; k++) {
+            c[k] = 0.0;
+            if (k < T) {
+                const int sl = __builtin_amdgcn_readlane(slot, k);
+                if (sl >= 0 && vc) c[k] = ex.coefO[(size_t)sl * os + col];
+            }
+        }
+        double v = vc ? ex.R[(size_t)i * os + s] : 0.0;
+        sched_fence();
+#pragma unroll
+        for (int k = 1; k < kExactMaxT; k++) {
+            if (k < T) {
+                const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)info, k);
+                v = !(b & 128u) ? DMIN : ((b & 63u) ? v + c[k] : v);
+            }
+        }
+        return v;
+    };
+    double m = DMAX;
+    for (int b = ex.lazy; b < nblk; b++) {
+        const int s = b * kWave + lane();
+        const double v = value(s);
+        if (s < ex.no) m = (v < m) ? v : m;
+    }
+    m = wave_fmin(m);
+    const double t0 = d.tw[node];
+    double nv = (m < t0) ? m : t0;
+    if (nv == 0.0 && nv > incumbent) {
+        for (int b = 0; b < nblk; b++) {
+            const int s = b * kWave + lane();
+            const double v = value(s);
+            const uint64_t hit = __ballot(s < ex.no && v == 0.0);
+            if (hit) {
+                nv = lane_get(v, (int)(__ffsll((unsigned long long)hit) - 1));
+                break;
+            }
+        }
+    }
+    if (lane() == 0) {
+        d.tw[node] = nv;
+        d.nflag[node] &= (uint8_t)~kLazy;
+        atomicAdd(&ex.ctr[4], 1ull);
+        atomicAdd(&ex.ctr[5], (unsigned long long)(nblk - ex.lazy));
+    }
+    wave_mem_sync();
+}
+
+// first maximum over the alive leaves of an exact DD (vp_pick, first wins on ties), every
+// flagged leaf that comes out on top above optimalLB completed first
+__device__ VP exact_argmax(const NetDev &net, DD &d, const ExactIO &ex, int i, double incumbent) {
+    const int last = d.T - 1;
+    const uint32_t lo = uni(d.noff[last]), ln = uni(d.nn[last]);
+    for (;;) {
+        VP best{0.0, INT_MIN};
+        for (uint32_t base = 0; base < ln; base += kWave) {
+            const uint32_t k = base + lane();
+            if (k < ln && (d.nflag[lo + k] & kAlive)) best = vp_pick(best, VP{d.tw[lo + k], prio_old((int)k)});
+        }
+        best = wave_vp(best);
+        if (best.p == INT_MIN || !(best.v > incumbent) || i < 0) return best;
+        const uint32_t node = lo + (uint32_t)(-best.p - 2);
+        if (!(d.nflag[node] & kLazy)) return best;
+        exact_resolve(net, d, ex, i, node, incumbent);
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Kernel 3: apply one freshly generated cut to exact DDs kept in their slots
 // (the refinement loop of NodeExplorer.cpp:946-969).
 __global__ void __launch_bounds__(kWave) k_refine(NetDev net, Scratch sc, BatchIn in, Pool pool, BatchOut out,
                                                   const int32_t *slots, const int32_t *cut_ids,
-                                                  const uint8_t *cut_is_feas, int n, double incumbent) {
+                                                  const uint8_t *cut_is_feas, int n, double incumbent, ExactIO ex) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
     const int w = blockIdx.x;
@@ -2551,10 +2658,17 @@ __global__ void __launch_bounds__(kWave) k_refine(NetDev net, Scratch sc, BatchI
     int status = kNeedsSubproblem;
     double ub = sc.ubv[slot];
     if (lane() == 0) out.sweeps[slot] += 1u;
+    // flagged (lazy) leaves: the batch's pending index of this record (-1: none flagged)
+    const int pi = (ex.lazy > 0 && d.exact) ? ex.pidx[slot] : -1;
     if (cut_is_feas[w]) {
         if (!dd_post_feasibility(net, d, row)) status = kPrunedFeasibility;
+        else if (pi >= 0) exact_argmax(net, d, ex, pi, incumbent);   // the path below takes the first maximum
     } else {
         ub = dd_post_optimality(net, d, row, incumbent);
+        if (pi >= 0 && ub > incumbent) {
+            const VP best = exact_argmax(net, d, ex, pi, incumbent);
+            ub = (best.p == INT_MIN) ? DMIN : smax(DMIN, best.v);
+        }
         if (ub <= incumbent) status = kPrunedOptimality;
     }
     if (status == kNeedsSubproblem) {
@@ -2587,14 +2701,7 @@ __global__ void __launch_bounds__(kWave) k_exact_fin(NetDev net, Scratch sc, Bat
     DD d;
     dd_bind(d, smem, sc, slot);
     load_meta_layers(d, sc, slot);
-    const int last = d.T - 1;
-    const uint32_t lo = uni(d.noff[last]), ln = uni(d.nn[last]);
-    VP best{0.0, INT_MIN};
-    for (uint32_t base = 0; base < ln; base += kWave) {
-        const uint32_t k = base + lane();
-        if (k < ln && (d.nflag[lo + k] & kAlive)) best = vp_pick(best, VP{d.tw[lo + k], prio_old((int)k)});
-    }
-    best = wave_vp(best);
+    const VP best = exact_argmax(net, d, ex, ex.lazy > 0 ? i : -1, incumbent);
     const double term = (best.p == INT_MIN) ? DMIN : smax(DMIN, best.v);
     const int last_cut = pool.o_order[pool.no - 1];
     int status = kNeedsSubproblem;
@@ -2692,11 +2799,11 @@ bool relax_has_phases() {
 
 hipError_t launch_refine(const NetDev &net, const Scratch &sc, const BatchIn &in, const Pool &pool,
                          const BatchOut &out, const int32_t *slots, const int32_t *cut_ids,
-                         const uint8_t *cut_is_feas, int n, double incumbent, hipStream_t st) {
+                         const uint8_t *cut_is_feas, int n, double incumbent, const ExactIO &ex, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     size_t lds = relax_lds_bytes(sc.Tcap, sc.Lcap, 1, sc.us);
     hipLaunchKernelGGL(k_refine, dim3(n), dim3(kWave), lds, st, net, sc, in, pool, out, slots, cut_ids,
-                       cut_is_feas, n, incumbent);
+                       cut_is_feas, n, incumbent, ex);
     return hipGetLastError();
 }
 

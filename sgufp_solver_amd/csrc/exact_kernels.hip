@@ -272,7 +272,10 @@ __global__ void __launch_bounds__(kLeafWaves * kWave) k_exact_leaf(NetDev net, S
         for (int j = 0; j < kLeavesPerWave; j++) m[j] = EDMAX;
         uint32_t done = 0;
         int nb_done = 0;
-        for (int bb = 0; bb < nblk; bb++) {
+        bool finished = false;   // every leaf of the pass <= optimalLB
+        // lazy passes stop after ex.lazy blocks (the newest cuts); see ExactIO::lazy
+        const int nlim = (ex.lazy > 0 && nbs == 0) ? min(nblk, ex.lazy) : nblk;
+        for (int bb = 0; bb < nlim; bb++) {
             nb_done = bb + 1;
             const bool scr = bb < nbs;
             const int b = scr ? bb : bb - nbs;
@@ -310,7 +313,7 @@ __global__ void __launch_bounds__(kLeafWaves * kWave) k_exact_leaf(NetDev net, S
                     }
                 }
                 // every fourth block (and the last): leaves some lane already took to <= optimalLB
-                if ((bb & 3) == 3 || bb == nblk - 1) {
+                if ((bb & 3) == 3 || bb == nlim - 1) {
 #pragma unroll
                     for (int j = 0; j < kLeavesPerWave; j++)
                         if ((open >> j) & 1u)
@@ -323,16 +326,23 @@ __global__ void __launch_bounds__(kLeafWaves * kWave) k_exact_leaf(NetDev net, S
 #pragma unroll
             for (int q = 0; q < kLeafWaves; q++) all &= S.flags[q];
             __syncthreads();
-            if (all) break;
+            if (all) {
+                finished = true;
+                break;
+            }
         }
+        const bool lazy = !finished && nlim < nblk;
         if (tid == 0) atomicAdd(&ex.ctr[3], (unsigned long long)nb_done);   // diagnostics: cut blocks swept
         // terminal weights: min over the lanes
 #pragma unroll
         for (int j = 0; j < kLeavesPerWave; j++) {
             if ((alive >> j) & 1u) {
                 double v = lane_reduce<1>(m[j], [](double a, double b) { return rmin(a, b); });
-                if (v == 0.0 && v > incumbent && !((done >> j) & 1u)) v = first_zero(net, ex, S, w, j, T, us, i);
-                if (lane() == 0) sc.tw[N + lnoff + (uint32_t)(j0 + j)] = v;
+                if (!lazy && v == 0.0 && v > incumbent && !((done >> j) & 1u)) v = first_zero(net, ex, S, w, j, T, us, i);
+                if (lane() == 0) {
+                    sc.tw[N + lnoff + (uint32_t)(j0 + j)] = v;
+                    if (lazy) sc.nflag[N + lnoff + (uint32_t)(j0 + j)] |= kLazy;
+                }
             }
         }
         __syncthreads();
