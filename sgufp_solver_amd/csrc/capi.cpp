@@ -671,12 +671,13 @@ bool sgufp_ctx::sub_init() {
         for (int a = 0; a < m; a++) sr += std::abs((int64_t)rew[a]);
         for (size_t i = 0; i < ub.size(); i++) umax = std::max<int64_t>(umax, ub[i]);
         sn.cost_bound = 2 * (1 + 2 * sr * (umax + 1));
-        // 32-bit keys and 12-byte chain records (k_sub_scenario): no lower bound, no negative
-        // upper bound (a chain is then never infeasible up front), small rewards and ids
+        // 32-bit keys and 8-byte chain records (k_sub_scenario): no lower bound, no negative
+        // upper bound (a chain is then never infeasible up front), small rewards, ids and
+        // upper bounds (11-bit fields)
         bool any_lb = false, neg_ub = false;
         for (size_t i = 0; i < lb.size(); i++) any_lb |= lb[i] != 0;
         for (size_t i = 0; i < ub.size(); i++) neg_ub |= ub[i] < 0;
-        sn.key32 = (!any_lb && !neg_ub && sr < ((int64_t)1 << 18) && n + 2 < (1 << 11)) ? 1 : 0;
+        sn.key32 = (!any_lb && !neg_ub && sr < ((int64_t)1 << 18) && n + 2 < (1 << 11) && umax < (1 << 11)) ? 1 : 0;
         const char *ep = getenv("SGUFP_SUB_PREDS_LDS");
         sn.preds_lds = (ep && atoi(ep) == 1) ? 1 : 0;
     }

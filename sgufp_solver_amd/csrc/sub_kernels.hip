@@ -69,7 +69,12 @@ constexpr int32_t kNoPred = INT32_MAX;
 // ALLREG: every chain group of the launch sits in registers (single wave: nct_cap <= 16 x 64;
 // eight waves: <= 10 x 8 x 64): no sweep reads chain records from LDS, predecessors come from
 // the registers too
-template <typename KT, bool ALLREG = false>
+__device__ __forceinline__ int ch_t(uint64_t a);
+__device__ __forceinline__ int ch_h(uint64_t a);
+__device__ __forceinline__ int ch_R(uint64_t a);
+__device__ __forceinline__ uint64_t pack_a(int t, int h, int R);
+
+template <typename KT, bool ALLREG = false, bool PACK = false>
 struct SubLds {
     using Key = KT;
     static constexpr bool kAllReg = ALLREG;
@@ -78,24 +83,66 @@ struct SubLds {
     LDS int16_t *dec;       // [m] decision at the head (out-arc id, -1 none, -2 head not V-bar);
                             //     phases 1-2 only (union), phase 5 reads dec_of from HBM
     LDS uint64_t *cta;      // [nct_cap] chains, in the topological order of their tails
-    // ctb: the b words.  16-byte records (L:16 | U:16 | x:16 | first arc:16); with 32-bit keys
-    // (no lower bound anywhere, host) 12-byte records: U:16 | x:16 (L = 0; the first arc is
-    // re-derived from the path where it is needed) -- more scenarios fit the LDS of a CU
+    // 16-byte records: cta (above) and ctb = L:16 | U:16 | x:16 | first arc:16.  With 32-bit
+    // keys (no lower bound anywhere, u < 2^11, n + 2 < 2^11, sum |r| < 2^18: host) the first
+    // arc is not stored (re-derived from the path where it is needed) and L = 0: 12-byte
+    // records, ctb = U:16 | x:16, in the eight-wave kernel; one 8-byte word per chain in the
+    // single-wave one (PACK), tail:11 | head:11 | R:19 | U:11 | x:11 -- 16 instead of 12
+    // scenarios of a 1k-arc network fit the LDS of a CU (C4 32 x 256: 23.4 -> 21.7 ms); the
+    // eight-wave kernel, two scenarios per CU either way, keeps the 12-byte records.
+    // ra / rb / wa / wb / add_x read and write the fields in the 16-byte layout's encoding
+    // whatever the storage.
     static constexpr bool kCompact = sizeof(KT) == 4;
+    static constexpr bool kPack = kCompact && PACK;
     using CBT = std::conditional_t<kCompact, uint32_t, uint64_t>;
-    LDS CBT *ctb;           // [nct_cap]
-    // read / write a b word in the 16-byte layout
+    LDS CBT *ctb;           // [nct_cap], none with kPack
+    // 11-bit node id, 0x7FF = -1 (no node; ids < 2^11 - 2 by the host check)
+    static __device__ __forceinline__ int id11(uint64_t v) {
+        const int x = (int)(v & 0x7FFull);
+        return x == 0x7FF ? -1 : x;
+    }
+    __device__ __forceinline__ uint64_t ra(int k) const {
+        if constexpr (kPack) {
+            const uint64_t w = cta[k];
+            return pack_a(id11(w), id11(w >> 11), (int)((int64_t)(w << 23) >> 45));   // R: bits 22..40, signed
+        } else {
+            return cta[k];
+        }
+    }
     __device__ __forceinline__ uint64_t rb(int k) const {
-        if constexpr (kCompact) {
+        if constexpr (kPack) {
+            const uint64_t w = cta[k];
+            return ((w >> 41) & 0x7FFull) << 16 | ((w >> 52) & 0x7FFull) << 32;
+        } else if constexpr (kCompact) {
             const uint32_t v = ctb[k];
             return (uint64_t)(v & 0xFFFFu) << 16 | (uint64_t)(v >> 16) << 32;
         } else {
             return ctb[k];
         }
     }
+    __device__ __forceinline__ void wa(int k, uint64_t a) const {
+        if constexpr (kPack) {
+            const uint64_t f = ((uint64_t)(uint32_t)ch_t(a) & 0x7FFull) | ((uint64_t)(uint32_t)ch_h(a) & 0x7FFull) << 11 |
+                               ((uint64_t)(uint32_t)ch_R(a) & 0x7FFFFull) << 22;
+            cta[k] = (cta[k] & ~((1ull << 41) - 1ull)) | f;
+        } else {
+            cta[k] = a;
+        }
+    }
     __device__ __forceinline__ void wb(int k, uint64_t b) const {
-        if constexpr (kCompact) ctb[k] = (uint32_t)((b >> 16) & 0xFFFFu) | (uint32_t)((b >> 32) & 0xFFFFu) << 16;
-        else ctb[k] = b;
+        if constexpr (kPack) {
+            const uint64_t f = ((b >> 16) & 0x7FFull) << 41 | ((b >> 32) & 0x7FFull) << 52;
+            cta[k] = (cta[k] & ((1ull << 41) - 1ull)) | f;
+        } else if constexpr (kCompact) {
+            ctb[k] = (uint32_t)((b >> 16) & 0xFFFFu) | (uint32_t)((b >> 32) & 0xFFFFu) << 16;
+        } else {
+            ctb[k] = b;
+        }
+    }
+    // flow of chain k += d (0 <= x + d <= U)
+    __device__ __forceinline__ void add_x(int k, int d) const {
+        if constexpr (kPack) cta[k] += (uint64_t)(int64_t)d << 52;
+        else *((LDS int16_t *)&ctb[k] + (kCompact ? 1 : 2)) += (int16_t)d;
     }
     LDS int16_t *chosen;    // [m] in-arc that chose this out-arc of a V-bar node (phases 1-2;
                             //     aliases key / pred)
@@ -153,7 +200,8 @@ constexpr int kSubLdsParts = 12;
 __host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int nz, int nw, size_t *off, int kbytes = 8) {
     size_t o = 0;
     off[1] = o; o = a16(o + (size_t)nct_cap * 8);
-    off[2] = o; o = a16(o + (size_t)nct_cap * (kbytes == 4 ? 4 : 8));   // compact b words with 32-bit keys
+    // b words: 8 bytes, 4 with 32-bit keys, none in the single-wave kernel's 8-byte records
+    off[2] = o; o = a16(o + (size_t)nct_cap * (kbytes == 4 ? (nw == 1 ? 0 : 4) : 8));
     const size_t u0 = o;
     off[3] = o; o = a16(o + (size_t)(n + 2) * kbytes);   // key | chosen
     off[4] = o; o = a16(o + (size_t)(n + 2) * 4);   // pred
@@ -185,8 +233,6 @@ __device__ __forceinline__ uint64_t pack_b(int L, int U, int x, int first) {
            (uint64_t)(uint16_t)first << 48;
 }
 // the flow field of chain k (lane 0 augments)
-template <class WS>
-__device__ __forceinline__ LDS int16_t *ch_xp(const WS &W, int k) { return (LDS int16_t *)&W.ctb[k] + (WS::kCompact ? 1 : 2); }
 
 __device__ __forceinline__ bool is_src(const SubNet &N, int v) { return N.in_off[v + 1] == N.in_off[v]; }
 __device__ __forceinline__ bool is_snk(const SubNet &N, int v) { return N.out_off[v + 1] == N.out_off[v]; }
@@ -211,7 +257,7 @@ __device__ __forceinline__ void for_residual(const SubNet &N, const WS &W, int n
     using B = Blk<NW>;
     // contracted arcs: code 2k (forward), 2k+1 (backward)
     for (int k = B::tid(); k < nct; k += B::T) {
-        const uint64_t ca = W.cta[k], cb = W.rb(k);
+        const uint64_t ca = W.ra(k), cb = W.rb(k);
         const int t = ch_t(ca), h = ch_h(ca);
         if (t < 0 || h < 0) continue;
         const int64_t x = ch_x(cb), L = ch_L(cb), U = ch_U(cb), R = ch_R(ca);
@@ -301,7 +347,7 @@ __device__ __forceinline__ void load_chain_regs(const WS &W, int n, int nct, int
     for (int g = 0; g < RG; g++) {
         const int k = (g * NW + Blk<NW>::wid()) * kWave + lane();
         uint64_t ca = 0, cb = 0;
-        if (k < nct) { ca = W.cta[k]; cb = W.rb(k); }
+        if (k < nct) { ca = W.ra(k); cb = W.rb(k); }
         const ChainArcs<KT> c = chain_arcs<KT>(ca, cb, k < nct, n, mode, M);
         C.th[g] = c.th;
         if constexpr (sizeof(WT) == sizeof(KT)) {   // key increments, formed once
@@ -365,7 +411,7 @@ __device__ __forceinline__ uint32_t bf_sweep(const SubNet &N, const WS &W, int n
         const int k = g * kWave + lane();
         ca = 0;
         cb = 0;
-        if (k < nct) { ca = W.cta[k]; cb = W.rb(k); }
+        if (k < nct) { ca = W.ra(k); cb = W.rb(k); }
     };
     auto reg_w = [&](WT w) -> KT { return sizeof(WT) == sizeof(KT) ? (KT)w : (KT)(((int64_t)w << WS::kHop) + 1); };
     if constexpr (NW > 1) {
@@ -740,7 +786,7 @@ template <class WS>
 __device__ __forceinline__ ChainOut assemble_chain(const SubNet &N, const WS &W, const SubIO &io, int64_t poff, int64_t plen,
                                    int k, int first, int s, bool ray_mode, int ray_p, int ray_q, bool &ok) {
     ChainOut o{0, 0};
-    const uint64_t ca = W.cta[k];
+    const uint64_t ca = W.ra(k);
     const int t = ch_t(ca), h = ch_h(ca);
     const size_t so = (size_t)s * N.m;
     auto rew = [&](int a) -> int64_t { return ray_mode ? 0 : (int64_t)N.reward[a]; };
@@ -882,8 +928,8 @@ __device__ __forceinline__ void chain_starts(const SubNet &N, const WS &W, const
 
 // ---------------------------------------------------------------------------------------
 template <int RG, typename WT, int NW, typename KT, bool ALLREG>
-__global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : (sizeof(KT) == 4 ? 4 : 1)) k_sub_scenario(SubNet N, SubIO io) {
-    using WS = SubLds<KT, ALLREG>;
+__global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3) : (sizeof(KT) == 4 ? 4 : 1)) k_sub_scenario(SubNet N, SubIO io) {
+    using WS = SubLds<KT, ALLREG, NW == 1>;
     using B = Blk<NW>;
     const int tid = B::tid();
     constexpr int T = B::T;
@@ -997,7 +1043,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : (sizeof(KT) == 4 ? 4
             R += N.reward[a];
         }
         const int t = N.vbar[t0] ? -1 : t0;
-        W.cta[k] = pack_a(t, h, R);
+        W.wa(k, pack_a(t, h, R));
         W.wb(k, pack_b(L, U, 0, first));   // compact: L = 0 (host), no first arc
         const bool complete = t >= 0 && h >= 0;
         if ((complete && L > U) || (!complete && L > 0)) first_bad = min(first_bad, k);
@@ -1017,7 +1063,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : (sizeof(KT) == 4 ? 4
     int status = kSubOptimal;
     int64_t M = 0, max_aug = 0;
     for (int k = tid; k < nct; k += T) {
-        const uint64_t ca = W.cta[k];
+        const uint64_t ca = W.ra(k);
         if (ch_t(ca) >= 0 && ch_h(ca) >= 0) {
             const int64_t R = ch_R(ca), U = ch_U(W.rb(k));
             M += 2 * (R < 0 ? -R : R) * (U + 1);
@@ -1043,7 +1089,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : (sizeof(KT) == 4 ? 4
         ray_chain = first_bad;
         const int k = first_bad;
         int a = ch_first(W.rb(k));
-        const bool complete = ch_t(W.cta[k]) >= 0 && ch_h(W.cta[k]) >= 0;
+        const bool complete = ch_t(W.ra(k)) >= 0 && ch_h(W.ra(k)) >= 0;
         int bp = a, bq = a;
         int64_t bl = N.lb[so + a], bu = N.ub[so + a];
         for (int len = 0; len < kMaxChain; len++) {
@@ -1118,10 +1164,10 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : (sizeof(KT) == 4 ? 4
                 const int code = W.plist[i];
                 if (code >= 2 * m) continue;
                 const int k = code >> 1;
-                const uint64_t ca = W.cta[k], cb = W.rb(k);
+                const uint64_t ca = W.ra(k), cb = W.rb(k);
                 const int64_t x = ch_x(cb), L = ch_L(cb), U = ch_U(cb);
                 const int64_t cap = (code & 1) ? (x > L ? x - L : x) : (x < L ? L - x : U - x);
-                *ch_xp(W, k) += (int16_t)((code & 1) ? -delta : delta);
+                W.add_x(k, (int)((code & 1) ? -delta : delta));
                 if (cap == delta) W.key[(code & 1) ? ch_t(ca) : ch_h(ca)] = WS::kKInf;   // segment used up
             }
             B::sync();
@@ -1143,7 +1189,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? 3 : (sizeof(KT) == 4 ? 4
         // lower bounds met?
         int unmet = 0;
         for (int k = tid; k < nct; k += T) {
-            const uint64_t ca = W.cta[k], cb = W.rb(k);
+            const uint64_t ca = W.ra(k), cb = W.rb(k);
             if (ch_t(ca) >= 0 && ch_h(ca) >= 0) {
                 if (ch_x(cb) < ch_L(cb)) unmet = 1;
                 primal += (int64_t)ch_R(ca) * ch_x(cb);
@@ -1274,8 +1320,11 @@ hipError_t launch_scenarios(const SubNet &N, const SubIO &io, hipStream_t st) {
     if (lds < SGUFP_SUB_LDS_MIN) lds = SGUFP_SUB_LDS_MIN;   // occupancy experiments
 #endif
     // the large variant (kLargeWaves waves per scenario, 32-bit costs in registers) once the
-    // LDS allows at most two scenarios per CU and the big-M costs fit 32 bits (host bound)
-    const bool large = lds > 64 * 1024 && io.nct_cap > kRegGroupsSmall * kWave && N.cost_bound < ((int64_t)1 << 30);
+    // LDS allows at most two scenarios per CU (in its own layout: the single-wave 8-byte
+    // records would bring C5 under the bar and back to one wave per scenario, 4x slower) and
+    // the big-M costs fit 32 bits (host bound)
+    const bool large = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, kLargeWaves, kb) > 64 * 1024 &&
+                       io.nct_cap > kRegGroupsSmall * kWave && N.cost_bound < ((int64_t)1 << 30);
     const char *ev = getenv("SGUFP_SUB_WAVES");
     if (large && !(ev && atoi(ev) == 1)) {
         lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, kLargeWaves, kb);

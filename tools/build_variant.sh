@@ -9,7 +9,7 @@ OUT=sgufp_solver_amd/lib_var/$NAME
 mkdir -p $OUT/obj
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Iinclude -Isgufp_solver_amd/csrc $*"
 /opt/rocm/bin/hipcc $FLAGS -x hip -c $SRC -o $OUT/obj/sub.o
-for f in dd_kernels.hip bnb_kernels.hip rdd_kernels.hip; do
+for f in dd_kernels.hip bnb_kernels.hip rdd_kernels.hip exact_kernels.hip; do
   cp sgufp_solver_amd/lib/obj/$f.o $OUT/obj/$f.o
 done
 for f in capi.cpp bnb.cpp network.cpp shard.cpp; do cp sgufp_solver_amd/lib/obj/$f.o $OUT/obj/$f.o; done
