@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import os
 import subprocess
+import sys
 import tempfile
 from typing import List, Sequence
 
@@ -317,7 +318,7 @@ def check_search(cfg: str, seed: int, width: int, rounds: int, batch: int, sampl
         rep["closed"] += len(closed)
         print(f"[bnb parity {cfg}] round {r}: popped {st.popped} relaxed {st.relaxed} subproblems {len(subs)} "
               f"closed {len(closed)} pool {len(pool)} checked {rep['checked']} failures {len(fail)} "
-              f"{time.perf_counter() - t0:.1f} s", flush=True)
+              f"{time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
         zc = max([z0] + [c[3] for c in closed])
         if z != zc:
             fail.append(f"round {r}: incumbent {z!r} != max(zOpt, closed bounds) {zc!r}")

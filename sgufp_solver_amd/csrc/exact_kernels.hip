@@ -86,6 +86,7 @@ __global__ void __launch_bounds__(256) k_exact_root(NetDev net, Scratch sc, Exac
     const int nblk = nbs + (ex.no + kWave - 1) / kWave;        // + pool blocks
     const long long total = (long long)npend * nblk;
     const int ns = net.n_slots;
+    if (total == 0) return;   // no exact record in the batch (a DD-only batch): no counter traffic
     for (;;) {
         if (lane() == 0) item_s[w] = (int32_t)atomicAdd(&ex.ctr[1], 1ull);
         __builtin_amdgcn_wave_barrier();
