@@ -179,10 +179,23 @@ struct ChildOut {
 // same tree), a workgroup per pass of kLeafPass leaves of one record, every cut column read
 // once per pass from a cut-minor copy of the O rows.
 constexpr int32_t kExactPending = 5;
-constexpr int kExactMaxT = 16;         // DD layers (root included) the hand-off takes
-constexpr int kExactMaxEntries = 64;   // (T - 1) * ustride coefficient rows staged per cut block
-constexpr int kLeafWaves = 8;          // waves per leaf-kernel workgroup
-constexpr int kLeavesPerWave = 32;
+#ifndef SGUFP_EXACT_MAXT
+#define SGUFP_EXACT_MAXT 8
+#endif
+#ifndef SGUFP_EXACT_ENTRIES
+#define SGUFP_EXACT_ENTRIES 64
+#endif
+#ifndef SGUFP_LEAVES_PER_WAVE
+#define SGUFP_LEAVES_PER_WAVE 16
+#endif
+// Leaf-kernel sizing (seeded C3 B&B, tools/gpu_r04o.sh): 16 layers / 32 leaves per wave at 2 waves
+// per SIMD (101 KB of LDS per workgroup) 1 915 relaxations/s; 8 layers / 16 leaves per wave, two
+// workgroups per CU at 4 waves per SIMD (105 VGPRs) 2 232; 8 / 32 at 4 waves per SIMD (128 VGPRs)
+// 2 112.  The exact DDs of the C3 / C4 searches all have 7 layers; deeper ones take k_relax's path.
+constexpr int kExactMaxT = SGUFP_EXACT_MAXT;           // DD layers (root included) the hand-off takes
+constexpr int kExactMaxEntries = SGUFP_EXACT_ENTRIES;  // (T - 1) * ustride coefficient rows staged per cut block
+constexpr int kLeafWaves = 8;                          // waves per leaf-kernel workgroup
+constexpr int kLeavesPerWave = SGUFP_LEAVES_PER_WAVE;
 constexpr int kLeafPass = kLeafWaves * kLeavesPerWave;
 
 struct ExactIO {

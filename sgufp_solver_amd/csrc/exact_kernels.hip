@@ -13,7 +13,7 @@
 //   k_exact_cols  new optimality rows -> the cut-minor copy coefO (row n_slots + 1 = RHS)
 //   k_exact_root  the root prefix (DD.cpp:3938-3949: RHS, then + coef per decision of the
 //                 record's solution, in order) of every (pending record, cut): lanes = cuts
-//   k_exact_leaf  per (record, pass of kLeafPass leaves): 8 waves x 32 leaves, lanes = cuts
+//   k_exact_leaf  per (record, pass of kLeafPass leaves): 8 waves x 16 leaves, lanes = cuts
 //                 of a 64-cut block staged in LDS; per leaf the lane keeps the running
 //                 std::min of its cuts' path values (DD.cpp:3975-3984) in a register; a
 //                 pass stops early once every leaf is <= optimalLB (the outcome no longer
@@ -184,7 +184,10 @@ __device__ double first_zero(const NetDev &net, const ExactIO &ex, LeafShared &S
     return 0.0;
 }
 
-__global__ void __launch_bounds__(kLeafWaves * kWave) k_exact_leaf(NetDev net, Scratch sc, ExactIO ex, double incumbent) {
+#ifndef SGUFP_LEAF_MIN_WAVES
+#define SGUFP_LEAF_MIN_WAVES 4   // two 8-wave workgroups per CU (VGPRs <= 128)
+#endif
+__global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_exact_leaf(NetDev net, Scratch sc, ExactIO ex, double incumbent) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LeafShared &S = *(LeafShared *)smem_raw;
     const int w = wid();

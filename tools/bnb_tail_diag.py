@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--slots", type=int, default=2048, help="resident k_relax waves (2 per SIMD x 1024 SIMDs)")
     ap.add_argument("--round-iters", type=int, default=0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--gl-hist", action="store_true", help="histogram of the DD layers of the exact survivors")
     a = ap.parse_args()
     from sgufp_solver_amd import engine as E
     from sgufp_solver_amd import instance
@@ -50,6 +51,7 @@ def main():
     eng.frontier_clear()
     eng.frontier_push([root])
     t0 = time.perf_counter()
+    t_hist = {}
     rows = []
     seen_paths = {}
     dup = 0
@@ -57,6 +59,11 @@ def main():
     while time.perf_counter() - t0 < a.seconds and eng.frontier_size():
         eng.bnb_set_limits(a.round_iters, a.round_seconds)
         b = 64 if diving else a.batch
+        gls = None
+        if a.gl_hist:
+            fs = eng.frontier_size()
+            nb = min(b, fs)
+            gls = eng.frontier_peek(fs - nb, nb).gl.astype(np.int64)
         tr = time.perf_counter()
         z, st = eng.bnb_step(z, b)
         wall = time.perf_counter() - tr
@@ -73,6 +80,10 @@ def main():
         redo = np.array([w[1] for w in waves])
         sw = np.array([w[2] for w in waves])
         stt = np.array([p[1] for p in popped])
+        if gls is not None and len(gls) == len(stt):
+            # DD layers of the records that reached the subproblem (exact DDs): total - gl + 1
+            for t in (eng.info.total_layers - gls[stt == 3] + 1):
+                t_hist[int(t)] = t_hist.get(int(t), 0) + 1
         ms = ticks / 1e5
         launch = float(st.ms_relax)
         fill = float(ms.sum() / max(1e-9, launch * min(a.slots, max(n, 1)))) if launch else 0.0
@@ -93,6 +104,8 @@ def main():
     tot["k_relax_share"] = round(tot["k_relax_ms"] / tot["wall_ms"], 3)
     tot["duplicate_subproblem_paths"] = dup
     tot["round_iters"] = a.round_iters
+    if a.gl_hist:
+        tot["exact_dd_layers_hist"] = dict(sorted(t_hist.items()))
     print(json.dumps({"total": tot}))
     if a.out:
         with open(a.out, "w") as fh:
