@@ -183,15 +183,17 @@ constexpr int32_t kExactPending = 5;
 #define SGUFP_EXACT_MAXT 8
 #endif
 #ifndef SGUFP_EXACT_ENTRIES
-#define SGUFP_EXACT_ENTRIES 64
+#define SGUFP_EXACT_ENTRIES 40
 #endif
 #ifndef SGUFP_LEAVES_PER_WAVE
 #define SGUFP_LEAVES_PER_WAVE 16
 #endif
-// Leaf-kernel sizing (seeded C3 B&B, tools/gpu_r04o.sh): 16 layers / 32 leaves per wave at 2 waves
-// per SIMD (101 KB of LDS per workgroup) 1 915 relaxations/s; 8 layers / 16 leaves per wave, two
-// workgroups per CU at 4 waves per SIMD (105 VGPRs) 2 232; 8 / 32 at 4 waves per SIMD (128 VGPRs)
-// 2 112.  The exact DDs of the C3 / C4 searches all have 7 layers; deeper ones take k_relax's path.
+// Leaf-kernel sizing (seeded C3 B&B, tools/gpu_r04o.sh, gpu_r04r.sh): 16 layers / 64 staged rows /
+// 32 leaves per wave at 2 waves per SIMD (101 KB of LDS per workgroup) 1 915 relaxations/s; 8 / 64 /
+// 16, two workgroups per CU at 4 waves per SIMD (105 VGPRs) 2 232; 8 / 40 / 16, three workgroups
+// per CU at 6 waves per SIMD (80 VGPRs, 50 KB): k_relax 4.08 -> 3.30 s over the same 88 rounds.
+// The exact DDs of the C3 / C4 searches all have 7 layers and 5 state ranks (30 rows); deeper or
+// wider ones take k_relax's own path.
 constexpr int kExactMaxT = SGUFP_EXACT_MAXT;           // DD layers (root included) the hand-off takes
 constexpr int kExactMaxEntries = SGUFP_EXACT_ENTRIES;  // (T - 1) * ustride coefficient rows staged per cut block
 constexpr int kLeafWaves = 8;                          // waves per leaf-kernel workgroup

@@ -140,7 +140,7 @@ struct LeafShared {
     double C[kExactMaxEntries][kWave];   // staged coefficients of a 64-cut block, row = (k-1)*us + r
     int32_t stab[kExactMaxEntries];      // their slots (-1: no coefficient)
     LeafWave lw[kLeafWaves];
-    double vb[kLeafWaves][kExactMaxT][kWave];   // ancestor values of the current leaf, per wave
+    double vb[kLeafWaves][kExactMaxT - 1][kWave];   // ancestor values of the current leaf (layers 0 .. T - 2), per wave
     int32_t item, flags[kLeafWaves];
 };
 
@@ -185,7 +185,7 @@ __device__ double first_zero(const NetDev &net, const ExactIO &ex, LeafShared &S
 }
 
 #ifndef SGUFP_LEAF_MIN_WAVES
-#define SGUFP_LEAF_MIN_WAVES 4   // two 8-wave workgroups per CU (VGPRs <= 128)
+#define SGUFP_LEAF_MIN_WAVES 6   // three 8-wave workgroups per CU (VGPRs <= 85)
 #endif
 __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_exact_leaf(NetDev net, Scratch sc, ExactIO ex, double incumbent) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
@@ -369,7 +369,7 @@ hipError_t launch_exact(const NetDev &net, const Scratch &sc, const ExactIO &ex,
     hipLaunchKernelGGL(k_exact_root, dim3(4 * cus), dim3(256), 0, st, net, sc, ex);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_exact_leaf, dim3(2 * cus), dim3(kLeafWaves * kWave), sizeof(LeafShared), st, net, sc, ex,
+    hipLaunchKernelGGL(k_exact_leaf, dim3(4 * cus), dim3(kLeafWaves * kWave), sizeof(LeafShared), st, net, sc, ex,
                        incumbent);
     return hipGetLastError();
 }
