@@ -89,6 +89,10 @@ bool sgufp_ctx::frontier_reserve(int64_t entries, size_t sol_entries) {
     return true;
 }
 
+// Seen-path lists of the refinement loops: slots x cap entries of Lcap int16 + len + hash, i.e.
+// slots x cap x (2 Lcap + 10) bytes (1 024 slots x 64 x 572 B = 37 MB at 1k arcs).  cap doubles
+// when one loop outgrows it and is kept for the search (the longest loop sets it); the lists go
+// with sgufp_frontier_clear.
 bool sgufp_ctx::loop_reserve(int slots, int cap) {
     const int Lc = std::max(sc.Lcap, 1);
     if (!d_lact) {
@@ -247,6 +251,15 @@ int sgufp_frontier_clear(sgufp_ctx *ctx) {
     ctx->fr_n = 0;
     ctx->fr_sol_top = 0;
     ctx->deferred_seen.clear();
+    if (ctx->seen.paths) {   // a new search starts with small seen-path lists again
+        if (!ctx->sync()) return SGUFP_ERR_HIP;
+        ctx->release(ctx->seen.paths);
+        ctx->release(ctx->seen.len);
+        ctx->release(ctx->seen.hash);
+        ctx->release(ctx->seen.n);
+        ctx->seen = SeenLists{};
+        ctx->seen_slots = 0;
+    }
     return SGUFP_OK;
 }
 
