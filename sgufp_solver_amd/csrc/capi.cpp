@@ -319,6 +319,7 @@ bool sgufp_ctx::exact_prepare() {
         return false;
     ex.lazy = ex.nsc == 0 ? exact_lazy : 0;
     ex.pidx = d_pidx;
+    ex.nslots = max_batch;
     ex.ostride = ocap;
     ex.coefO = d_coefO;
     ex.R = d_R;

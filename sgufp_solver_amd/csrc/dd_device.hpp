@@ -217,7 +217,8 @@ struct ExactIO {
     // (k_exact_fin, k_refine) complete a flagged leaf over the remaining blocks only when it
     // is the maximum (exact_resolve).  0: every pass sweeps the whole pool.
     int lazy;
-    int32_t SGUFP_GBL *pidx;              // [max_batch] batch slot -> pending index (-1: none)
+    int32_t SGUFP_GBL *pidx;              // [nslots] batch slot -> pending index (-1: none)
+    int nslots;                           // batch slots (max_batch)
     // screening columns swept first (any order gives the same terminal minima; these -- the
     // strongest O cuts by their node-independent bound, Pool::o_rank -- end pruned records
     // early): nsc of them, kExactScreen columns allocated

@@ -76,27 +76,38 @@ __global__ void __launch_bounds__(256) k_exact_cols(const double *rows, const do
 }
 
 // ---- k_exact_root: R[i][s] = root prefix of pending record i under O cut s (newest first) --
+// The records of a batch are mostly siblings of a few cutsets: neighbouring batch slots share
+// long solution prefixes.  A work item is (a chunk of kRootChunk batch slots, a 64-cut block);
+// its wave folds the chunk's pending records in slot order and keeps the partial sums at every
+// st-th solution position (checkpoints in LDS): a record restarts from the last checkpoint inside
+// its common prefix with the previous record.  The partial sums are the same additions in the same
+// order, so the values are bit-identical to a fold from the RHS (DD.cpp:3938-3949).
 constexpr int kFold = 16;
-__global__ void __launch_bounds__(256) k_exact_root(NetDev net, Scratch sc, ExactIO ex) {
-    __shared__ int32_t item_s[4];
+constexpr int kRootChunk = 64;        // batch slots per work item
+constexpr int kRootCk = 24;           // checkpoints per wave
+constexpr int kRootWaves = 4;
+__global__ void __launch_bounds__(kRootWaves * kWave) k_exact_root(NetDev net, Scratch sc, ExactIO ex) {
+    __shared__ int32_t item_s[kRootWaves];
+    __shared__ double ck_s[kRootWaves][kRootCk][kWave];
     const int w = wid();
     const unsigned long long packed = ex.ctr[0];
     const int npend = (int)(packed >> 32);
+    if (npend == 0) return;   // no exact record in the batch (a DD-only batch): no counter traffic
     const int nbs = (ex.nsc + kWave - 1) / kWave;              // screening blocks
     const int nblk = nbs + (ex.no + kWave - 1) / kWave;        // + pool blocks
-    const long long total = (long long)npend * nblk;
+    const int nchunk = (ex.nslots + kRootChunk - 1) / kRootChunk;
+    const long long total = (long long)nchunk * nblk;
     const int ns = net.n_slots;
-    if (total == 0) return;   // no exact record in the batch (a DD-only batch): no counter traffic
+    // checkpoint stride: positions 0, st, 2 st, ... (ck[q] = the sum after q * st entries)
+    const int st = max(kFold, ((sc.Lcap + kRootCk - 1) / kRootCk + kFold - 1) / kFold * kFold);
+    double(&ck)[kRootCk][kWave] = ck_s[w];
     for (;;) {
         if (lane() == 0) item_s[w] = (int32_t)atomicAdd(&ex.ctr[1], 1ull);
         __builtin_amdgcn_wave_barrier();
         const long long item = (long long)uni(item_s[w]);
         __builtin_amdgcn_wave_barrier();
         if (item >= total) break;
-        const int i = (int)(item / nblk), bb = (int)(item % nblk);
-        const int slot = ex.pend_slot[i];
-        const int len = sc.meta[(size_t)slot * 8 + 1];
-        const GBL int32_t *rs = sc.rslot + (size_t)slot * sc.Lcap;
+        const int c = (int)(item / nblk), bb = (int)(item % nblk);
         const bool scr = bb < nbs;
         const int b = scr ? bb : bb - nbs;
         const int s = b * kWave + lane();
@@ -104,25 +115,57 @@ __global__ void __launch_bounds__(256) k_exact_root(NetDev net, Scratch sc, Exac
         const int col = vc ? (scr ? s : ex.no - 1 - s) : 0;
         const GBL double *cm = scr ? ex.coefS : ex.coefO;
         const size_t cs = scr ? (size_t)kExactScreen : (size_t)ex.ostride;
-        double v = cm[(size_t)(ns + 1) * cs + col];
-        for (int t0 = 0; t0 < len; t0 += kFold) {
-            double x[kFold];
-            bool ok[kFold];
-#pragma unroll
-            for (int j = 0; j < kFold; j++) {
-                const int t = t0 + j;
-                const int sl = t < len ? uni(rs[t]) : -1;
-                ok[j] = sl >= 0;
-                x[j] = cm[(size_t)(ok[j] ? sl : ns) * cs + col];
+        const double rhs = cm[(size_t)(ns + 1) * cs + col];
+        const GBL int32_t *prs = nullptr;   // previous record's slots and length, valid checkpoints
+        int plen = 0, qvalid = 0;
+        const int s0 = c * kRootChunk, s1 = min(ex.nslots, s0 + kRootChunk);
+        for (int slot = s0; slot < s1; slot++) {
+            const int i = uni(ex.pidx[slot]);
+            if (i < 0) continue;
+            const int len = uni(sc.meta[(size_t)slot * 8 + 1]);
+            const GBL int32_t *rs = sc.rslot + (size_t)slot * sc.Lcap;
+            // common prefix with the previous record (64 positions per step)
+            int lcp = 0;
+            if (prs) {
+                const int m = min(len, plen);
+                lcp = m;
+                for (int t0 = 0; t0 < m; t0 += kWave) {
+                    const int t = t0 + lane();
+                    const uint64_t diff = __ballot(t < m && rs[t] != prs[t]);
+                    if (diff) {
+                        lcp = t0 + (int)(__ffsll((unsigned long long)diff) - 1);
+                        break;
+                    }
+                }
             }
-            sched_fence();
+            const int q0 = min(lcp / st, qvalid);
+            double v = q0 > 0 ? ck[q0][lane()] : rhs;
+            for (int t0 = q0 * st; t0 < len; t0 += kFold) {
+                if (t0 % st == 0 && t0 / st < kRootCk) ck[t0 / st][lane()] = v;
+                double x[kFold];
+                bool ok[kFold];
 #pragma unroll
-            for (int j = 0; j < kFold; j++)
-                if (ok[j]) v = v + x[j];
-        }
-        if (vc) {
-            if (scr) ex.RS[(size_t)i * kExactScreen + s] = v;
-            else ex.R[(size_t)i * ex.ostride + s] = v;
+                for (int j = 0; j < kFold; j++) {
+                    const int t = t0 + j;
+                    const int sl = t < len ? uni(rs[t]) : -1;
+                    ok[j] = sl >= 0;
+                    x[j] = cm[(size_t)(ok[j] ? sl : ns) * cs + col];
+                }
+                sched_fence();
+#pragma unroll
+                for (int j = 0; j < kFold; j++)
+                    if (ok[j]) v = v + x[j];
+            }
+            // checkpoints 0 .. floor(len / st) hold this record's prefix (the one at len itself
+            // only when len is a multiple of st: written here)
+            if (len % st == 0 && len / st < kRootCk) ck[len / st][lane()] = v;
+            qvalid = min(len / st, kRootCk - 1);
+            prs = rs;
+            plen = len;
+            if (vc) {
+                if (scr) ex.RS[(size_t)i * kExactScreen + s] = v;
+                else ex.R[(size_t)i * ex.ostride + s] = v;
+            }
         }
     }
 }
@@ -366,7 +409,7 @@ hipError_t launch_exact_cols(const double *rows, const double *rhs, const int32_
 // the pending records' root folds and terminal weights; k_exact_fin (dd_kernels.hip) ends them
 hipError_t launch_exact(const NetDev &net, const Scratch &sc, const ExactIO &ex, double incumbent, int cus,
                         hipStream_t st) {
-    hipLaunchKernelGGL(k_exact_root, dim3(4 * cus), dim3(256), 0, st, net, sc, ex);
+    hipLaunchKernelGGL(k_exact_root, dim3(4 * cus), dim3(kRootWaves * kWave), 0, st, net, sc, ex);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_exact_leaf, dim3(4 * cus), dim3(kLeafWaves * kWave), sizeof(LeafShared), st, net, sc, ex,
