@@ -99,18 +99,25 @@ bool sgufp_ctx::init() {
     int64_t tail = 0;
     int64_t ncap = node_bound(net, &tail);
     ustride = std::max(1, net.max_states);
-    if (const char *e = getenv("SGUFP_CUT_BATCH")) cb = atoi(e);
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+            cus = prop.multiProcessorCount;
+    }
+    // Cuts per batched sweep: 4 (k_relax runs 2 waves per SIMD, 20 KB of LDS each).  A context
+    // whose batches fill at most half of those wave slots (the B&B rounds: 1 024 records on 2 048
+    // slots) sweeps 8 cuts at a time (28 KB, 5 waves per CU, still one wave per record): the
+    // non-exact survivors of a seeded C3 search that sweep a pool of 39k / 75k cuts take 791 ->
+    // 545 / 2 462 -> 2 081 ms per round (tools/gpu_r04v.sh).  SGUFP_CUT_BATCH forces a size.
+    const char *ecb = getenv("SGUFP_CUT_BATCH");
+    if (ecb) cb = atoi(ecb);
+    else if (2 * (int64_t)max_batch <= 8 * (int64_t)cus) cb = 8;
     if (cb != 1 && cb != 4 && cb != 8 && cb != 16) cb = 4;
     nscreen = cb;
     if (const char *e = getenv("SGUFP_SCREEN")) nscreen = std::max(0, atoi(e));
     if (const char *e = getenv("SGUFP_EXACT_FAST")) exact_fast = atoi(e) != 0;
     if (const char *e = getenv("SGUFP_EXACT_SCREEN")) exact_screen = std::max(0, std::min(kExactScreen, atoi(e)));
     if (const char *e = getenv("SGUFP_EXACT_LAZY")) exact_lazy = std::max(0, atoi(e));
-    {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
-            cus = prop.multiProcessorCount;
-    }
     int64_t acap = std::max<int64_t>(1, (int64_t)std::max(0, L - 4) * (kRelaxedMaxWidth - 1) * maxU);
     if (ncap > (int64_t)kParentMask || acap > (int64_t)0x7FFFFFFF) { err = "DD capacity beyond 22-bit indices"; return false; }
     sc.Ncap = (int)ncap;
