@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--round-iters", type=int, default=0)
     ap.add_argument("--out", default=None)
     ap.add_argument("--gl-hist", action="store_true", help="histogram of the DD layers of the exact survivors")
+    ap.add_argument("--no-trace", action="store_true", help="search without the round trace (as the bench legs run)")
     a = ap.parse_args()
     from sgufp_solver_amd import engine as E
     from sgufp_solver_amd import instance
@@ -45,7 +46,7 @@ def main():
     inst.write(net)
     eng = E.Engine(net, 0, a.batch)
     eng.set_timing(True)
-    eng.bnb_set_trace(True)
+    eng.bnb_set_trace(not a.no_trace)
     root = NodeRecord(0, DOUBLE_MIN, DOUBLE_MAX, [], [])
     z = RestrictedExplorer(eng, a.width).incumbent([root], DOUBLE_MIN) if a.width else DOUBLE_MIN
     eng.frontier_clear()
@@ -70,9 +71,9 @@ def main():
         if st.exact:
             diving = False
         n = int(st.popped)
-        waves = eng.bnb_trace(3)
-        popped = eng.bnb_trace(0)
-        for sub in eng.bnb_trace(1):
+        waves = eng.bnb_trace(3) if not a.no_trace else []
+        popped = eng.bnb_trace(0) if not a.no_trace else []
+        for sub in (eng.bnb_trace(1) if not a.no_trace else []):
             key = hash(tuple(sub[4]))
             dup += 1 if key in seen_paths else 0
             seen_paths[key] = 1
@@ -94,8 +95,8 @@ def main():
                           "wave_ms_max": round(float(ms[m].max()), 3), "sweeps_mean": round(float(sw[m].mean()), 1),
                           "redo_mean": round(float(redo[m].mean()), 2), "redo_frac": round(float((redo[m] > 0).mean()), 3)}
         rows.append({"round": len(rows), "popped": n, "wall_ms": round(wall * 1e3, 2), "k_relax_ms": round(launch, 2),
-                     "wave_ms_max": round(float(ms.max()), 3) if n else 0.0,
-                     "wave_ms_mean": round(float(ms.mean()), 3) if n else 0.0,
+                     "wave_ms_max": round(float(ms.max()), 3) if len(ms) else 0.0,
+                     "wave_ms_mean": round(float(ms.mean()), 3) if len(ms) else 0.0,
                      "fill": round(fill, 3), "subproblems": int(st.subproblems), "iters": int(st.refine_iters),
                      "pool": eng.cuts_count(0) + eng.cuts_count(1), "by_status": by})
         print(json.dumps(rows[-1]), flush=True)
