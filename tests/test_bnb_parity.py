@@ -73,3 +73,15 @@ def test_bnb_parity_c5():
     seen = _search_rounds("C5", 1, 0, rounds=80, batch=32, sample=8, round_seconds=3.0, replay=False,
                           min_subproblems=1, rounds_after=1, round_iters=1)
     assert seen["relaxed"] > 0 and seen["subproblems"] > 0
+
+
+@pytest.mark.parametrize("knob,value", [("SGUFP_EXACT_FAST", "0"), ("SGUFP_EXACT_LAZY", "1"),
+                                        ("SGUFP_EXACT_SCREEN", "64")])
+def test_bnb_parity_exact_phase_variants(monkeypatch, knob, value):
+    """The other ways the exact DDs' optimality phase can run (capi.cpp, exact_kernels.hip):
+    k_relax's own in-order sweeps (deeper / wider exact DDs take it), lazy terminal weights
+    completed on demand in k_exact_fin / k_refine, and screening columns swept first -- on M1,
+    whose refinement loops close, so k_refine and the argmax paths are exercised too."""
+    monkeypatch.setenv(knob, value)
+    seen = _search_rounds("M1", 1, 0, rounds=120, batch=64, sample=32, min_closed=2)
+    assert seen["closed"] >= 2 and seen["replayed"] > 0
