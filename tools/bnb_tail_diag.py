@@ -98,9 +98,10 @@ def main():
                      "wave_ms_max": round(float(ms.max()), 3) if len(ms) else 0.0,
                      "wave_ms_mean": round(float(ms.mean()), 3) if len(ms) else 0.0,
                      "fill": round(fill, 3), "subproblems": int(st.subproblems), "iters": int(st.refine_iters),
-                     "pool": eng.cuts_count(0) + eng.cuts_count(1), "by_status": by})
+                     "pool": eng.cuts_count(0) + eng.cuts_count(1), "resumed": int(st.resumed),
+                     "deferred": int(st.deferred), "by_status": by})
         print(json.dumps(rows[-1]), flush=True)
-    tot = {k: sum(r[k] for r in rows) for k in ("wall_ms", "k_relax_ms", "popped", "subproblems")}
+    tot = {k: sum(r[k] for r in rows) for k in ("wall_ms", "k_relax_ms", "popped", "subproblems", "resumed")}
     tot["relaxations_per_s"] = round(tot["popped"] / (tot["wall_ms"] / 1e3), 1)
     tot["k_relax_share"] = round(tot["k_relax_ms"] / tot["wall_ms"], 3)
     tot["duplicate_subproblem_paths"] = dup
