@@ -20,10 +20,16 @@ per-step time is the max over ranks.
 Beside the headline the line carries: `parity` (the timed step's results for the first
 --cpu-sample records against the reference's own RelaxedDDNew on the same records, bit for
 bit), `cpu_baseline` (that reference run's rate on the host cores), `roofline` (PMC-counted
-HBM bytes of this build per k_relax launch), `subproblem` (the scenario LP kernels alone),
-`bnb` (the device B&B with its exact-leaf subproblems on the same 256-scenario network) and
-`config5` (BASELINE configs[4]: 5k arcs, 512 scenarios, relaxation + subproblem + B&B with
-cut generation).
+HBM bytes of this build per k_relax launch, with the issue counters of the same build),
+`subproblem` (the scenario LP kernels alone), `bnb` / `bnb_seeded` (the device B&B with its
+exact-leaf subproblems on the same 256-scenario network, without an incumbent / seeded by the
+restricted-DD heuristic inside the timed region), `bnb_parity` (rounds of the seeded search
+checked against the reference under the search's own Benders pools, oracle/bnb_parity.py) and
+`config5` (BASELINE configs[4]: 5k arcs, 512 scenarios, relaxation with a 256-record parity
+block, subproblem, B&B with cut generation).  With N > 1 ranks `bnb_multi` is the seeded C4
+search strong-scaled over the N frontier shards (incumbent all-reduce, cut-row all-gather and
+work sharing every round; through the library's own RCCL communicator, shard.cpp, when the
+backend is nccl).  Progress goes to stderr; stdout carries the one JSON line.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 the driver uses
 torch.distributed.run and this script reads RANK / LOCAL_RANK / WORLD_SIZE.
