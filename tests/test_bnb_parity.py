@@ -83,5 +83,5 @@ def test_bnb_parity_exact_phase_variants(monkeypatch, knob, value):
     completed on demand in k_exact_fin / k_refine, and screening columns swept first -- on M1,
     whose refinement loops close, so k_refine and the argmax paths are exercised too."""
     monkeypatch.setenv(knob, value)
-    seen = _search_rounds("M1", 1, 0, rounds=120, batch=64, sample=32, min_closed=2)
+    seen = _search_rounds("M1", 1, 0, rounds=120, batch=64, sample=12, min_closed=2, highs=False)
     assert seen["closed"] >= 2 and seen["replayed"] > 0
