@@ -600,9 +600,13 @@ def main():
         dist.destroy_process_group()
 
 
+WATCHDOG_EXIT = 3   # a stalled collective fails the run (exit status), it is not hidden in the line
+
+
 def watchdog(seconds, line, rank):
     """After `seconds` without stop.set(): rank 0 prints the line built so far (the leg marked
-    as timed out) and every rank exits (a shard stuck in a collective cannot be unwound)."""
+    as timed out) and every rank exits with WATCHDOG_EXIT (a shard stuck in a collective cannot
+    be unwound, and a run that stalled must not look like a successful one)."""
     import threading
     stop = threading.Event()
 
@@ -612,7 +616,9 @@ def watchdog(seconds, line, rank):
                 line["bnb_multi"] = {"error": f"timed out after {seconds:.0f} s"}
                 print(json.dumps(line), flush=True)
             sys.stdout.flush()
-            os._exit(0)
+            sys.stderr.write(f"bench: rank {rank}: multi-rank leg stalled for {seconds:.0f} s, exiting {WATCHDOG_EXIT}\n")
+            sys.stderr.flush()
+            os._exit(WATCHDOG_EXIT)
 
     threading.Thread(target=run, daemon=True).start()
     return stop

@@ -6,6 +6,8 @@
 //   Inavap::Cut / cut_node_t / Container / getKey        Cut.h:201-337, 342-344, 448-485
 //   CutType                                             Cut.h:22-25
 //   Inavap::OutObject (STATUS_OP)                        NodeExplorer.h:78-110
+//   Inavap::RelaxedDDNew (buildTree / isTreeExact /     DD.h:797-808, DD.cpp:3528-4218
+//     applyFeasibilityCut / applyOptimalityCut / getSolution / getCutset)
 //   Inavap::GuroSolver::solveSubProblem(path)            grb.h:75, grb.cpp:139-360 (device LP)
 //   Inavap::NodeExplorer::process(node, lb, F, O)        NodeExplorer.h:124-130, NodeExplorer.cpp:915-986
 //   Inavap::DDSolver(net, nWorkers) / start / startSolver DDSolver.h:431-439, DDSolver.cpp:782-867
@@ -131,6 +133,27 @@ class Device {
     Device &operator=(const Device &) = delete;
     sgufp_ctx *get() const { return ctx_; }
     void check(int rc, const char *what) const;
+};
+
+// RelaxedDDNew (DD.h:797-808) on the device, one DD at a time: the DD is built and kept in
+// a device slot (sgufp_dd_* of the C ABI); every call is one kernel launch and returns what
+// the reference returns, bit for bit.  DDSolver::startSolver's root DD (DDSolver.cpp:788-791)
+// and a NodeExplorer written against the reference's DD class use it unchanged.  For
+// throughput use NodeExplorer::process / DDSolver, which batch the same work.
+class RelaxedDDNew {
+    const Network *networkPtr;
+    std::unique_ptr<Device> dev;
+    bool built = false, exact = false;
+    void upload_cut(const Cut &cut, std::vector<uint64_t> &keys, std::vector<double> &vals) const;
+
+  public:
+    explicit RelaxedDDNew(const Network *pointer);
+    void buildTree(Node root);
+    Path getSolution() const;
+    bool isTreeExact() const noexcept { return exact; }
+    uint8_t applyFeasibilityCut(const Cut &cut);
+    double applyOptimalityCut(const Cut &cut, double optimal, double upperbound);
+    std::vector<Node> getCutset(double ub);
 };
 
 // The scenario subproblem on the device; returns the cut the reference builds (cutToCut

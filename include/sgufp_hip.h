@@ -124,9 +124,34 @@ int sgufp_batch_paths(sgufp_ctx *ctx, int64_t *path_off, int16_t *paths);
 int sgufp_batch_stats(sgufp_ctx *ctx, int64_t *dd_nodes, int64_t *dd_arcs, int32_t *dd_layers, int32_t *sweeps);
 /* Apply, for each listed staged node (still SGUFP_NEEDS_SUBPROBLEM), the pool cut
  * (is_feasibility[k], index in that pool) -- appended beforehand with
- * sgufp_cuts_append -- and recompute status / ub / path. */
+ * sgufp_cuts_append -- and recompute status / ub / path.  optimal_lb must not be below the
+ * optimalLB the batch was relaxed with (NodeExplorer::process keeps it fixed within a call,
+ * NodeExplorer.cpp:946-969): the cut-parallel phase of exact DDs stops a leaf's minimum once it
+ * is <= that optimalLB, so a lower value returns SGUFP_ERR_ARG. */
 int sgufp_batch_refine(sgufp_ctx *ctx, int n, const int32_t *node_idx, const uint8_t *is_feasibility,
                        const int32_t *cut_index, double optimal_lb);
+
+/* -- one DD at a time: Inavap::RelaxedDDNew (DD.h:797-808) ------------------------------
+ * The C++ API's Inavap::RelaxedDDNew is a batch of one through these calls; any staged node
+ * can be driven this way.  The DD stays resident in the node's slot between calls.
+ *   sgufp_dd_build     buildTree(Node) for every staged node, no cut applied (DD.cpp:3528-3600);
+ *                      sgufp_batch_results then gives the exact flag (isTreeExact) and status
+ *                      SUCCESS (non-exact) / NEEDS_SUBPROBLEM (exact)
+ *   sgufp_dd_apply     applyFeasibilityCut(cut) -> *value 1 / 0 (DD.cpp:3842-3930), or
+ *                      applyOptimalityCut(cut, optimal, ub) -> *value (DD.cpp:3932-4023; the
+ *                      reference ignores ub); the cut as sgufp_cuts_append takes it (keys
+ *                      getKey(q,i,j), first match).  After a call that prunes the node (0, or a
+ *                      value <= optimal) the DD is only good for a new sgufp_dd_build.
+ *   sgufp_dd_solution  getSolution() (DD.cpp:3825-3840): the argmax path under the last cut
+ *                      applied; path holds total_layers entries, *len gets its length
+ *   sgufp_dd_cutset    getCutset(ub) (DD.cpp:4179-4218) of a non-exact DD; the children are
+ *                      then read with sgufp_batch_children_size / sgufp_batch_children (other
+ *                      staged nodes contribute none).  SGUFP_ERR_STATE for an exact tree. */
+int sgufp_dd_build(sgufp_ctx *ctx);
+int sgufp_dd_apply(sgufp_ctx *ctx, int node, int is_feasibility, double rhs, int64_t nnz, const uint64_t *keys,
+                   const double *vals, double optimal, double *value);
+int sgufp_dd_solution(sgufp_ctx *ctx, int node, int16_t *path, int32_t *len);
+int sgufp_dd_cutset(sgufp_ctx *ctx, int node, double ub, int64_t *n_children);
 
 /* Diagnostics of the last relax: wall_clock64 ticks (100 MHz) of each node's wave and
  * the number of batched-sweep restarts (exact single-cut redo after pruning).  Ticks and
@@ -243,6 +268,15 @@ int sgufp_cuts_rows(sgufp_ctx *ctx, int is_feasibility, int first, int count, do
 int sgufp_comm_unique_id(uint8_t *id, int bytes);
 int sgufp_comm_init(sgufp_ctx *ctx, int world, int rank, const uint8_t *id);
 int sgufp_comm_info(const sgufp_ctx *ctx, int *world, int *rank);
+/* The same exchanges between `world` contexts of ONE process, each driven by its own host
+ * thread (several shards on one GPU; tests of the multi-shard protocol on one card): a group
+ * handle, then sgufp_comm_init_loopback on every context with its rank.  Collectives become
+ * device-to-device copies between two barriers; every rank must make the same calls in the
+ * same order (a rank that stops makes the others fail after 300 s instead of hanging). */
+typedef struct sgufp_loopback sgufp_loopback;
+sgufp_loopback *sgufp_loopback_create(int world);
+void sgufp_loopback_destroy(sgufp_loopback *group);   /* after sgufp_comm_destroy / sgufp_destroy of its contexts */
+int sgufp_comm_init_loopback(sgufp_ctx *ctx, sgufp_loopback *group, int rank);
 void sgufp_comm_destroy(sgufp_ctx *ctx);
 /* *inout := max over the shards (replaces the CAS-max, DDSolver.cpp:723-731). */
 int sgufp_incumbent_allreduce(sgufp_ctx *ctx, double *inout);

@@ -20,6 +20,8 @@
 //                  (every node, static work queue over threads; timing JSON on stdout,
 //                   results in node order as "relax" writes them: CPU baseline + parity)
 //   ref_dd apply  <network> <cuts> <nodes> <out>     (per-cut trace, exact/non-exact alike)
+//   ref_dd api    <network> <cuts> <nodes> <incumbent-hex> <out>
+//                  (RelaxedDDNew call by call: values, getSolution, getCutset)
 //   ref_dd restricted <network> <cuts> <nodes> <incumbent-hex> <width> <out>
 //                  (Inavap::RestrictedDDNew, DD.cpp:3090-3505, under the cut phases of
 //                   NodeExplorer::processX3, NodeExplorer.cpp:605-656)
@@ -389,6 +391,65 @@ int main(int argc, char **argv) {
         for (auto &r : res) write_result(f, r);
         std::fclose(f);
         std::printf("{\"relaxations\": %zu, \"seconds\": %.6f, \"threads\": %d}\n", nodes.size(), el, threads);
+        return 0;
+    }
+    if (mode == "api" && argc == 7) {
+        // The RelaxedDDNew surface one call at a time (DD.h:797-808), as the C++ API's
+        // Inavap::RelaxedDDNew drives the device: buildTree, then every pool cut newest first
+        // in pool order (types interleaved as inserted) with optimalLB = the incumbent, the
+        // value each call returns, getSolution() after every 4th cut and at the end, and for
+        // a non-exact tree getCutset(min(node.ub, returned bounds)) (NodeExplorer.cpp:975-985).
+        // A call that prunes (F 0, or O <= optimalLB) ends the node: NodeExplorer::process
+        // never touches the DD after that.
+        Network net{argv[2]};
+        auto cuts = read_cuts(argv[3]);
+        auto nodes = read_nodes(argv[4]);
+        const double inc = parse_double(argv[5]);
+        Inavap::RelaxedDDNew dd{&net};
+        FILE *f = std::fopen(argv[6], "w");
+        std::fprintf(f, "%zu %zu\n", nodes.size(), cuts.size());
+        auto put_path = [&](const std::vector<int16_t> &p) {
+            std::fprintf(f, "P %zu", p.size());
+            for (auto d : p) std::fprintf(f, " %d", (int)d);
+            std::fprintf(f, "\n");
+        };
+        for (auto &nd : nodes) {
+            dd.buildTree(nd);
+            const int exact = dd.isTreeExact() ? 1 : 0;
+            double ub = nd.ub;
+            bool pruned = false;
+            std::vector<std::string> vals;
+            std::vector<std::vector<int16_t>> sols;
+            size_t applied = 0;
+            for (size_t k = cuts.size(); k-- > 0 && !pruned;) {
+                char buf[64];
+                if (cuts[k].type == 1) {
+                    const int ok = dd.applyFeasibilityCut(cuts[k].cut);
+                    std::snprintf(buf, sizeof buf, "F%d", ok);
+                    pruned = !ok;
+                } else {
+                    const double v = dd.applyOptimalityCut(cuts[k].cut, inc, ub);
+                    std::snprintf(buf, sizeof buf, "O%a", v);
+                    ub = exact ? v : std::min(v, ub);
+                    pruned = v <= inc;
+                }
+                vals.emplace_back(buf);
+                applied++;
+                if (!pruned && applied % 4 == 0) sols.push_back(dd.getSolution());
+            }
+            std::fprintf(f, "N %d %zu %zu\n", exact, applied, sols.size());
+            std::fprintf(f, "V");
+            for (auto &v : vals) std::fprintf(f, " %s", v.c_str());
+            std::fprintf(f, "\n");
+            for (auto &p : sols) put_path(p);
+            if (pruned) { std::fprintf(f, "E 0\n"); continue; }
+            put_path(dd.getSolution());
+            if (exact) { std::fprintf(f, "E 1\n"); continue; }
+            auto ch = dd.getCutset(ub);
+            std::fprintf(f, "C %a %zu\n", ub, ch.size());
+            for (auto &c : ch) write_node(f, c);
+        }
+        std::fclose(f);
         return 0;
     }
     if (mode == "apply" && argc == 6) {

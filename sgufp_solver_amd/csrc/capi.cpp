@@ -286,8 +286,31 @@ bool sgufp_ctx::exact_prepare() {
     if (!ex.enabled) return true;
     const size_t rows_c = (size_t)net.n_slots + 2;
     if (no > ocap) {
-        const int cap = std::max(no, std::max(2 * ocap, 256));
+        int cap = std::max(no, std::max(2 * ocap, 256));
+        // footprint (n_slots + 2 + max_batch) x cap doubles: the doubling stops at what fits in
+        // half of the free device memory; a pool past that leaves the exact DDs to k_relax's own
+        // in-order sweeps (same results) instead of failing the search
+        size_t fr = 0, tot = 0;
+        const size_t per_col = (rows_c + (size_t)max_batch) * sizeof(double);
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+            const size_t have = (size_t)ocap * per_col;   // released when the copy is done
+            const size_t fit = (fr + have) / 2 / per_col;
+            if ((size_t)cap > fit) cap = (int)std::max<size_t>((size_t)no, fit);
+            if ((size_t)no > fit) {
+                ex.enabled = 0;
+                exact_capped = true;
+                return true;
+            }
+        }
         double *c = nullptr, *r = nullptr;
+        if (hipMalloc((void **)&c, rows_c * cap * sizeof(double)) != hipSuccess) {
+            (void)hipGetLastError();
+            ex.enabled = 0;
+            exact_capped = true;
+            return true;
+        }
+        (void)hipFree(c);
+        c = nullptr;
         if (!alloc(c, rows_c * cap, "exact coefO")) return false;
         if (o_built && !hip_ok(hipMemcpy2DAsync(c, (size_t)cap * 8, d_coefO, (size_t)ocap * 8, (size_t)o_built * 8, rows_c,
                                                 hipMemcpyDeviceToDevice, stream), "D2D 2D"))
@@ -338,6 +361,7 @@ bool sgufp_ctx::exact_prepare() {
 
 bool sgufp_ctx::relax_current(double optimal_lb) {
     if (!push_orders() || !exact_prepare()) return false;
+    relax_lb = optimal_lb;
     BatchIn in = cur;
     if (!relax_order(in)) return false;
     const Pool p = pool();
@@ -345,6 +369,11 @@ bool sgufp_ctx::relax_current(double optimal_lb) {
     if (timing) hipEventRecord(ev[0], st);
     if (!hip_ok(launch_relax(nd, sc, in, p, out, optimal_lb, cb, ex, cus, st), "k_relax")) return false;
     if (timing) hipEventRecord(ev[1], st);
+    return emit_current(in, p);
+}
+
+bool sgufp_ctx::emit_current(const BatchIn &in, const Pool &p) {
+    hipStream_t st = stream;
     if (in.n > 0 && !hip_ok(launch_scan(out.nchild, out.sol_need, in.n, d_coff, d_soff, st), "k_scan2")) return false;
     uint64_t tot[2] = {0, 0};
     if (in.n > 0) {
@@ -518,29 +547,37 @@ int sgufp_probe_network(const char *path, int32_t *total_layers, int32_t *n_vbar
     return SGUFP_OK;
 }
 
+// One cut's (key, value) list -> dense row of n_slots + 1 doubles (the last slot 0: absent key)
+int sgufp_ctx::densify(int64_t nnz, const uint64_t *keys, const double *vals, double *row) {
+    const size_t stride = (size_t)net.n_slots + 1;
+    std::fill(row, row + stride, 0.0);
+    std::vector<uint8_t> seen(stride, 0);
+    for (int64_t k = 0; k < nnz; k++) {
+        uint64_t key = keys[k] & 0xFFFFFFFFFFFFull;
+        auto it = key_slots.find(key);
+        if (it == key_slots.end()) {
+            err = "cut key is not an (i,q,j) triple of a DD layer";
+            return SGUFP_ERR_KEY;
+        }
+        for (int s : it->second) {
+            if (seen[s]) continue;  // Cut::get returns the first match (Cut.h:278-281)
+            seen[s] = 1;
+            row[s] = vals[k];
+        }
+    }
+    return SGUFP_OK;
+}
+
 int sgufp_cuts_append(sgufp_ctx *ctx, int is_feasibility, int n_cuts, const double *rhs, const int64_t *nnz_off,
                       const uint64_t *keys, const double *vals) {
     if (!ctx || n_cuts < 0 || (n_cuts && (!rhs || !nnz_off))) return SGUFP_ERR_ARG;
     if (n_cuts == 0) return SGUFP_OK;
     const size_t stride = (size_t)ctx->net.n_slots + 1;
     std::vector<double> rows((size_t)n_cuts * stride, 0.0);
-    std::vector<uint8_t> seen(stride);
     for (int c = 0; c < n_cuts; c++) {
-        std::fill(seen.begin(), seen.end(), 0);
-        double *row = rows.data() + (size_t)c * stride;
-        for (int64_t k = nnz_off[c]; k < nnz_off[c + 1]; k++) {
-            uint64_t key = keys[k] & 0xFFFFFFFFFFFFull;
-            auto it = ctx->key_slots.find(key);
-            if (it == ctx->key_slots.end()) {
-                ctx->err = "cut key is not an (i,q,j) triple of a DD layer";
-                return SGUFP_ERR_KEY;
-            }
-            for (int s : it->second) {
-                if (seen[s]) continue;  // Cut::get returns the first match (Cut.h:278-281)
-                seen[s] = 1;
-                row[s] = vals[k];
-            }
-        }
+        const int rc = ctx->densify(nnz_off[c + 1] - nnz_off[c], keys + nnz_off[c], vals + nnz_off[c],
+                                    rows.data() + (size_t)c * stride);
+        if (rc != SGUFP_OK) return rc;
     }
     return ctx->append_rows(is_feasibility, n_cuts, rhs, rows) ? SGUFP_OK : SGUFP_ERR_HIP;
 }
@@ -831,7 +868,79 @@ int sgufp_batch_upload(sgufp_ctx *ctx, int n, const uint16_t *gl, const double *
         return SGUFP_ERR_HIP;
     ctx->cur = ctx->staged();
     ctx->relaxed = false;
+    ctx->dd_built = false;
     ctx->restricted_done = false;   // sgufp_restricted_* results belong to the previous batch
+    return SGUFP_OK;
+}
+
+// ---- one DD at a time: Inavap::RelaxedDDNew (DD.h:797-808) -------------------------------
+int sgufp_dd_build(sgufp_ctx *ctx) {
+    if (!ctx) return SGUFP_ERR_ARG;
+    const size_t stride = (size_t)ctx->net.n_slots + 1;
+    if (!ctx->d_ddrow && (!ctx->alloc(ctx->d_ddrow, (size_t)ctx->max_batch * stride, "dd rows") ||
+                          !ctx->alloc(ctx->d_ddval, 1, "dd value")))
+        return SGUFP_ERR_HIP;
+    BatchIn in = ctx->cur;
+    in.bound_prune = 0;
+    in.perm = nullptr;
+    if (!ctx->hip_ok(launch_dd_build(ctx->nd, ctx->sc, in, ctx->out, (int)stride, ctx->stream), "k_relax (build)") ||
+        !ctx->sync())
+        return SGUFP_ERR_HIP;
+    ctx->total_children = 0;
+    ctx->total_csol = 0;
+    ctx->relaxed = true;   // sgufp_batch_results: SUCCESS (non-exact) / NEEDS_SUBPROBLEM (exact), exact flag
+    ctx->dd_built = true;
+    return SGUFP_OK;
+}
+
+int sgufp_dd_apply(sgufp_ctx *ctx, int node, int is_feasibility, double rhs, int64_t nnz, const uint64_t *keys,
+                   const double *vals, double optimal, double *value) {
+    if (!ctx || !ctx->dd_built || node < 0 || node >= ctx->n || nnz < 0 || (nnz && (!keys || !vals)) || !value)
+        return ctx && !ctx->dd_built ? SGUFP_ERR_STATE : SGUFP_ERR_ARG;
+    const size_t stride = (size_t)ctx->net.n_slots + 1;
+    std::vector<double> row(stride);
+    const int rc = ctx->densify(nnz, keys, vals, row.data());
+    if (rc != SGUFP_OK) return rc;
+    if (!ctx->upload(ctx->d_ddrow + (size_t)node * stride, row.data(), stride) ||
+        !ctx->hip_ok(launch_dd_apply(ctx->nd, ctx->sc, ctx->cur, ctx->out, node, ctx->d_ddrow, (int)stride, rhs,
+                                     is_feasibility ? 1 : 0, optimal, ctx->d_ddval, ctx->stream),
+                     "k_dd_apply") ||
+        !ctx->download(value, ctx->d_ddval, 1) || !ctx->sync())
+        return SGUFP_ERR_HIP;
+    return SGUFP_OK;
+}
+
+int sgufp_dd_solution(sgufp_ctx *ctx, int node, int16_t *path, int32_t *len) {
+    if (!ctx || !ctx->dd_built || node < 0 || node >= ctx->n || !len)
+        return ctx && !ctx->dd_built ? SGUFP_ERR_STATE : SGUFP_ERR_ARG;
+    const int stride = ctx->net.n_slots + 1;
+    uint16_t pl = 0;
+    if (!ctx->hip_ok(launch_dd_solution(ctx->nd, ctx->sc, ctx->cur, ctx->out, node, ctx->d_ddrow, stride, ctx->stream),
+                     "k_dd_solution") ||
+        !ctx->download(&pl, ctx->out.path_len + node, 1) || !ctx->sync())
+        return SGUFP_ERR_HIP;
+    *len = pl;
+    if (path && (!ctx->download(path, ctx->out.path + (size_t)node * ctx->sc.Lcap, pl) || !ctx->sync()))
+        return SGUFP_ERR_HIP;
+    return SGUFP_OK;
+}
+
+int sgufp_dd_cutset(sgufp_ctx *ctx, int node, double ub, int64_t *n_children) {
+    if (!ctx || !ctx->dd_built || node < 0 || node >= ctx->n)
+        return ctx && !ctx->dd_built ? SGUFP_ERR_STATE : SGUFP_ERR_ARG;
+    int32_t st = 0;
+    Pool p = ctx->pool();
+    p.rows = ctx->d_ddrow;   // the slot's own row (k_dd_apply keeps meta last_cut = slot)
+    if (!ctx->hip_ok(hipMemsetAsync(ctx->out.nchild, 0, (size_t)ctx->n * sizeof(uint32_t), ctx->stream), "memset") ||
+        !ctx->hip_ok(hipMemsetAsync(ctx->out.sol_need, 0, (size_t)ctx->n * sizeof(uint32_t), ctx->stream), "memset") ||
+        !ctx->hip_ok(launch_dd_cutset(ctx->nd, ctx->sc, ctx->out, node, ub, ctx->stream), "k_dd_cutset") ||
+        !ctx->emit_current(ctx->cur, p) || !ctx->download(&st, ctx->out.status + node, 1) || !ctx->sync())
+        return SGUFP_ERR_HIP;
+    if (st != SGUFP_SUCCESS) {
+        ctx->err = "getCutset: the DD has no width-1 layer at index >= 3 (an exact tree)";
+        return SGUFP_ERR_STATE;
+    }
+    if (n_children) *n_children = ctx->total_children;
     return SGUFP_OK;
 }
 
@@ -964,6 +1073,12 @@ int sgufp_batch_refine(sgufp_ctx *ctx, int n, const int32_t *node_idx, const uin
     if (!ctx || !ctx->relaxed || n < 0 || n > ctx->max_batch || (n && (!node_idx || !is_feasibility || !cut_index)))
         return SGUFP_ERR_ARG;
     if (n == 0) return SGUFP_OK;
+    if (ctx->ex.enabled && optimal_lb < ctx->relax_lb) {
+        // the cut-parallel phase left partial leaf minima (upper bounds, all <= the relax-time
+        // optimalLB) as terminal weights; a lower optimalLB could make one of them the argmax
+        ctx->err = "sgufp_batch_refine: optimal_lb below the batch's relaxation incumbent";
+        return SGUFP_ERR_ARG;
+    }
     std::vector<int32_t> rows(n);
     for (int k = 0; k < n; k++) {
         const auto &v = is_feasibility[k] ? ctx->f_rows : ctx->o_rows;

@@ -21,6 +21,7 @@
 #include "rdd_device.hpp"
 
 namespace sgufp {
+struct Transport;   // shard.cpp
 // dd_kernels.hip
 size_t relax_lds_bytes(int Tcap, int Lcap, int cb, int us);
 size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw, int kbytes = 8);
@@ -39,6 +40,13 @@ hipError_t launch_gather_paths(const BatchOut &, int Lcap, const int32_t *idx, c
                                int16_t *dst, hipStream_t);
 hipError_t launch_push_children(const ChildOut &, const BatchOut &, const int32_t *parents, const int64_t *dst_child,
                                 const int64_t *dst_sol, int n, const FrontierDev &, hipStream_t);
+// one DD at a time (RelaxedDDNew surface): build without cuts, one cut, argmax path, cutset
+hipError_t launch_dd_build(const NetDev &, const Scratch &, const BatchIn &, const BatchOut &, int stride, hipStream_t);
+hipError_t launch_dd_apply(const NetDev &, const Scratch &, const BatchIn &, const BatchOut &, int slot, const double *rows,
+                           int stride, double rhs, int is_feas, double optimal, double *value, hipStream_t);
+hipError_t launch_dd_solution(const NetDev &, const Scratch &, const BatchIn &, const BatchOut &, int slot,
+                              const double *rows, int stride, hipStream_t);
+hipError_t launch_dd_cutset(const NetDev &, const Scratch &, const BatchOut &, int slot, double ub, hipStream_t);
 // 1 when k_relax was built with its per-wave clock stamps (SGUFP_PHASES, lib_prof/)
 bool relax_has_phases();
 // rdd_kernels.hip
@@ -163,6 +171,14 @@ struct sgufp_ctx {
     int16_t *d_csol = nullptr;
     int64_t total_children = 0, total_csol = 0;
     bool relaxed = false;
+    double relax_lb = 0.0;       // optimalLB of the last relaxation (sgufp_batch_refine may not go lower)
+    bool exact_capped = false;   // the exact phase's column store outgrew device memory: k_relax sweeps
+
+    // one DD at a time (sgufp_dd_*): per staged slot, the dense row of the last cut applied
+    bool dd_built = false;
+    double *d_ddrow = nullptr, *d_ddval = nullptr;
+    bool emit_current(const BatchIn &in, const Pool &p);   // scan + k_emit_children of the batch
+    int densify(int64_t nnz, const uint64_t *keys, const double *vals, double *row);   // cutToCut + Cut::get
 
     // refine staging
     int32_t *d_rslots = nullptr, *d_rcuts = nullptr;
@@ -187,8 +203,10 @@ struct sgufp_ctx {
     RddIO rio{};
     bool rdd_init();
 
-    // frontier shards over RCCL (shard.cpp); comm is an ncclComm_t, nullptr for one shard
-    void *comm = nullptr;
+    // frontier shards (shard.cpp): the exchanges go through a transport -- RCCL between
+    // processes / GPUs, or an in-process loopback between contexts driven by threads of one
+    // process (tests, several shards on one GPU); nullptr for one shard
+    sgufp::Transport *comm = nullptr;
     int world = 1, rank = 0;
     int shared[2] = {0, 0};                   // rows of the optimality [0] / feasibility [1] list
                                               // already exchanged (own rows after that are new)

@@ -2659,7 +2659,8 @@ __global__ void __launch_bounds__(kWave) k_refine(NetDev net, Scratch sc, BatchI
     double ub = sc.ubv[slot];
     if (lane() == 0) out.sweeps[slot] += 1u;
     // flagged (lazy) leaves: the batch's pending index of this record (-1: none flagged)
-    const int pi = (ex.lazy > 0 && d.exact) ? ex.pidx[slot] : -1;
+    // (ex.enabled: a launch without the exact phase leaves pidx of an earlier batch behind)
+    const int pi = (ex.enabled && ex.lazy > 0 && d.exact) ? ex.pidx[slot] : -1;
     if (cut_is_feas[w]) {
         if (!dd_post_feasibility(net, d, row)) status = kPrunedFeasibility;
         else if (pi >= 0) exact_argmax(net, d, ex, pi, incumbent);   // the path below takes the first maximum
@@ -2683,6 +2684,104 @@ __global__ void __launch_bounds__(kWave) k_refine(NetDev net, Scratch sc, BatchI
         out.ub[slot] = ub;
     }
     store_meta_layers(d, sc, slot, id, status, 0, ub);
+}
+
+// ------------------------------------------------------------------------------------
+// One DD at a time: the RelaxedDDNew surface (DD.h:797-808) behind the C++ API's
+// Inavap::RelaxedDDNew.  A staged record is built with no cut applied (k_relax over an empty
+// pool), then each call applies ONE cut to its resident DD -- exact or not, whatever its
+// status -- exactly as the single-cut path of k_relax does (applyFeasibilityCut DD.cpp:3842-3930,
+// applyOptimalityCut :3932-4023), and returns what the reference returns.  The cut's dense row
+// is kept in the slot's own row (rows + slot * stride, meta last_cut = slot) so that
+// getSolution / getCutset read the weights of the last cut applied (DD.cpp:3796-3840).
+__global__ void __launch_bounds__(kWave) k_dd_apply(NetDev net, Scratch sc, BatchIn in, BatchOut out, int slot,
+                                                    const double *rows, int stride, double rhs, int is_feas,
+                                                    double optimal, double *value) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
+    DD d;
+    dd_bind(d, smem, sc, slot);
+    load_meta_layers(d, sc, slot);
+    const GBL int32_t *meta = sc.meta + (size_t)slot * 8;
+    const int status = uni(meta[6]), cut_layer = uni(meta[7]);
+    const double ub = sc.ubv[slot];
+    const GBL int16_t *rsol = in.sol + in.sol_off[slot];
+    for (int t = lane(); t < d.len; t += kWave) {
+        int dec = rsol[t];
+        int s = -1;
+        if (dec != -1) {
+            s = net.n_slots;
+            if (dec >= 0 && dec < net.m) {
+                int j = net.arc_head[dec];
+                for (int q = net.slot_off[t]; q < net.slot_off[t + 1]; q++)
+                    if (net.slot_head[q] == j) { s = q; break; }
+            }
+        }
+        d.rslot[t] = (int16_t)s;
+    }
+    wave_lds_sync();
+    const GBL double *row = (const GBL double *)(rows + (size_t)slot * stride);
+    dd_sweep(net, d, row, root_fold(row, rhs, d));
+    double v;
+    if (is_feas) v = dd_post_feasibility(net, d, row) ? 1.0 : 0.0;
+    else v = dd_post_optimality(net, d, row, optimal);
+    if (lane() == 0) {
+        value[0] = v;
+        out.sweeps[slot] += 1u;
+    }
+    store_meta_layers(d, sc, slot, slot, status, cut_layer, ub);
+}
+
+// getSolution (DD.cpp:3825-3840): argmax terminal weight, first-match walk of the last cut
+__global__ void __launch_bounds__(kWave) k_dd_solution(NetDev net, Scratch sc, BatchIn in, BatchOut out, int slot,
+                                                       const double *rows, int stride) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
+    DD d;
+    dd_bind(d, smem, sc, slot);
+    load_meta_layers(d, sc, slot);
+    const int last = uni(sc.meta[(size_t)slot * 8 + 5]);
+    const GBL double *row = last >= 0 ? (const GBL double *)(rows + (size_t)last * stride) : nullptr;
+    const GBL int16_t *rsol = in.sol + in.sol_off[slot];
+    const int plen = dd_solution_path(net, d, row, out.path + (size_t)slot * sc.Lcap, rsol);
+    if (lane() == 0) out.path_len[slot] = (uint16_t)plen;
+}
+
+// getCutset(ub) (DD.cpp:4179-4218): the first width-1 layer at index >= 3 and the alive
+// in-arcs of its node; k_emit_children writes them (status SUCCESS, nchild, cut layer)
+__global__ void __launch_bounds__(kWave) k_dd_cutset(NetDev net, Scratch sc, BatchOut out, int slot, double ub) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
+    DD d;
+    dd_bind(d, smem, sc, slot);
+    load_meta_layers(d, sc, slot);
+    const int last = uni(sc.meta[(size_t)slot * 8 + 5]);
+    int status = kSuccess, k = 3;
+    uint32_t nchild = 0;
+    while (k < d.T && uni(d.nalive[k]) != 1) k++;
+    if (d.exact || k >= d.T) {
+        status = kErrCutset;   // a tree has no merged layer (the reference would run off its layers)
+        k = 0;
+    } else {
+        const uint32_t M = layer_single(d, k);
+        if (uni(d.acnt[k])) {
+            const uint32_t aoff = uni(d.aoff[k]), acnt = uni(d.acnt[k]);
+            for (uint32_t base = 0; base < acnt; base += kWave) {
+                uint32_t a = base + lane();
+                nchild += wave_sum((a < acnt && (d.aflag[aoff + a] & kAlive)) ? 1u : 0u);
+            }
+        } else {
+            nchild = (d.nflag[M] & kInAlive) ? 1u : 0u;
+        }
+    }
+    if (lane() == 0) {
+        out.status[slot] = status;
+        out.lb[slot] = DMIN;
+        out.ub[slot] = ub;
+        out.nchild[slot] = nchild;
+        out.sol_need[slot] = nchild * (uint32_t)(d.len + k);
+    }
+    store_meta_layers(d, sc, slot, last, status, k, ub);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2795,6 +2894,41 @@ bool relax_has_phases() {
 #else
     return false;
 #endif
+}
+
+// RelaxedDDNew one DD at a time (k_dd_*): build without cuts, apply one cut, path, cutset
+hipError_t launch_dd_build(const NetDev &net, const Scratch &sc, const BatchIn &in, const BatchOut &out, int stride,
+                           hipStream_t st) {
+    if (in.n <= 0) return hipSuccess;
+    Pool none{};
+    none.stride = stride;
+    none.ustride = 1;
+    ExactIO ex{};
+    hipLaunchKernelGGL(k_relax<1>, dim3(in.n), dim3(kWave), relax_lds_bytes(sc.Tcap, sc.Lcap, 1, sc.us), st, net, sc,
+                       in, none, out, DMIN, ex);
+    return hipGetLastError();
+}
+
+hipError_t launch_dd_apply(const NetDev &net, const Scratch &sc, const BatchIn &in, const BatchOut &out, int slot,
+                           const double *rows, int stride, double rhs, int is_feas, double optimal, double *value,
+                           hipStream_t st) {
+    hipLaunchKernelGGL(k_dd_apply, dim3(1), dim3(kWave), relax_lds_bytes(sc.Tcap, sc.Lcap, 1, sc.us), st, net, sc, in,
+                       out, slot, rows, stride, rhs, is_feas, optimal, value);
+    return hipGetLastError();
+}
+
+hipError_t launch_dd_solution(const NetDev &net, const Scratch &sc, const BatchIn &in, const BatchOut &out, int slot,
+                              const double *rows, int stride, hipStream_t st) {
+    hipLaunchKernelGGL(k_dd_solution, dim3(1), dim3(kWave), relax_lds_bytes(sc.Tcap, sc.Lcap, 1, sc.us), st, net, sc,
+                       in, out, slot, rows, stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_dd_cutset(const NetDev &net, const Scratch &sc, const BatchOut &out, int slot, double ub,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(k_dd_cutset, dim3(1), dim3(kWave), relax_lds_bytes(sc.Tcap, sc.Lcap, 1, sc.us), st, net, sc,
+                       out, slot, ub);
+    return hipGetLastError();
 }
 
 hipError_t launch_refine(const NetDev &net, const Scratch &sc, const BatchIn &in, const Pool &pool,

@@ -48,6 +48,87 @@ void Device::check(int rc, const char *what) const {
     if (rc != SGUFP_OK) throw sgufp_error(std::string(what) + ": " + sgufp_last_error(ctx_));
 }
 
+// ---- RelaxedDDNew: one device slot ---------------------------------------------------------
+RelaxedDDNew::RelaxedDDNew(const Network *pointer) : networkPtr{pointer}, dev{new Device(*pointer, 1)} {}
+
+void RelaxedDDNew::buildTree(Node root) {
+    sgufp_ctx *g = dev->get();
+    uint16_t gl = root.globalLayer;
+    int64_t so[2] = {0, (int64_t)root.states.size()}, po[2] = {0, (int64_t)root.solutionVector.size()};
+    static const int16_t empty = 0;
+    dev->check(sgufp_batch_upload(g, 1, &gl, &root.lb, &root.ub, so, root.states.empty() ? &empty : root.states.data(),
+                                  po, root.solutionVector.empty() ? &empty : root.solutionVector.data()),
+               "buildTree upload");
+    dev->check(sgufp_dd_build(g), "buildTree");
+    int32_t st = 0;
+    uint8_t ex = 0;
+    dev->check(sgufp_batch_results(g, &st, &ex, nullptr, nullptr, nullptr), "buildTree results");
+    if (st != SGUFP_SUCCESS && st != SGUFP_NEEDS_SUBPROBLEM)
+        throw sgufp_error("buildTree: record rejected by the device (status " + std::to_string(st) + ")");
+    exact = ex != 0;
+    built = true;
+}
+
+void RelaxedDDNew::upload_cut(const Cut &cut, std::vector<uint64_t> &keys, std::vector<double> &vals) const {
+    if (!built) throw sgufp_error("RelaxedDDNew: buildTree first");
+    keys.clear();
+    vals.clear();
+    for (auto &[k, v] : cut.coeff) {
+        keys.push_back(k);
+        vals.push_back(v);
+    }
+}
+
+uint8_t RelaxedDDNew::applyFeasibilityCut(const Cut &cut) {
+    std::vector<uint64_t> keys;
+    std::vector<double> vals;
+    upload_cut(cut, keys, vals);
+    double v = 0.0;
+    dev->check(sgufp_dd_apply(dev->get(), 0, 1, cut.RHS, (int64_t)keys.size(), keys.data(), vals.data(), DOUBLE_MIN, &v),
+               "applyFeasibilityCut");
+    return v != 0.0 ? 1 : 0;
+}
+
+double RelaxedDDNew::applyOptimalityCut(const Cut &cut, double optimal, double /*upperbound: unused, DD.cpp:3932*/) {
+    std::vector<uint64_t> keys;
+    std::vector<double> vals;
+    upload_cut(cut, keys, vals);
+    double v = 0.0;
+    dev->check(sgufp_dd_apply(dev->get(), 0, 0, cut.RHS, (int64_t)keys.size(), keys.data(), vals.data(), optimal, &v),
+               "applyOptimalityCut");
+    return v;
+}
+
+Path RelaxedDDNew::getSolution() const {
+    if (!built) throw sgufp_error("RelaxedDDNew: buildTree first");
+    Path p((size_t)std::max(networkPtr->totalLayers, 1));
+    int32_t len = 0;
+    dev->check(sgufp_dd_solution(dev->get(), 0, p.data(), &len), "getSolution");
+    p.resize((size_t)len);
+    return p;
+}
+
+std::vector<Node> RelaxedDDNew::getCutset(double ub) {
+    if (!built) throw sgufp_error("RelaxedDDNew: buildTree first");
+    sgufp_ctx *g = dev->get();
+    int64_t n = 0, ns = 0, nsol = 0;
+    dev->check(sgufp_dd_cutset(g, 0, ub, &n), "getCutset");
+    dev->check(sgufp_batch_children_size(g, &n, &ns, &nsol), "getCutset size");
+    std::vector<int64_t> coff(2), soff(n + 1), poff(n + 1);
+    std::vector<uint16_t> cg(n + 1);
+    std::vector<double> cl(n + 1), cu(n + 1);
+    std::vector<int16_t> st(ns + 1), sol(nsol + 1);
+    dev->check(sgufp_batch_children(g, coff.data(), cg.data(), cl.data(), cu.data(), soff.data(), st.data(), poff.data(),
+                                    sol.data()),
+               "getCutset children");
+    std::vector<Node> out;
+    out.reserve((size_t)n);
+    for (int64_t c = 0; c < n; c++)
+        out.emplace_back(std::vector<int16_t>(st.begin() + soff[c], st.begin() + soff[c + 1]),
+                         std::vector<int16_t>(sol.begin() + poff[c], sol.begin() + poff[c + 1]), cl[c], cu[c], cg[c]);
+    return out;
+}
+
 // ---- scenario subproblem -------------------------------------------------------------------
 GuroSolver::GuroSolver(const std::shared_ptr<Network> &networkPtr) : net{networkPtr}, dev{*networkPtr, 1} {
     sgufp_network_info info{};

@@ -20,10 +20,22 @@
 //                               records in contiguous chunks, sent field by field straight
 //                               from / into the SoA frontier arrays (ncclSend / ncclRecv).
 // The same plan is computed by sgufp_solver_amd/shards.py (the torch.distributed driver).
+//
+// The collectives go through a Transport: RCCL (one context per GPU / process, the production
+// path) or an in-process loopback between contexts of one process driven by one host thread
+// each (sgufp_comm_init_loopback: device-to-device copies on the contexts' streams between two
+// barriers), which runs this very code -- plan, packing, rebase, drop-bottom, row append -- with
+// W > 1 shards on a single GPU.
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include "ctx.hpp"
@@ -87,10 +99,169 @@ bool grow(sgufp_ctx *ctx, T *&p, size_t &cap, size_t need, const char *what) {
 
 }  // namespace
 
+namespace sgufp {
+
+// The four collectives of the shard protocol, on device buffers of the calling context's
+// stream.  Every rank calls them in the same order.
+struct Transport {
+    virtual ~Transport() = default;
+    virtual bool allreduce_max_f64(sgufp_ctx *ctx, double *d) = 0;                      // one f64, in place
+    virtual bool allgather(sgufp_ctx *ctx, const void *send, void *recv, size_t bytes) = 0;   // recv [world][bytes]
+    virtual bool group_start(sgufp_ctx *ctx) = 0;                                        // point-to-point group
+    virtual bool send(sgufp_ctx *ctx, const void *p, size_t bytes, int peer) = 0;
+    virtual bool recv(sgufp_ctx *ctx, void *p, size_t bytes, int peer) = 0;
+    virtual bool group_end(sgufp_ctx *ctx) = 0;
+};
+
+struct RcclTransport : Transport {
+    ncclComm_t c;
+    ncclResult_t pending = ncclSuccess;
+    explicit RcclTransport(ncclComm_t c_) : c{c_} {}
+    ~RcclTransport() override { (void)ncclCommDestroy(c); }
+    bool allreduce_max_f64(sgufp_ctx *ctx, double *d) override {
+        return nccl_ok(ctx, ncclAllReduce(d, d, 1, ncclFloat64, ncclMax, c, ctx->stream), "ncclAllReduce");
+    }
+    bool allgather(sgufp_ctx *ctx, const void *send, void *recv, size_t bytes) override {
+        return nccl_ok(ctx, ncclAllGather(send, recv, bytes, ncclUint8, c, ctx->stream), "ncclAllGather");
+    }
+    bool group_start(sgufp_ctx *ctx) override {
+        pending = ncclSuccess;
+        return nccl_ok(ctx, ncclGroupStart(), "ncclGroupStart");
+    }
+    bool send(sgufp_ctx *ctx, const void *p, size_t bytes, int peer) override {
+        if (bytes && pending == ncclSuccess) pending = ncclSend(p, bytes, ncclUint8, peer, c, ctx->stream);
+        return true;
+    }
+    bool recv(sgufp_ctx *ctx, void *p, size_t bytes, int peer) override {
+        if (bytes && pending == ncclSuccess) pending = ncclRecv(p, bytes, ncclUint8, peer, c, ctx->stream);
+        return true;
+    }
+    bool group_end(sgufp_ctx *ctx) override {
+        const ncclResult_t re = ncclGroupEnd();
+        return nccl_ok(ctx, pending, "ncclSend/ncclRecv") && nccl_ok(ctx, re, "ncclGroupEnd");
+    }
+};
+
+// Shared state of the loopback shards: a generation barrier (with a time limit, so that a
+// rank that stops calling fails the others instead of hanging them), published pointers /
+// values, and per (from, to) queues of posted sends.
+struct LoopGroup {
+    int world;
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    bool broken = false;
+    std::vector<const void *> ptr;
+    std::vector<double> val;
+    std::vector<std::deque<std::pair<const void *, size_t>>> q;   // [from * world + to]
+    explicit LoopGroup(int w) : world{w}, ptr(w, nullptr), val(w, 0.0), q((size_t)w * w) {}
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(m);
+        if (broken) return false;
+        const uint64_t g = gen;
+        if (++arrived == world) {
+            arrived = 0;
+            gen++;
+            cv.notify_all();
+            return true;
+        }
+        static const int secs = [] {
+            const char *e = std::getenv("SGUFP_LOOPBACK_TIMEOUT");   // seconds a rank waits for the others
+            return e && std::atoi(e) > 0 ? std::atoi(e) : 300;
+        }();
+        if (!cv.wait_for(lk, std::chrono::seconds(secs), [&] { return gen != g || broken; }) || broken) {
+            broken = true;
+            cv.notify_all();
+            return false;
+        }
+        return true;
+    }
+};
+
+struct LoopbackTransport : Transport {
+    std::shared_ptr<LoopGroup> g;
+    int rank;
+    std::vector<std::pair<void *, std::pair<size_t, int>>> recvs;
+    std::vector<std::pair<const void *, std::pair<size_t, int>>> sends;
+    LoopbackTransport(std::shared_ptr<LoopGroup> g_, int r) : g{std::move(g_)}, rank{r} {}
+    bool fail(sgufp_ctx *ctx, const char *what) {
+        ctx->err = std::string("loopback transport: ") + what;
+        std::lock_guard<std::mutex> lk(g->m);
+        g->broken = true;
+        g->cv.notify_all();
+        return false;
+    }
+    bool allreduce_max_f64(sgufp_ctx *ctx, double *d) override {
+        double v = 0.0;
+        if (!ctx->download(&v, d, 1) || !ctx->sync()) return false;
+        g->val[rank] = v;
+        if (!g->barrier()) return fail(ctx, "barrier");
+        double mx = g->val[0];
+        for (int r = 1; r < g->world; r++) mx = std::max(mx, g->val[r]);
+        if (!g->barrier()) return fail(ctx, "barrier");
+        return ctx->upload(d, &mx, 1) && ctx->sync();
+    }
+    bool allgather(sgufp_ctx *ctx, const void *send, void *recv, size_t bytes) override {
+        if (!ctx->sync()) return false;   // the send block is complete on this stream
+        g->ptr[rank] = send;
+        if (!g->barrier()) return fail(ctx, "barrier");
+        for (int r = 0; r < g->world && bytes; r++)
+            if (!ctx->hip_ok(hipMemcpyAsync((uint8_t *)recv + (size_t)r * bytes, g->ptr[r], bytes,
+                                            hipMemcpyDeviceToDevice, ctx->stream), "loopback D2D"))
+                return fail(ctx, "copy");
+        if (!ctx->sync()) return fail(ctx, "sync");
+        return g->barrier() || fail(ctx, "barrier");   // every rank copied: send blocks reusable
+    }
+    bool group_start(sgufp_ctx *) override {
+        sends.clear();
+        recvs.clear();
+        return true;
+    }
+    bool send(sgufp_ctx *, const void *p, size_t bytes, int peer) override {
+        if (bytes) sends.push_back({p, {bytes, peer}});
+        return true;
+    }
+    bool recv(sgufp_ctx *, void *p, size_t bytes, int peer) override {
+        if (bytes) recvs.push_back({p, {bytes, peer}});
+        return true;
+    }
+    bool group_end(sgufp_ctx *ctx) override {
+        if (!ctx->sync()) return false;
+        {
+            std::lock_guard<std::mutex> lk(g->m);
+            for (auto &x : sends) g->q[(size_t)rank * g->world + x.second.second].push_back({x.first, x.second.first});
+        }
+        if (!g->barrier()) return fail(ctx, "barrier");
+        for (auto &x : recvs) {
+            std::pair<const void *, size_t> src;
+            {
+                std::lock_guard<std::mutex> lk(g->m);
+                auto &dq = g->q[(size_t)x.second.second * g->world + rank];
+                if (dq.empty()) return fail(ctx, "receive without a matching send");
+                src = dq.front();
+                dq.pop_front();
+            }
+            if (src.second != x.second.first) return fail(ctx, "send / receive sizes differ");
+            if (!ctx->hip_ok(hipMemcpyAsync(x.first, src.first, src.second, hipMemcpyDeviceToDevice, ctx->stream),
+                             "loopback D2D"))
+                return fail(ctx, "copy");
+        }
+        if (!ctx->sync()) return fail(ctx, "sync");
+        return g->barrier() || fail(ctx, "barrier");
+    }
+};
+
+}  // namespace sgufp
+
+struct sgufp_loopback {
+    std::shared_ptr<sgufp::LoopGroup> g;
+};
+
 sgufp_ctx::~sgufp_ctx() {
     if (comm) {
         if (device >= 0) (void)hipSetDevice(device);
-        (void)ncclCommDestroy((ncclComm_t)comm);
+        delete comm;
         comm = nullptr;
     }
     destroy_all();
@@ -143,7 +314,29 @@ int sgufp_comm_init(sgufp_ctx *ctx, int world, int rank, const uint8_t *id) {
     std::memcpy(&u, id, sizeof u);
     ncclComm_t c = nullptr;
     if (!nccl_ok(ctx, ncclCommInitRank(&c, world, u, rank), "ncclCommInitRank")) return SGUFP_ERR_HIP;
-    ctx->comm = c;
+    ctx->comm = new RcclTransport(c);
+    ctx->world = world;
+    ctx->rank = rank;
+    ctx->shared[0] = (int)ctx->o_rows.size();
+    ctx->shared[1] = (int)ctx->f_rows.size();
+    if (!ctx->alloc(ctx->d_comm_i64, (size_t)4 * world + 4, "comm") || !ctx->alloc(ctx->d_comm_f64, 1, "comm"))
+        return SGUFP_ERR_HIP;
+    return SGUFP_OK;
+}
+
+sgufp_loopback *sgufp_loopback_create(int world) {
+    if (world < 1) return nullptr;
+    auto *h = new sgufp_loopback;
+    h->g = std::make_shared<LoopGroup>(world);
+    return h;
+}
+
+void sgufp_loopback_destroy(sgufp_loopback *group) { delete group; }
+
+int sgufp_comm_init_loopback(sgufp_ctx *ctx, sgufp_loopback *group, int rank) {
+    if (!ctx || !group || rank < 0 || rank >= group->g->world || ctx->comm) return SGUFP_ERR_ARG;
+    const int world = group->g->world;
+    ctx->comm = new LoopbackTransport(group->g, rank);
     ctx->world = world;
     ctx->rank = rank;
     ctx->shared[0] = (int)ctx->o_rows.size();
@@ -164,9 +357,7 @@ int sgufp_incumbent_allreduce(sgufp_ctx *ctx, double *inout) {
     if (!ctx || !inout) return SGUFP_ERR_ARG;
     if (!ctx->comm) return SGUFP_OK;   // one shard
     double *d = ctx->d_comm_f64;
-    if (!ctx->upload(d, inout, 1) ||
-        !nccl_ok(ctx, ncclAllReduce(d, d, 1, ncclFloat64, ncclMax, (ncclComm_t)ctx->comm, ctx->stream), "ncclAllReduce") ||
-        !ctx->download(inout, d, 1) || !ctx->sync())
+    if (!ctx->upload(d, inout, 1) || !ctx->comm->allreduce_max_f64(ctx, d) || !ctx->download(inout, d, 1) || !ctx->sync())
         return SGUFP_ERR_HIP;
     return SGUFP_OK;
 }
@@ -177,8 +368,7 @@ static bool allgather_i64(sgufp_ctx *ctx, const int64_t *mine, int k, std::vecto
     int64_t *d = ctx->d_comm_i64;   // [4 * W + 4]: send slot at the end
     int64_t *send = d + (size_t)4 * W;
     all.assign((size_t)W * k, 0);
-    return ctx->upload(send, mine, (size_t)k) &&
-           nccl_ok(ctx, ncclAllGather(send, d, (size_t)k, ncclInt64, (ncclComm_t)ctx->comm, ctx->stream), "ncclAllGather") &&
+    return ctx->upload(send, mine, (size_t)k) && ctx->comm->allgather(ctx, send, d, (size_t)k * sizeof(int64_t)) &&
            ctx->download(all.data(), d, all.size()) && ctx->sync();
 }
 
@@ -221,9 +411,7 @@ int sgufp_cuts_exchange(sgufp_ctx *ctx, int64_t *received) {
                       !ctx->hip_ok(launch_gather_rows(ctx->d_rows, ctx->d_rhs, ctx->d_xids, (int)k, stride, ctx->d_xsend,
                                                       ctx->stream), "k_gather_rows")))
             return SGUFP_ERR_HIP;
-        if (!nccl_ok(ctx, ncclAllGather(ctx->d_xsend, ctx->d_xrecv, block, ncclFloat64, (ncclComm_t)ctx->comm, ctx->stream),
-                     "ncclAllGather"))
-            return SGUFP_ERR_HIP;
+        if (!ctx->comm->allgather(ctx, ctx->d_xsend, ctx->d_xrecv, block * sizeof(double))) return SGUFP_ERR_HIP;
         for (int r = 0; r < W; r++) {
             const int n = (int)ks[r];
             if (r == me || n == 0) continue;
@@ -292,8 +480,7 @@ int sgufp_frontier_balance(sgufp_ctx *ctx, int64_t *received) {
         int64_t *send = ctx->d_xspan + (size_t)per * W;
         all_span.assign((size_t)per * W, 0);
         if (!ctx->upload(send, mine_sp.data(), (size_t)per) ||
-            !nccl_ok(ctx, ncclAllGather(send, ctx->d_xspan, (size_t)per, ncclInt64, (ncclComm_t)ctx->comm, ctx->stream),
-                     "ncclAllGather") ||
+            !ctx->comm->allgather(ctx, send, ctx->d_xspan, (size_t)per * sizeof(int64_t)) ||
             !ctx->download(all_span.data(), ctx->d_xspan, all_span.size()) || !ctx->sync())
             return SGUFP_ERR_HIP;
     }
@@ -316,38 +503,30 @@ int sgufp_frontier_balance(sgufp_ctx *ctx, int64_t *received) {
         if (!ctx->frontier_reserve(e, (size_t)s)) return SGUFP_ERR_HIP;
     }
     FrontierDev &f = ctx->fr;
-    ncclComm_t comm = (ncclComm_t)ctx->comm;
+    Transport *X = ctx->comm;
     hipStream_t st = ctx->stream;
     auto xfer = [&](bool send, void *p, size_t bytes, int peer) {
-        if (bytes == 0) return ncclSuccess;
-        return send ? ncclSend(p, bytes, ncclUint8, peer, comm, st) : ncclRecv(p, bytes, ncclUint8, peer, comm, st);
+        return send ? X->send(ctx, p, bytes, peer) : X->recv(ctx, p, bytes, peer);
     };
     auto fields = [&](bool send, int64_t e, int64_t n, int64_t s, int64_t slen, int peer) {
-        ncclResult_t r = ncclSuccess;
         const size_t k = (size_t)n;
-        if (r == ncclSuccess) r = xfer(send, f.gl + e, k * 2, peer);
-        if (r == ncclSuccess) r = xfer(send, f.lb + e, k * 8, peer);
-        if (r == ncclSuccess) r = xfer(send, f.ub + e, k * 8, peer);
-        if (r == ncclSuccess) r = xfer(send, f.mask + e, k * 4, peer);
-        if (r == ncclSuccess) r = xfer(send, f.valid + e, k, peer);
-        if (r == ncclSuccess) r = xfer(send, f.sol_len + e, k * 2, peer);
-        if (r == ncclSuccess) r = xfer(send, f.sol_off + e, k * 8, peer);
-        if (r == ncclSuccess) r = xfer(send, f.sol + s, (size_t)slen * 2, peer);
-        return r;
+        return xfer(send, f.gl + e, k * 2, peer) && xfer(send, f.lb + e, k * 8, peer) && xfer(send, f.ub + e, k * 8, peer) &&
+               xfer(send, f.mask + e, k * 4, peer) && xfer(send, f.valid + e, k, peer) &&
+               xfer(send, f.sol_len + e, k * 2, peer) && xfer(send, f.sol_off + e, k * 8, peer) &&
+               xfer(send, f.sol + s, (size_t)slen * 2, peer);
     };
-    if (!nccl_ok(ctx, ncclGroupStart(), "ncclGroupStart")) return SGUFP_ERR_HIP;
-    ncclResult_t rc = ncclSuccess;
+    if (!X->group_start(ctx)) return SGUFP_ERR_HIP;
+    bool ok = true;
     if (give[me] > 0) {
-        for (int j = 0; j < ni && rc == ncclSuccess; j++) {
+        for (int j = 0; j < ni && ok; j++) {
             int64_t lo, hi;
             chunk(me, j, lo, hi);
-            if (hi > lo) rc = fields(true, lo, hi - lo, span[2 * j], span[2 * j + 1] - span[2 * j], idle[j]);
+            if (hi > lo) ok = fields(true, lo, hi - lo, span[2 * j], span[2 * j + 1] - span[2 * j], idle[j]);
         }
     }
     for (const In &x : ins)
-        if (rc == ncclSuccess) rc = fields(false, x.e0, x.n, x.s0, x.slen, x.r);
-    const ncclResult_t re = ncclGroupEnd();
-    if (!nccl_ok(ctx, rc, "ncclSend/ncclRecv") || !nccl_ok(ctx, re, "ncclGroupEnd")) return SGUFP_ERR_HIP;
+        if (ok) ok = fields(false, x.e0, x.n, x.s0, x.slen, x.r);
+    if (!X->group_end(ctx) || !ok) return SGUFP_ERR_HIP;
     int64_t got = 0;
     for (const In &x : ins) {
         if (!ctx->hip_ok(launch_rebase(f.sol_off + x.e0, (int)x.n, x.s0 - x.slo, st), "k_rebase")) return SGUFP_ERR_HIP;
@@ -394,7 +573,7 @@ int sgufp_comm_allgather_i64(sgufp_ctx *ctx, const int64_t *mine, int k, int64_t
 
 void sgufp_comm_destroy(sgufp_ctx *ctx) {
     if (!ctx || !ctx->comm) return;
-    (void)ncclCommDestroy((ncclComm_t)ctx->comm);
+    delete ctx->comm;
     ctx->comm = nullptr;
     ctx->world = 1;
     ctx->rank = 0;

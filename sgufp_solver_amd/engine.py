@@ -35,6 +35,8 @@ EXPORTS = [
     "sgufp_comm_info", "sgufp_comm_destroy", "sgufp_incumbent_allreduce", "sgufp_cuts_exchange",
     "sgufp_frontier_sizes", "sgufp_frontier_balance", "sgufp_bnb_set_trace", "sgufp_bnb_trace",
     "sgufp_frontier_peek_size", "sgufp_frontier_peek", "sgufp_balance_plan", "sgufp_comm_allgather_i64",
+    "sgufp_dd_build", "sgufp_dd_apply", "sgufp_dd_solution", "sgufp_dd_cutset",
+    "sgufp_loopback_create", "sgufp_loopback_destroy", "sgufp_comm_init_loopback",
 ]
 
 
@@ -153,8 +155,37 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.sgufp_restricted_paths.argtypes = [P, P, P]
     lib.sgufp_restricted_cutset_size.argtypes = [P, P, P, P]
     lib.sgufp_restricted_cutset.argtypes = [P, P, P, P, P, P, P, P, P]
+    lib.sgufp_loopback_create.restype = P
+    lib.sgufp_loopback_create.argtypes = [C.c_int]
+    lib.sgufp_loopback_destroy.restype = None
+    lib.sgufp_loopback_destroy.argtypes = [P]
+    lib.sgufp_comm_init_loopback.argtypes = [P, P, C.c_int]
+    lib.sgufp_dd_build.argtypes = [P]
+    lib.sgufp_dd_apply.argtypes = [P, C.c_int, C.c_int, C.c_double, C.c_int64, P, P, C.c_double, P]
+    lib.sgufp_dd_solution.argtypes = [P, C.c_int, P, P]
+    lib.sgufp_dd_cutset.argtypes = [P, C.c_int, C.c_double, P]
     _lib = lib
     return lib
+
+
+class LoopbackGroup:
+    """sgufp_loopback_create(world): `world` contexts of this process exchanging through the
+    library's shard protocol with device-to-device copies (Engine.comm_init_loopback)."""
+
+    def __init__(self, world: int):
+        self.lib = load_library()
+        self.world = world
+        self.handle = self.lib.sgufp_loopback_create(int(world))
+        if not self.handle:
+            raise RuntimeError("sgufp_loopback_create failed")
+
+    def close(self):
+        if self.handle:
+            self.lib.sgufp_loopback_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
 
 
 def _ptr(a: Optional[np.ndarray]):
@@ -407,6 +438,36 @@ class Engine:
         ci = np.asarray(cut_index, dtype=np.int32)
         self._check(self.lib.sgufp_batch_refine(self.ctx, len(ni), _ptr(ni), _ptr(fe), _ptr(ci), C.c_double(incumbent)))
 
+    # -- one DD at a time: Inavap::RelaxedDDNew (DD.h:797-808) ----------------
+    def dd_build(self, nodes):
+        """buildTree for each record, no cut applied; returns the exact flags (isTreeExact)."""
+        self.upload(nodes)
+        self._check(self.lib.sgufp_dd_build(self.ctx))
+        _st, ex, _lb, _ub, _nc = self.results_arrays()
+        return ex
+
+    def dd_apply(self, node: int, cut: PoolCut, optimal: float) -> float:
+        """applyFeasibilityCut (1.0 / 0.0) or applyOptimalityCut (the returned bound) of one cut."""
+        keys = np.asarray([key_of(q, i, j) for (i, q, j, _v) in cut.coeff], dtype=np.uint64)
+        vals = np.asarray([v for (_i, _q, _j, v) in cut.coeff], dtype=np.float64)
+        out = np.zeros(1, dtype=np.float64)
+        self._check(self.lib.sgufp_dd_apply(self.ctx, int(node), int(cut.type), C.c_double(cut.rhs), len(keys),
+                                            _ptr(keys), _ptr(vals), C.c_double(optimal), _ptr(out)))
+        return float(out[0])
+
+    def dd_solution(self, node: int) -> List[int]:
+        buf = np.zeros(max(self.info.total_layers, 1), dtype=np.int16)
+        n = C.c_int32(0)
+        self._check(self.lib.sgufp_dd_solution(self.ctx, int(node), _ptr(buf), C.byref(n)))
+        return [int(x) for x in buf[:n.value]]
+
+    def dd_cutset(self, node: int, ub: float) -> List[NodeRecord]:
+        nc = C.c_int64(0)
+        self._check(self.lib.sgufp_dd_cutset(self.ctx, int(node), C.c_double(ub), C.byref(nc)))
+        child_off, gl, clb, cub, soff, states, poff, sol = self.children_arrays()
+        return [NodeRecord(int(gl[c]), float(clb[c]), float(cub[c]), [int(x) for x in states[soff[c]:soff[c + 1]]],
+                           [int(x) for x in sol[poff[c]:poff[c + 1]]]) for c in range(int(nc.value))]
+
     # -- scenario subproblem ---------------------------------------------------
     def slot_keys(self) -> np.ndarray:
         keys = np.zeros(max(self.info.n_slots, 1), dtype=np.uint64)
@@ -581,6 +642,11 @@ class Engine:
     def comm_init(self, world: int, rank: int, uid: bytes):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         self._check(self.lib.sgufp_comm_init(self.ctx, int(world), int(rank), buf))
+
+    def comm_init_loopback(self, group: "LoopbackGroup", rank: int):
+        """This context as shard `rank` of an in-process loopback group (shard.cpp): the
+        library's own exchanges between contexts of this process, one host thread each."""
+        self._check(self.lib.sgufp_comm_init_loopback(self.ctx, group.handle, int(rank)))
 
     def incumbent_allreduce(self, z: float) -> float:
         v = C.c_double(z)

@@ -6,7 +6,11 @@
 // prints "ddsolver <optimum %a>" (Inavap::DDSolver::start, batched device rounds) and
 // "explorer <optimum %a> <processed>" (a single-worker LIFO loop over
 // Inavap::NodeExplorer::process with two global Containers, as Worker::startWorker).
+#include <algorithm>
 #include <cstdio>
+#include <map>
+#include <string>
+#include <tuple>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -15,7 +19,121 @@
 
 #include "sgufp/inavap.hpp"
 
+// "dd" mode: Inavap::RelaxedDDNew call by call, printed as `ref_dd api` prints the
+// reference's (oracle/ref_driver.cpp; tests/test_dd_api.py reads both):
+//   host_api_test dd <network> <cuts> <nodes> <incumbent hex>
+static std::vector<std::pair<int, Inavap::Cut>> read_cuts(const char *path) {
+    FILE *f = std::fopen(path, "r");
+    if (!f) throw std::runtime_error("cannot open cuts");
+    size_t n = 0;
+    if (std::fscanf(f, "%zu", &n) != 1) throw std::runtime_error("bad cuts");
+    std::vector<std::pair<int, Inavap::Cut>> cuts;
+    for (size_t c = 0; c < n; c++) {
+        int type;
+        char rhs[64];
+        size_t nnz;
+        if (std::fscanf(f, "%d %63s %zu", &type, rhs, &nnz) != 3) throw std::runtime_error("bad cut");
+        std::map<std::tuple<int, int, int>, double> m;   // the reference's CutCoefficients map
+        for (size_t k = 0; k < nnz; k++) {
+            int i, q, j;
+            char v[64];
+            if (std::fscanf(f, "%d %d %d %63s", &i, &q, &j, v) != 4) throw std::runtime_error("bad coefficient");
+            m[std::make_tuple(i, q, j)] = std::strtod(v, nullptr);
+        }
+        std::vector<std::pair<uint64_t, double>> coeff;   // cutToCut (Cut.h:406-421): map order, no zeros
+        for (auto &[k, v] : m)
+            if (v != 0.0) coeff.emplace_back(Inavap::getKey(std::get<1>(k), std::get<0>(k), std::get<2>(k)), v);
+        cuts.emplace_back(type, Inavap::Cut{std::strtod(rhs, nullptr), std::move(coeff)});
+    }
+    std::fclose(f);
+    return cuts;
+}
+
+static std::vector<Inavap::Node> read_nodes(const char *path) {
+    FILE *f = std::fopen(path, "r");
+    if (!f) throw std::runtime_error("cannot open nodes");
+    size_t n = 0;
+    if (std::fscanf(f, "%zu", &n) != 1) throw std::runtime_error("bad nodes");
+    std::vector<Inavap::Node> out;
+    for (size_t k = 0; k < n; k++) {
+        int gl;
+        char lb[64], ub[64];
+        size_t ns, nsol;
+        if (std::fscanf(f, "%d %63s %63s %zu", &gl, lb, ub, &ns) != 4) throw std::runtime_error("bad node");
+        std::vector<int16_t> st(ns), sol;
+        for (auto &x : st) { int v; if (std::fscanf(f, "%d", &v) != 1) throw std::runtime_error("bad node"); x = (int16_t)v; }
+        if (std::fscanf(f, "%zu", &nsol) != 1) throw std::runtime_error("bad node");
+        sol.resize(nsol);
+        for (auto &x : sol) { int v; if (std::fscanf(f, "%d", &v) != 1) throw std::runtime_error("bad node"); x = (int16_t)v; }
+        out.emplace_back(std::move(st), std::move(sol), std::strtod(lb, nullptr), std::strtod(ub, nullptr), (uint16_t)gl);
+    }
+    std::fclose(f);
+    return out;
+}
+
+static int dd_mode(char **argv) {
+    Network net(argv[2]);
+    auto cuts = read_cuts(argv[3]);
+    auto nodes = read_nodes(argv[4]);
+    const double inc = std::strtod(argv[5], nullptr);
+    Inavap::RelaxedDDNew dd{&net};
+    std::printf("%zu %zu\n", nodes.size(), cuts.size());
+    auto put_path = [](const Inavap::Path &p) {
+        std::printf("P %zu", p.size());
+        for (auto d : p) std::printf(" %d", (int)d);
+        std::printf("\n");
+    };
+    for (auto &nd : nodes) {
+        dd.buildTree(nd);
+        const int exact = dd.isTreeExact() ? 1 : 0;
+        double ub = nd.ub;
+        bool pruned = false;
+        std::vector<std::string> vals;
+        std::vector<Inavap::Path> sols;
+        for (size_t k = cuts.size(); k-- > 0 && !pruned;) {
+            char buf[64];
+            if (cuts[k].first == 1) {
+                const int ok = dd.applyFeasibilityCut(cuts[k].second);
+                std::snprintf(buf, sizeof buf, "F%d", ok);
+                pruned = !ok;
+            } else {
+                const double v = dd.applyOptimalityCut(cuts[k].second, inc, ub);
+                std::snprintf(buf, sizeof buf, "O%a", v);
+                ub = exact ? v : std::min(v, ub);
+                pruned = v <= inc;
+            }
+            vals.emplace_back(buf);
+            if (!pruned && vals.size() % 4 == 0) sols.push_back(dd.getSolution());
+        }
+        std::printf("N %d %zu %zu\nV", exact, vals.size(), sols.size());
+        for (auto &v : vals) std::printf(" %s", v.c_str());
+        std::printf("\n");
+        for (auto &p : sols) put_path(p);
+        if (pruned) { std::printf("E 0\n"); continue; }
+        put_path(dd.getSolution());
+        if (exact) { std::printf("E 1\n"); continue; }
+        auto ch = dd.getCutset(ub);
+        std::printf("C %a %zu\n", ub, ch.size());
+        for (auto &c : ch) {
+            std::printf("%u %a %a %zu", (unsigned)c.globalLayer, c.lb, c.ub, c.states.size());
+            for (auto x : c.states) std::printf(" %d", (int)x);
+            std::printf(" %zu", c.solutionVector.size());
+            for (auto x : c.solutionVector) std::printf(" %d", (int)x);
+            std::printf("\n");
+        }
+    }
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc == 6 && std::strcmp(argv[1], "dd") == 0) {
+        try {
+            return dd_mode(argv);
+        } catch (const std::exception &e) {
+            std::fprintf(stderr, "error: %s\n", e.what());
+            return 1;
+        }
+    }
     if (argc < 3) {
         std::fprintf(stderr, "usage: %s <network> <known optimum hex|none>\n", argv[0]);
         return 2;

@@ -1,0 +1,64 @@
+"""bench.py's multi-rank watchdog: a shard stuck in a collective must fail the run.
+
+Two gloo ranks; rank 1 never joins rank 0's all-reduce, so rank 0 stalls inside the
+collective the way a hung RCCL exchange of the bnb_multi leg would.  Both ranks arm
+bench.watchdog; the job must end with bench.WATCHDOG_EXIT (non-zero) and rank 0 must still
+print the partial line with the leg marked as timed out (round-4 ADVICE / VERDICT item 5).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SCRIPT = textwrap.dedent("""
+    import os, sys, time
+    sys.path.insert(0, {root!r})
+    import torch
+    import torch.distributed as dist
+    import bench
+    rank = int(os.environ["RANK"])
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    line = {{"metric": "test", "value": 1.0}}
+    stop = bench.watchdog(3.0, line, rank)
+    if rank == 0:
+        dist.all_reduce(torch.ones(1))   # rank 1 never joins: stalls here
+    else:
+        time.sleep(60)
+    stop.set()
+    print("not reached", flush=True)
+""")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_stalled_collective_exits_nonzero(tmp_path):
+    sys.path.insert(0, ROOT)
+    import bench
+    script = tmp_path / "stall.py"
+    script.write_text(SCRIPT.format(root=ROOT))
+    port = _free_port()
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=120) for p in procs]
+    codes = [p.returncode for p in procs]
+    assert codes == [bench.WATCHDOG_EXIT, bench.WATCHDOG_EXIT], (codes, [o[1][-500:] for o in outs])
+    assert bench.WATCHDOG_EXIT != 0
+    lines = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
+    assert lines, outs[0]
+    rec = json.loads(lines[-1])
+    assert "timed out" in rec["bnb_multi"]["error"]
+    assert "not reached" not in outs[0][0] + outs[1][0]
