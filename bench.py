@@ -95,9 +95,11 @@ def parse():
     ap.add_argument("--c5-bnb-seconds", type=float, default=30.0,
                     help="config-5 leg: seconds of the C5 / 512-scenario B&B with cut generation (0: skip)")
     ap.add_argument("--no-parity", action="store_true", help="skip the reference parity check of the timed batch")
+    ap.add_argument("--bnb-parity-pool", type=int, default=10000,
+                    help="bnb_parity leg: optimality cuts the seeded search accumulates before the check")
     ap.add_argument("--bnb-parity-rounds", type=int, default=3,
-                    help="rounds (after the first subproblem) of the seeded device B&B checked against the reference "
-                         "under its own cuts (0: skip)")
+                    help="0: skip the bnb_parity leg (the seeded device B&B checked against the reference under its "
+                         "own cuts, at --bnb-parity-pool optimality cuts)")
     return ap.parse_args()
 
 
@@ -632,13 +634,16 @@ def bnb_parity_leg(args):
     from oracle import bnb_parity as bp
     if not os.path.exists(bp.REF_BIN):
         return None
-    rep = bp.check_search(args.config, args.seed, args.bnb_seeded_width, rounds=80, batch=64, sample=24,
-                          min_subproblems=1, rounds_after=args.bnb_parity_rounds, round_iters=2)
+    # at the pool size the timed legs run against: the seeded search until 10^4 optimality
+    # cuts, then the next round's batch (exact records, non-exact survivors, pruned records)
+    rep = bp.check_large_pool(args.config, args.seed, args.bnb_seeded_width, min_opt_cuts=args.bnb_parity_pool,
+                              per_kind=6)
     fails = rep.pop("failures")
+    rep["pool_last"] = rep["pool_total"]
     rep["bit_exact"] = not fails and rep["mismatches"] == 0
     rep["first_failures"] = fails[:5]
-    rep["against"] = ("oracle/_ref/ref_dd (the reference's RelaxedDDNew) relaxp / refine on the pools and "
-                      "frontiers of the running device search")
+    rep["against"] = ("oracle/_ref/ref_dd (the reference's RelaxedDDNew) relaxp on the pool and next batch of the "
+                      "running device search")
     return rep
 
 

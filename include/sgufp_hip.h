@@ -174,6 +174,18 @@ int sgufp_subproblem(sgufp_ctx *ctx, int n, const int64_t *path_off, const int16
 /* Per (path, scenario) detail of the last sgufp_subproblem call, [n * S] each: status (0
  * optimal, 1 infeasible, 2 error), primal objective, objective of the dual built. */
 int sgufp_subproblem_detail(sgufp_ctx *ctx, int32_t *status, double *objective, double *dual_objective);
+/* Warm-started subproblems (networks without lower bounds): path k starts every scenario from
+ * the optimal flow and potentials stored in ring slot warm_src[k] (-1: cold) and stores its own
+ * in slot warm_dst[k] (-1: none); slots are 0 .. 2 x max(n, 32) - 1, and no slot may be both
+ * written and read, or written twice, by one call.  Results are those of sgufp_subproblem (the
+ * same optimal objectives; the duals -- the cut -- may be another optimal one).  The B&B's
+ * refinement loops (sgufp_bnb_step) pick the closest earlier path themselves. */
+int sgufp_subproblem_warm(sgufp_ctx *ctx, int n, const int64_t *path_off, const int16_t *paths, const int32_t *warm_src,
+                          const int32_t *warm_dst, int32_t *type, double *rhs, double *rows, double *obj_mean);
+/* Per (path, scenario) of the last subproblem call: augmenting paths of the successive-
+ * shortest-path solve (warm: of the repair; a warm start that fell back to a cold solve
+ * reports -1 - cold augmentations) and Bellman-Ford passes. */
+int sgufp_subproblem_stats(sgufp_ctx *ctx, int32_t *augmentations, int32_t *passes);
 /* Inavap::getKey(q, i, j) (Cut.h:342-344) of every coefficient slot (n_slots entries). */
 int sgufp_slot_keys(const sgufp_ctx *ctx, uint64_t *keys);
 /* Append cuts given as dense rows (n_slots + 1 doubles each, as sgufp_subproblem returns

@@ -355,3 +355,113 @@ def check_search(cfg: str, seed: int, width: int, rounds: int, batch: int, sampl
     rep["failures"] = fail
     rep["seconds"] = round(time.perf_counter() - t0, 2)
     return rep
+
+
+# ---------------------------------------------------------------- parity at the timed pool sizes
+def write_pool_bin(path: str, eng: E.Engine) -> int:
+    """The context's pool (feasibility list, then optimality list, insertion order) as the
+    binary dense-row file ``ref_dd`` reads for large pools (oracle/ref_driver.cpp
+    read_cuts_bin).  Returns the number of cuts."""
+    keys = np.asarray(eng.slot_keys(), dtype=np.uint64)
+    ns = len(keys)
+    types, rhs, rows = [], [], []
+    for t in (1, 0):
+        n = eng.cuts_count(t)
+        if n:
+            r, w = eng.cut_rows(t)
+            types.append(np.full(n, t, np.int32))
+            rhs.append(np.asarray(r, np.float64))
+            rows.append(np.ascontiguousarray(np.asarray(w, np.float64)[:, :ns]))
+    nc = int(sum(len(x) for x in types))
+    with open(path, "wb") as fh:
+        fh.write(np.array([nc, ns], dtype=np.int64).tobytes())
+        fh.write(keys.tobytes())
+        for part in (types, rhs):
+            for x in part:
+                fh.write(x.tobytes())
+        for x in rows:
+            fh.write(x.tobytes())
+    return nc
+
+
+def check_large_pool(cfg: str, seed: int, width: int, min_opt_cuts: int, batch: int = 1024, per_kind: int = 8,
+                     round_seconds: float = 5.0, max_seconds: float = 240.0, device: int = 0, threads: int = 0):
+    """Parity at the pool sizes the timed B&B runs against: the seeded search of ``cfg`` (lower
+    bounds 0; incumbent from the width-``width`` restricted-DD heuristic) runs untraced, with
+    uncapped refinement loops, until its optimality list holds ``min_opt_cuts`` cuts.  The next
+    round's batch (``batch`` records, what sgufp_bnb_step pops) is relaxed on the device under
+    that pool and incumbent -- exact records through the cut-parallel phase (k_exact_cols /
+    k_exact_root / k_exact_leaf / k_exact_fin), non-exact survivors through k_relax's batched
+    sweeps -- and ``per_kind`` records of each outcome (exact leaves needing the subproblem,
+    non-exact survivors with cutsets, records pruned by a cut) are compared bit for bit with
+    ``ref_dd relaxp`` on the same pool (NodeExplorer.cpp:935-944 / 975-985, DD.cpp:3932-4023).
+    The round itself then runs and its statuses must equal the device relaxation's."""
+    import time
+    from sgufp_solver_amd import instance
+    from sgufp_solver_amd.pools import DOUBLE_MAX, DOUBLE_MIN, NodeRecord
+    t0 = time.perf_counter()
+    inst = instance.generate(instance.CONFIGS[cfg], seed)
+    inst.lb[:] = 0
+    work = tempfile.mkdtemp(prefix="sgufp_bigpool_")
+    net = os.path.join(work, "net.txt")
+    inst.write(net)
+    eng = E.Engine(net, device, batch)
+    root = NodeRecord(0, DOUBLE_MIN, DOUBLE_MAX, [], [])
+    z = DOUBLE_MIN
+    if width:
+        from sgufp_solver_amd.restricted import RestrictedExplorer
+        z = RestrictedExplorer(eng, width).incumbent([root], z)
+    eng.frontier_clear()
+    eng.frontier_push([root])
+    rep = {"config": cfg, "seed": seed, "heuristic_width": width, "rounds": 0, "search_seconds": 0.0}
+    diving = True
+    while eng.cuts_count(0) < min_opt_cuts and eng.frontier_size() and time.perf_counter() - t0 < max_seconds:
+        eng.bnb_set_limits(0, round_seconds)
+        z, st = eng.bnb_step(z, 64 if diving else batch)
+        if st.exact:
+            diving = False
+        rep["rounds"] += 1
+    rep["search_seconds"] = round(time.perf_counter() - t0, 2)
+    rep["pool_feasibility"] = eng.cuts_count(1)
+    rep["pool_optimality"] = eng.cuts_count(0)
+    rep["incumbent"] = z
+    fail: List[str] = []
+    snap = snapshot_top(eng, batch)
+    recs = E.batch_to_records(snap)
+    got_all = eng.relax(recs, z)
+    kinds = {"exact": [], "survivor": [], "pruned": []}
+    for k, g in enumerate(got_all):
+        if snap.ub[k] <= z:
+            continue                                     # skipped unprocessed by the round
+        kind = "exact" if g.status == E.NEEDS_SUBPROBLEM else ("survivor" if g.status == 0 else "pruned")
+        if len(kinds[kind]) < per_kind:
+            kinds[kind].append(k)
+    idx = sorted(i for v in kinds.values() for i in v)
+    rep["sampled"] = {k: len(v) for k, v in kinds.items()}
+    rep["batch"] = len(recs)
+    pool_path = os.path.join(work, "pool.bin")
+    rep["pool_total"] = write_pool_bin(pool_path, eng)
+    nodes = os.path.join(work, "nodes.txt")
+    out = os.path.join(work, "ref.txt")
+    pools.write_nodes(nodes, [recs[i] for i in idx])
+    t1 = time.perf_counter()
+    subprocess.run([REF_BIN, "relaxp", net, pool_path, nodes, z.hex(), str(threads or _threads()), out], check=True,
+                   capture_output=True, timeout=1800)
+    rep["reference_seconds"] = round(time.perf_counter() - t1, 2)
+    want = pools.read_results(out)
+    bad = compare([got_all[i] for i in idx], want)
+    rep["checked"] = len(idx)
+    rep["mismatches"] = len(bad)
+    fail += bad[:10]
+    # the round itself on the same batch, pool and incumbent
+    eng.bnb_set_trace(True)
+    eng.bnb_set_limits(1, round_seconds)
+    z2, st = eng.bnb_step(z, batch)
+    by_rec = {rk: c for rk, c, _, _, _ in eng.bnb_trace(0)}
+    for i in idx:
+        if by_rec.get(i) != got_all[i].status:
+            fail.append(f"record {i}: round status {by_rec.get(i)} != device relaxation {got_all[i].status}")
+    eng.close()
+    rep["failures"] = fail
+    rep["seconds"] = round(time.perf_counter() - t0, 2)
+    return rep

@@ -28,6 +28,7 @@
 //
 // File formats (text; doubles as C99 hex floats, "%a"):
 //   cuts : <ncuts>\n then per cut "<type 0=opt 1=feas> <rhs> <nnz>\n" and nnz lines "<i> <q> <j> <val>"
+//          (or a binary dense-row pool, file name *.bin: read_cuts_bin)
 //          (insertion order; the Container is a LIFO list, Cut.h:456-485, so application is newest first)
 //   nodes: <n>\n then per node "<gl> <lb> <ub> <ns> s... <nsol> d..."
 #include "DD.h"
@@ -59,7 +60,39 @@ struct PoolCut {
 
 static double parse_double(const std::string &s) { return std::strtod(s.c_str(), nullptr); }
 
+// Binary pool (large pools read back from a running device search, oracle/bnb_parity.py):
+// int64 n_cuts, int64 n_slots, uint64 slot keys [n_slots] (getKey(q,i,j)), int32 types [n_cuts],
+// f64 rhs [n_cuts], f64 dense rows [n_cuts][n_slots]; non-zero slots become (i,q,j) entries.
+static std::vector<PoolCut> read_cuts_bin(const std::string &path) {
+    FILE *f = std::fopen(path.c_str(), "rb");
+    if (!f) { std::cerr << "cannot open " << path << "\n"; std::exit(2); }
+    int64_t nc = 0, ns = 0;
+    if (std::fread(&nc, 8, 1, f) != 1 || std::fread(&ns, 8, 1, f) != 1) std::exit(2);
+    std::vector<uint64_t> keys((size_t)ns);
+    std::vector<int32_t> types((size_t)nc);
+    std::vector<double> rhs((size_t)nc), row((size_t)ns);
+    if (std::fread(keys.data(), 8, (size_t)ns, f) != (size_t)ns || std::fread(types.data(), 4, (size_t)nc, f) != (size_t)nc ||
+        std::fread(rhs.data(), 8, (size_t)nc, f) != (size_t)nc)
+        std::exit(2);
+    std::vector<PoolCut> cuts;
+    cuts.reserve((size_t)nc);
+    for (int64_t c = 0; c < nc; c++) {
+        if (std::fread(row.data(), 8, (size_t)ns, f) != (size_t)ns) std::exit(2);
+        CutCoefficients coeff;
+        for (int64_t s = 0; s < ns; s++) {
+            if (row[(size_t)s] == 0.0) continue;
+            const uint64_t k = keys[(size_t)s];
+            coeff[std::make_tuple((int)((k >> 16) & 0xFFFF), (int)(k & 0xFFFF), (int)((k >> 32) & 0xFFFF))] = row[(size_t)s];
+        }
+        ::Cut legacy{types[(size_t)c] ? FEASIBILITY : OPTIMALITY, rhs[(size_t)c], coeff};
+        cuts.push_back(PoolCut{types[(size_t)c], Inavap::cutToCut(legacy, nullptr)});
+    }
+    std::fclose(f);
+    return cuts;
+}
+
 static std::vector<PoolCut> read_cuts(const std::string &path) {
+    if (path.size() > 4 && path.compare(path.size() - 4, 4, ".bin") == 0) return read_cuts_bin(path);
     std::ifstream in(path);
     if (!in) { std::cerr << "cannot open " << path << "\n"; std::exit(2); }
     size_t n;

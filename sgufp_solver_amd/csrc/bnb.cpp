@@ -680,6 +680,18 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
             io.path_stride = ctx->sc.Lcap;
             io.paths = o.path;
             io.path_off = nullptr;
+            // warm starts: every path starts from the stored state of the closest path solved
+            // before (the record's own previous path, a sibling's, ...) and leaves its own state
+            // in the ring for the next ones (k_warm_pick, k_sub_scenario<..., WARM>)
+            if (ctx->warm_reserve(ctx->max_batch)) {
+                if (!ctx->hip_ok(launch_warm_pick(io, ctx->wring, ctx->warm_ptr, ctx->stream), "k_warm_pick"))
+                    return SGUFP_ERR_HIP;
+                io.warm_src = ctx->wring.src;
+                io.warm_dst = ctx->wring.dst;
+                io.wst_x = ctx->d_wx;
+                io.wst_a = ctx->d_wa;
+                ctx->warm_ptr = (ctx->warm_ptr + nf) % ctx->wring.R;
+            }
             if (!ctx->hip_ok(launch_subproblem(ctx->sn, io, ctx->stream), "subproblem launch")) return SGUFP_ERR_HIP;
             ctx->sub_last_n = nf;
             const int first = ctx->n_rows;

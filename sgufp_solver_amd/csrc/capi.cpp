@@ -116,6 +116,7 @@ bool sgufp_ctx::init() {
     nscreen = cb;
     if (const char *e = getenv("SGUFP_SCREEN")) nscreen = std::max(0, atoi(e));
     if (const char *e = getenv("SGUFP_EXACT_FAST")) exact_fast = atoi(e) != 0;
+    if (const char *e = getenv("SGUFP_SUB_WARM")) warm_on = atoi(e) != 0;   // warm-started subproblems (A/B)
     if (const char *e = getenv("SGUFP_EXACT_SCREEN")) exact_screen = std::max(0, std::min(kExactScreen, atoi(e)));
     if (const char *e = getenv("SGUFP_EXACT_LAZY")) exact_lazy = std::max(0, atoi(e));
     int64_t acap = std::max<int64_t>(1, (int64_t)std::max(0, L - 4) * (kRelaxedMaxWidth - 1) * maxU);
@@ -754,6 +755,9 @@ bool sgufp_ctx::sub_grow(int n, size_t total) {
         }
         sio.status = st; sio.obj = ob; sio.dual = du; sio.rhs = rh; sio.coef = cf;
         sio.cut_type = ct; sio.cut_rhs = crh; sio.cut_row = crow; sio.obj_mean = om;
+        if (d_wstat) release(d_wstat);
+        if (!alloc(d_wstat, (size_t)cap * S * 2, "sub io")) return false;
+        sio.wstat = d_wstat;
         int64_t *po;
         if (!alloc(po, (size_t)cap + 1, "sub io")) return false;
         if (d_spoff) release(d_spoff);
@@ -771,8 +775,85 @@ bool sgufp_ctx::sub_grow(int n, size_t total) {
     return true;
 }
 
+// The warm-start ring: R = 2 x the most paths one launch solves (so every launch has
+// candidates outside its own destinations), states of every scenario per slot.  Allocated on
+// first use; a network with lower bounds (64-bit-key kernels) or a failed allocation leaves the
+// subproblems cold.
+bool sgufp_ctx::warm_reserve(int paths_per_launch) {
+    if (!warm_on || !sn.key32) return false;
+    const int R = 2 * std::max(paths_per_launch, 1);
+    if (wring.R >= R) return true;
+    const size_t S = (size_t)net.S, m = (size_t)net.m, n_ = (size_t)net.n;
+    const size_t bytes = (size_t)R * S * (m * 2 + n_ * 4);
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && bytes > fr / 2) {
+        warm_on = false;
+        return false;
+    }
+    WarmRing w{};
+    int16_t *wx = nullptr;
+    int32_t *wa = nullptr;
+    if (!alloc(wx, (size_t)R * S * m, "warm ring") || !alloc(wa, (size_t)R * S * n_, "warm ring") ||
+        !alloc(w.path, (size_t)R * std::max(sc.Lcap, 1), "warm ring") || !alloc(w.plen, (size_t)R, "warm ring") ||
+        !alloc(w.valid, (size_t)R, "warm ring") || !alloc(w.src, (size_t)R, "warm ring") ||
+        !alloc(w.dst, (size_t)R, "warm ring") || !alloc(w.dist, (size_t)R, "warm ring") ||
+        !hip_ok(hipMemsetAsync(w.valid, 0, (size_t)R, stream), "memset") || !sync())
+        return false;
+    if (wring.R) {   // a larger ring: the old states go (they only speed up later solves)
+        release(d_wx); release(d_wa); release(wring.path); release(wring.plen); release(wring.valid);
+        release(wring.src); release(wring.dst); release(wring.dist);
+    }
+    static const int maxd = [] {
+        const char *e = std::getenv("SGUFP_SUB_WARM_DIST");   // farther donors: cold start
+        return e ? std::atoi(e) : 48;
+    }();
+    w.R = R;
+    w.Lcap = std::max(sc.Lcap, 1);
+    w.max_dist = maxd;
+    wring = w;
+    d_wx = wx;
+    d_wa = wa;
+    warm_ptr = 0;
+    return true;
+}
+
+// shared body of sgufp_subproblem / sgufp_subproblem_warm: explicit warm slots (src / dst,
+// host arrays of n entries) or none
+static int subproblem_run(sgufp_ctx *ctx, int n, const int64_t *path_off, const int16_t *paths, const int32_t *src,
+                          const int32_t *dst, int32_t *type, double *rhs, double *rows, double *obj_mean);
+
 int sgufp_subproblem(sgufp_ctx *ctx, int n, const int64_t *path_off, const int16_t *paths, int32_t *type,
                      double *rhs, double *rows, double *obj_mean) {
+    return subproblem_run(ctx, n, path_off, paths, nullptr, nullptr, type, rhs, rows, obj_mean);
+}
+
+int sgufp_subproblem_warm(sgufp_ctx *ctx, int n, const int64_t *path_off, const int16_t *paths, const int32_t *warm_src,
+                          const int32_t *warm_dst, int32_t *type, double *rhs, double *rows, double *obj_mean) {
+    if (!ctx || n < 0 || (n && (!warm_src || !warm_dst))) return SGUFP_ERR_ARG;
+    if (!ctx->sub_init()) return SGUFP_ERR_HIP;
+    if (!ctx->warm_reserve(std::max(n, 32))) {
+        ctx->err = "warm starts need a network without lower bounds (32-bit-key kernels) and device memory";
+        return SGUFP_ERR_STATE;
+    }
+    for (int k = 0; k < n; k++)
+        if (warm_src[k] >= ctx->wring.R || warm_dst[k] < -1 || warm_dst[k] >= ctx->wring.R) return SGUFP_ERR_ARG;
+    return subproblem_run(ctx, n, path_off, paths, warm_src, warm_dst, type, rhs, rows, obj_mean);
+}
+
+int sgufp_subproblem_stats(sgufp_ctx *ctx, int32_t *augmentations, int32_t *passes) {
+    if (!ctx) return SGUFP_ERR_ARG;
+    const size_t cnt = (size_t)ctx->sub_last_n * ctx->net.S;
+    std::vector<int32_t> w(cnt * 2);
+    if (cnt && (!ctx->download(w.data(), ctx->d_wstat, w.size()) || !ctx->sync())) return SGUFP_ERR_HIP;
+    for (size_t i = 0; i < cnt; i++) {
+        if (augmentations) augmentations[i] = w[2 * i];
+        if (passes) passes[i] = w[2 * i + 1];
+    }
+    return SGUFP_OK;
+}
+
+static int subproblem_run(sgufp_ctx *ctx, int n, const int64_t *path_off, const int16_t *paths, const int32_t *src,
+                          const int32_t *dst, int32_t *type, double *rhs, double *rows, double *obj_mean) {
     if (!ctx || n < 0 || (n && (!path_off || !paths))) return SGUFP_ERR_ARG;
     if (n == 0) return SGUFP_OK;
     for (int k = 0; k < n; k++)
@@ -813,6 +894,14 @@ int sgufp_subproblem(sgufp_ctx *ctx, int n, const int64_t *path_off, const int16
     io.path_slot = nullptr;
     io.path_len = nullptr;
     io.path_stride = 0;
+    if (src) {   // explicit warm slots (sgufp_subproblem_warm)
+        if (!ctx->upload(ctx->wring.src, src, (size_t)n) || !ctx->upload(ctx->wring.dst, dst, (size_t)n))
+            return SGUFP_ERR_HIP;
+        io.warm_src = ctx->wring.src;
+        io.warm_dst = ctx->wring.dst;
+        io.wst_x = ctx->d_wx;
+        io.wst_a = ctx->d_wa;
+    }
     if (!ctx->hip_ok(launch_subproblem(ctx->sn, io, ctx->stream), "subproblem launch")) return SGUFP_ERR_HIP;
     ctx->sub_last_n = n;
     const size_t stride = (size_t)ctx->net.n_slots + 1;

@@ -26,6 +26,7 @@ struct Transport;   // shard.cpp
 size_t relax_lds_bytes(int Tcap, int Lcap, int cb, int us);
 size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw, int kbytes = 8);
 hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st);
+hipError_t launch_warm_pick(const SubIO &io, const WarmRing &wr, int ptr, hipStream_t st);
 hipError_t launch_relax(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &, double, int,
                         const ExactIO &, int, hipStream_t);
 // exact_kernels.hip
@@ -193,6 +194,15 @@ struct sgufp_ctx {
     int64_t *d_spoff = nullptr;
     int16_t *d_spaths = nullptr;
     int sub_last_n = 0;
+    int32_t *d_wstat = nullptr;               // [sub_cap * S * 2] per (path, scenario): augmentations, passes
+    // warm-start ring of the scenario subproblem (SGUFP_SUB_WARM=0: off): flows + potentials of
+    // earlier solves, for the refinement loops' next paths (bnb.cpp)
+    bool warm_on = true;
+    WarmRing wring{};
+    int warm_ptr = 0;
+    int16_t *d_wx = nullptr;
+    int32_t *d_wa = nullptr;
+    bool warm_reserve(int paths_per_launch);  // false: no ring (cold subproblems)
     bool sub_init();
     bool sub_grow(int n, size_t total);
     bool append_rows(int is_feasibility, int n_cuts, const double *rhs, const std::vector<double> &rows);

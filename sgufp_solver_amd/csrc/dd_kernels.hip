@@ -202,6 +202,15 @@ __device__ __forceinline__ void dd_bind(DD &d, LDS uint8_t *smem, const Scratch 
     d.tw = sc.tw + N;
     d.atopo = sc.atopo + A;
     d.aflag = sc.aflag + A;
+    // no packed-topology mirror unless k_relax's batched path builds one (build_stream): the
+    // other kernels (refine, emit, one-cut apply) edit the master flags only
+    d.tmir = nullptr;
+    d.gstart = nullptr;
+    d.stream = 0;
+    d.ng = 0;
+    d.kg = 0;
+    d.Nn = 0;
+    d.Amir = 0;
 }
 
 // Coefficient slot of state rank r at DD layer k (arc from tree layer k-1 into k).

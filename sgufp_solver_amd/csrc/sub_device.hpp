@@ -64,6 +64,35 @@ struct SubIO {
     double SGUFP_GBL *cut_rhs;           // [P]
     double SGUFP_GBL *cut_row;           // [P][n_slots+1] dense cut row (last slot 0)
     double SGUFP_GBL *obj_mean;          // [P] sum_s obj_s / S (optimality)
+    // Warm starts (32-bit-key launches: no lower bound, so every scenario is feasible).  The
+    // state of (slot, scenario) is an optimal flow per network arc and the optimal node
+    // potentials (alpha of grb.cpp's dual, 0 at free and V-bar nodes) of an earlier solve.
+    // Path p starts scenario s from slot warm_src[p]'s state (-1: cold) and writes its own final
+    // state to slot warm_dst[p] (-1: none).  A solve reads only its source slot and writes only
+    // its destination: two paths of one launch may share neither a destination nor a
+    // destination with another path's source (the host guarantees it).
+    const int32_t SGUFP_GBL *warm_src;   // [P] or null
+    const int32_t SGUFP_GBL *warm_dst;   // [P] or null
+    int16_t SGUFP_GBL *wst_x;            // [slots][S][m]
+    int32_t SGUFP_GBL *wst_a;            // [slots][S][n]
+    int32_t SGUFP_GBL *wstat;            // [P*S][2] or null: augmentations (negative: a warm start fell
+                                         // back to the cold SSP), Bellman-Ford passes
+};
+
+// Ring of warm-start states (the B&B's refinement loops, bnb.cpp): R slots, each holding the
+// path it was solved for here and its flows / potentials for every scenario in SubIO::wst_x /
+// wst_a.  k_warm_pick gives each path of a launch the slot whose path differs in the fewest
+// decisions (slots written by the same launch excluded) and the slot its own state goes to.
+struct WarmRing {
+    int R;                                // slots
+    int Lcap;                             // decisions per stored path
+    int max_dist;                         // farther than this: cold start
+    int16_t SGUFP_GBL *path;              // [R][Lcap]
+    uint16_t SGUFP_GBL *plen;             // [R]
+    uint8_t SGUFP_GBL *valid;             // [R]
+    int32_t SGUFP_GBL *src;               // [paths per launch] chosen source slot (-1: cold)
+    int32_t SGUFP_GBL *dst;               // [paths per launch] destination slot
+    int32_t SGUFP_GBL *dist;              // [paths per launch] decisions that differ (-1: none)
 };
 
 }  // namespace sgufp

@@ -206,8 +206,9 @@ __host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int 
     off[3] = o; o = a16(o + (size_t)(n + 2) * kbytes);   // key | chosen
     off[4] = o; o = a16(o + (size_t)(n + 2) * 4);   // pred
     off[8] = o; o = a16(o + (size_t)(n + 2) * 2);   // plist
-    off[0] = a16(u0 + (size_t)m * 2);               // dec, after chosen
-    if (o < a16(off[0] + (size_t)m * 2)) o = a16(off[0] + (size_t)m * 2);
+    off[0] = a16(u0 + (size_t)m * 2);               // dec, after chosen; then the warm start's
+    const size_t dsz = (size_t)m * 2 > (size_t)(n + 2) * 4 ? (size_t)m * 2 : (size_t)(n + 2) * 4;   // node imbalances
+    if (o < a16(off[0] + dsz)) o = a16(off[0] + dsz);
     off[5] = o;
     off[6] = o; o = a16(o + (size_t)nz * 4);
     off[7] = o; o = a16(o + 8 * 4);
@@ -554,9 +555,7 @@ __device__ __forceinline__ bool bf_converge(const SubNet &N, const WS &W, int nc
     using B = Blk<NW>;
     bool prev_quiet = false;   // the sweep before the current one changed nothing
     for (int it = 0; it < 2 * (N.n + 4); it++) {
-#ifdef SGUFP_SUB_TRACE
-        if (B::tid() == 0 && !(it & 1)) W.misc[5]++;
-#endif
+        if (B::tid() == 0 && !(it & 1)) W.misc[5]++;   // passes (io.wstat)
         const uint32_t changed = bf_sweep<RG, WT, NW>(N, W, nct, nz, mode, M, C, !(it & 1));
         B::sync();
         const bool quiet = !B::any(changed, W.red);
@@ -570,9 +569,9 @@ __device__ __forceinline__ bool bf_converge(const SubNet &N, const WS &W, int nc
 // node that are tight in (cost, hops).  Hops grow by one along such arcs, so the
 // predecessor graph has no cycle and the walk from Z_in ends at Z_out.
 template <int NW, class WS>
-__device__ __forceinline__ void ssp_preds(const SubNet &N, const WS &W, int nct, int nz, int64_t M) {
+__device__ __forceinline__ void ssp_preds(const SubNet &N, const WS &W, int nct, int nz, int64_t M, int mode = kSsp) {
     using KT = typename WS::Key;
-    for_residual<NW>(N, W, nct, nz, kSsp, M, [&](int u, int v, int64_t w, int code) {
+    for_residual<NW>(N, W, nct, nz, mode, M, [&](int u, int v, int64_t w, int code) {
         const KT ku = W.key[u];
         if (ku >= WS::kKInf) return;
         if ((KT)(ku + (KT)((w << WS::kHop) + 1)) == W.key[v])
@@ -585,7 +584,8 @@ __device__ __forceinline__ void ssp_preds(const SubNet &N, const WS &W, int nct,
 // registers; slot j of wave w holds group j * NW + w): the costs are the ones the Bellman-Ford
 // used, no chain record is re-read.
 template <int RG, typename WT, int NW, class WS>
-__device__ __forceinline__ void ssp_preds_regs(const SubNet &N, const WS &W, int nct, int nz, const ChainRegs<RG, WT> &C) {
+__device__ __forceinline__ void ssp_preds_regs(const SubNet &N, const WS &W, int nct, int nz, const ChainRegs<RG, WT> &C,
+                                               int mode = kSsp) {
     using KT = typename WS::Key;
     using B = Blk<NW>;
     const int n = N.n, m = N.m;
@@ -616,8 +616,13 @@ __device__ __forceinline__ void ssp_preds_regs(const SubNet &N, const WS &W, int
     for (int i = B::tid(); i < nz; i += B::T) {
         const uint32_t e = (uint32_t)W.zlist[i];
         const int v = (int)(e & 0x1FFFFFFFu);
-        if ((e >> 30) & 1u) tight(n, v, (KT)1, 2 * m + 2 * v, true);
-        if ((e >> 29) & 1u) tight(v, n + 1, (KT)1, 2 * m + 2 * v + 1, true);
+        if (mode == kSsp) {
+            if ((e >> 30) & 1u) tight(n, v, (KT)1, 2 * m + 2 * v, true);
+            if ((e >> 29) & 1u) tight(v, n + 1, (KT)1, 2 * m + 2 * v + 1, true);
+        } else {   // Z tied to every free node both ways (for_residual's potential mode)
+            tight(n, v, (KT)1, 2 * m + 2 * v, true);
+            tight(v, n, (KT)1, 2 * m + 2 * v + 1, true);
+        }
     }
     B::sync();
 }
@@ -626,7 +631,7 @@ __device__ __forceinline__ void ssp_preds_regs(const SubNet &N, const WS &W, int
 // Z_out alone -- Bellman-Ford from any upper bounds of the shortest keys reaches them.
 template <int RG, typename WT, int NW, class WS>
 __device__ __forceinline__ bool bellman_ford(const SubNet &N, const WS &W, int nct, int nz, int mode, int64_t M,
-                                    bool warm = false) {
+                                    bool warm = false, bool preds = false) {
     using B = Blk<NW>;
     const int nn = N.n + 2;
     for (int v = B::tid(); v < nn; v += B::T) {
@@ -637,7 +642,16 @@ __device__ __forceinline__ bool bellman_ford(const SubNet &N, const WS &W, int n
     load_chain_regs<RG, WT, NW>(W, N.n, nct, mode, M, C);
     B::sync();
     const bool converged = bf_converge<RG, WT, NW>(N, W, nct, nz, mode, M, C);
-    if (mode != kSsp || !converged) return converged;
+    if (!converged) return false;
+    if (mode != kSsp) {
+        // potentials; with preds (the warm start's repair): the tight in-arcs under the
+        // potential mode's Z arcs
+        if (preds) {
+            if constexpr (WS::kAllReg) ssp_preds_regs<RG, WT, NW>(N, W, nct, nz, C, mode);
+            else ssp_preds<NW>(N, W, nct, nz, M, mode);
+        }
+        return true;
+    }
 #ifdef SGUFP_SUB_VERIFY
     // Debug build: the labels a warm start converged to must equal those of a cold
     // Bellman-Ford from Z_out alone (invalidate_subtrees' exactness argument, checked).
@@ -720,6 +734,140 @@ __device__ __forceinline__ void invalidate_subtrees(const SubNet &N, const WS &W
     for (int v = B::tid(); v < nn; v += B::T)
         if (anc[v] & 0x8000u) W.key[v] = kKInf;
     B::sync();
+}
+
+// ---------------------------------------------------------------------------------------
+// Warm start.  The chains of a new path start from an earlier optimal state of the same
+// scenario (flow per arc, potentials alpha): a chain keeps the smallest earlier flow of its
+// arcs, then its reduced reward E = R - alpha(h) + alpha(t) under the old potentials fixes it
+// -- E > 0: x = U, E < 0: x = 0, E = 0: kept within [0, U] -- so every residual arc has a
+// non-negative reduced cost (no negative cycle: the pseudoflow is optimal for its imbalances).
+// Chains that did not change keep their flow, so only the nodes around the changed V-bar
+// matchings are out of balance.  The repair is successive shortest paths from the excess to
+// the deficit nodes (potential mode: every free node is tied to Z both ways at cost 0, so
+// free supply / demand absorbs anything):
+//   stage 0: multi-source Bellman-Ford from every excess node (key 0), augment towards the
+//            closest deficit node or Z (absorbed by a free node);
+//   stage 1: from Z (free supply) to the remaining deficit nodes.
+// Each augmentation is a shortest path of the extended network (super source -> sources at
+// cost 0, targets -> super sink at cost 0), so the residual stays free of negative cycles and
+// the repaired flow is optimal.  Between augmentations the Bellman-Ford resumes from its
+// labels as the cold SSP does: the heads of used-up arcs and a source whose excess is gone
+// restart at infinity with their predecessor subtrees (invalidate_subtrees).  Returns false
+// (the caller falls back to the cold SSP) if a target is unreachable or the augmentation
+// bound is hit; neither happens with lower bounds 0.
+__device__ __forceinline__ bool is_cons(const SubNet &N, int v) { return N.inner[v] && !N.vbar[v]; }
+
+// Warm start.  The chains of a new path start from an earlier optimal state of the same
+// scenario (flow per arc, potentials alpha): a chain keeps the smallest earlier flow of its
+// arcs, then its reduced reward E = R - alpha(h) + alpha(t) under the old potentials fixes it
+// -- E > 0: x = U, E < 0: x = 0, E = 0: kept within [0, U] -- so every residual arc has a
+// non-negative reduced cost (no negative cycle: the pseudoflow is optimal for its imbalances).
+// Chains that did not change keep their flow, so only the nodes around the changed V-bar
+// matchings are out of balance.  The repair is successive shortest paths from the excess to
+// the deficit nodes (potential mode: every free node is tied to Z both ways at cost 0, so
+// free supply / demand absorbs anything):
+//   stage 0: multi-source Bellman-Ford from every excess node (key 0), augment towards the
+//            closest deficit node or Z (absorbed by a free node);
+//   stage 1: from Z (free supply) to the remaining deficit nodes.
+// Each augmentation is a shortest path of the extended network (super source -> sources at
+// cost 0, targets -> super sink at cost 0), so the residual stays free of negative cycles and
+// the repaired flow is optimal.  Between augmentations the Bellman-Ford resumes from its
+// labels as the cold SSP does: the heads of used-up arcs and a source whose excess is gone
+// restart at infinity with their predecessor subtrees (invalidate_subtrees).  Returns false
+// (the caller falls back to the cold SSP) if a target is unreachable or the augmentation
+// bound is hit; neither happens with lower bounds 0.  Only the WARM instantiation of
+// k_sub_scenario carries it (launches with warm starts); the cold one is unchanged.
+template <int RG, typename WT, int NW, class WS>
+__device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nct, int nz, int64_t M,
+                                                      LDS int32_t *imb, int64_t max_aug, int &augs) {
+    using B = Blk<NW>;
+    using KT = typename WS::Key;
+    constexpr KT kKInf = WS::kKInf;
+    const int n = N.n, m = N.m;
+    const int tid = B::tid();
+    constexpr int T = B::T;
+    for (int stage = 0; stage < 2; stage++) {
+        bool fresh = true;
+        for (;;) {
+            uint32_t left = 0;
+            for (int v = tid; v < n; v += T)
+                if (is_cons(N, v) && (stage == 0 ? imb[v] > 0 : imb[v] < 0)) left = 1;
+            if (!B::any(left, W.red)) break;
+            if (fresh) {
+                for (int v = tid; v < n + 2; v += T) {
+                    KT k = kKInf;
+                    if (stage == 0 ? (v < n && is_cons(N, v) && imb[v] > 0) : v == n) k = 0;
+                    W.key[v] = k;
+                }
+                B::sync();
+                fresh = false;
+            }
+            if (!bellman_ford<RG, WT, NW>(N, W, nct, nz, kPotPlain, M, true, true)) return false;
+            // the closest target (key, then node id): deficit nodes, and Z in stage 0
+            int64_t best = INT64_MAX;
+            for (int v = tid; v <= n; v += T) {
+                const bool tgt = v < n ? (is_cons(N, v) && imb[v] < 0) : stage == 0;
+                const KT k = W.key[v];
+                if (tgt && k < kKInf) {
+                    const int64_t c = (int64_t)k * 4096 + v;   // compact keys < 2^30, ids < 2^11 (host)
+                    best = c < best ? c : best;
+                }
+            }
+            best = B::all(best, [](int64_t x, int64_t y) { return x < y ? x : y; }, W.red);
+            if (best == INT64_MAX) return false;
+            const int tgt = (int)(best & 4095);
+            if (tid == 0) {
+                int v = tgt, len = 0;
+                while (len < n + 2) {
+                    const int32_t pr = W.pred[v];
+                    if (pr == kNoPred) break;
+                    W.plist[len++] = (uint16_t)(pr >> 15);
+                    v = (int)(pr & 0x7FFF);
+                }
+                W.misc[3] = len;
+                W.misc[4] = v;
+            }
+            B::sync();
+            const int plen = W.misc[3], src = W.misc[4];
+            const bool src_ok = stage == 0 ? (src < n && is_cons(N, src) && imb[src] > 0) : src == n;
+            int64_t delta = kInf;
+            for (int i = tid; i < plen; i += T) {
+                const int code = W.plist[i];
+                if (code >= 2 * m) continue;   // Z arcs: uncapacitated
+                const uint64_t cb = W.rb(code >> 1);
+                const int64_t x = ch_x(cb), U = ch_U(cb);
+                const int64_t cap = (code & 1) ? x : U - x;
+                delta = cap < delta ? cap : delta;
+            }
+            delta = B::all(delta, [](int64_t p, int64_t q) { return p < q ? p : q; }, W.red);
+            if (stage == 0 && src_ok) delta = (int64_t)imb[src] < delta ? (int64_t)imb[src] : delta;
+            if (tgt < n) delta = (int64_t)(-imb[tgt]) < delta ? (int64_t)(-imb[tgt]) : delta;
+            if (!src_ok || plen >= n + 2 || delta <= 0 || delta >= kInf) return false;
+            B::sync();   // every lane read the imbalances before they change
+            for (int i = tid; i < plen; i += T) {
+                const int code = W.plist[i];
+                if (code >= 2 * m) continue;
+                const int k = code >> 1;
+                const uint64_t ca = W.ra(k), cb = W.rb(k);
+                const int64_t x = ch_x(cb), U = ch_U(cb);
+                const int64_t cap = (code & 1) ? x : U - x;
+                W.add_x(k, (int)((code & 1) ? -delta : delta));
+                if (cap == delta) W.key[(code & 1) ? ch_t(ca) : ch_h(ca)] = kKInf;   // segment used up
+            }
+            if (tid == 0) {
+                if (stage == 0) {
+                    imb[src] -= (int32_t)delta;
+                    if (imb[src] == 0) W.key[src] = kKInf;   // no longer a source
+                }
+                if (tgt < n) imb[tgt] += (int32_t)delta;
+            }
+            B::sync();
+            invalidate_subtrees<NW>(N, W);
+            if (++augs > max_aug) return false;
+        }
+    }
+    return true;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -927,7 +1075,7 @@ __device__ __forceinline__ void chain_starts(const SubNet &N, const WS &W, const
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
-template <int RG, typename WT, int NW, typename KT, bool ALLREG>
+template <int RG, typename WT, int NW, typename KT, bool ALLREG, bool WARM = false>
 __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3) : (sizeof(KT) == 4 ? 4 : 1)) k_sub_scenario(SubNet N, SubIO io) {
     using WS = SubLds<KT, ALLREG, NW == 1>;
     using B = Blk<NW>;
@@ -968,6 +1116,12 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         plen = io.path_off[p + 1] - poff;
     }
     const size_t b = (size_t)p * S + s;
+    // warm start (compact kernels only: no lower bound, every scenario feasible)
+    constexpr bool kWarm = WARM && WS::kCompact;
+    const int wsrc = (kWarm && io.warm_src) ? io.warm_src[p] : -1;
+    const int wdst = (kWarm && io.warm_dst) ? io.warm_dst[p] : -1;
+    const GBL int16_t *xprev = wsrc >= 0 ? io.wst_x + ((size_t)wsrc * S + s) * m : nullptr;
+    const GBL int32_t *aprev = wsrc >= 0 ? io.wst_a + ((size_t)wsrc * S + s) * n : nullptr;
 
     // 1. decisions and matching
     if (tid < 8) W.misc[tid] = 0;
@@ -1030,6 +1184,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         const int first = a;
         const int t0 = N.tail[a];
         int L = N.lb[so + a], U = N.ub[so + a], R = N.reward[a];
+        int xw = xprev ? (int)xprev[a] : 0;   // warm start: the smallest earlier flow of the chain's arcs
         int h = -1, len = 1;
         for (;;) {
             const int q = N.head[a];
@@ -1041,11 +1196,18 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
             L = max(L, (int)N.lb[so + a]);
             U = min(U, (int)N.ub[so + a]);
             R += N.reward[a];
+            if (xprev) xw = min(xw, (int)xprev[a]);
         }
         const int t = N.vbar[t0] ? -1 : t0;
-        W.wa(k, pack_a(t, h, R));
-        W.wb(k, pack_b(L, U, 0, first));   // compact: L = 0 (host), no first arc
         const bool complete = t >= 0 && h >= 0;
+        int x0 = 0;
+        if (xprev && complete) {
+            // reduced reward under the earlier potentials (alpha 0 at free / V-bar nodes)
+            const int E = R - (int)aprev[h] + (int)aprev[t];
+            x0 = E > 0 ? U : (E < 0 ? 0 : max(0, min(xw, U)));
+        }
+        W.wa(k, pack_a(t, h, R));
+        W.wb(k, pack_b(L, U, x0, first));   // compact: L = 0 (host), no first arc
         if ((complete && L > U) || (!complete && L > 0)) first_bad = min(first_bad, k);
     }
     first_bad = B::all(first_bad, [](int x, int y) { return x < y ? x : y; }, W.red);
@@ -1058,6 +1220,23 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         if (tid == 0) { io.status[b] = kSubError; io.obj[b] = 0; io.dual[b] = 0; io.rhs[b] = 0; }
         for (int v = tid; v < N.n_slots; v += T) io.coef[b * N.n_slots + v] = 0.0;
         return;
+    }
+
+    // warm start: node imbalances of the initial flow (conservation rows only; dec is dead in
+    // the compact kernels from here and its space holds them)
+    LDS int32_t *imb = (LDS int32_t *)W.dec;
+    if (xprev) {
+        for (int v = tid; v < n + 2; v += T) imb[v] = 0;
+        B::sync();
+        for (int k = tid; k < nct; k += T) {
+            const uint64_t ca = W.ra(k);
+            const int t = ch_t(ca), h = ch_h(ca), x = ch_x(W.rb(k));
+            if (t >= 0 && h >= 0 && x) {
+                __hip_atomic_fetch_add(&imb[h], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&imb[t], -x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        B::sync();
     }
 
     int status = kSubOptimal;
@@ -1117,13 +1296,45 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
 #define SUB_T1(acc)
 #endif
         int iters = 0;
+        int warm_augs = 0;
+        bool repaired = false, fell_back = false;
+#ifdef SGUFP_SUB_VERIFY
+        int64_t verify_primal = INT64_MIN;
+#endif
+        if (xprev) {
+            int64_t imb_tot = 0;
+            for (int v = tid; v < n; v += T)
+                if (is_cons(N, v)) imb_tot += imb[v] > 0 ? imb[v] : -imb[v];
+            imb_tot = B::all(imb_tot, [](int64_t x, int64_t y) { return x + y; }, W.red);
+            repaired = warm_repair<RG, WT, NW>(N, W, nct, nz, M, imb, imb_tot + 2 * (int64_t)nct + 8, warm_augs);
+#ifdef SGUFP_SUB_VERIFY
+            if (repaired) {   // debug build: the cold SSP below must reach the same objective
+                int64_t pw = 0;
+                for (int k = tid; k < nct; k += T) {
+                    const uint64_t ca = W.ra(k);
+                    if (ch_t(ca) >= 0 && ch_h(ca) >= 0) pw += (int64_t)ch_R(ca) * ch_x(W.rb(k));
+                }
+                verify_primal = B::all(pw, [](int64_t x, int64_t y) { return x + y; }, W.red);
+                repaired = false;
+            }
+#endif
+            if (!repaired) {   // cold from zero flow
+                fell_back = true;
+                B::sync();
+                for (int k = tid; k < nct; k += T) {
+                    const int x = ch_x(W.rb(k));
+                    if (x) W.add_x(k, -x);
+                }
+                B::sync();
+            }
+        }
         // Each round: Bellman-Ford labels and predecessors, stop when the shortest Z_out ->
         // Z_in path no longer gains, else augment along it.  After the first round the
         // Bellman-Ford resumes from the previous labels, with only the subtrees under the
         // used-up arcs restarted (invalidate_subtrees).  (Reusing the labels without any
         // Bellman-Ford while a tight residual path survives never found one on C3 / C4.)
         bool warm = false;
-        for (; status == kSubOptimal; iters++) {
+        for (; status == kSubOptimal && !repaired; iters++) {
             SUB_T0();
             if (!bellman_ford<RG, WT, NW>(N, W, nct, nz, kSsp, M, warm)) { status = kSubError; err_site = 1; break; }
             SUB_T1(t_bf);
@@ -1197,6 +1408,16 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         }
         primal = B::all(primal, [](int64_t x, int64_t y) { return x + y; }, W.red);
         unmet = (int)B::any((uint32_t)unmet, W.red);
+#ifdef SGUFP_SUB_VERIFY
+        if (verify_primal != INT64_MIN && verify_primal != primal && status == kSubOptimal) {
+            status = kSubError;
+            err_site = 9;
+        }
+#endif
+        if (io.wstat && tid == 0) {
+            io.wstat[2 * b] = repaired ? warm_augs : (fell_back ? -iters - 1 : iters);
+            io.wstat[2 * b + 1] = W.misc[5];
+        }
         if (status == kSubOptimal) {
             // 4. potentials of the final residual: plain costs (optimal duals) or big-M
             //    costs (their M-multiple is a dual ray, case (iii))
@@ -1219,6 +1440,18 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         }
     }
 
+    // the final state for later warm starts: potentials now, flows per arc with the chain walk
+    // below (zeros first: arcs outside complete chains carry none)
+    const bool save = wdst >= 0 && status == kSubOptimal;
+    GBL int16_t *xs = save ? io.wst_x + ((size_t)wdst * S + s) * m : nullptr;
+    if (save) {
+        GBL int32_t *as = io.wst_a + ((size_t)wdst * S + s) * n;
+        for (int a = tid; a < m; a += T) xs[a] = 0;
+        for (int v = tid; v < n; v += T) as[v] = (int32_t)W.alpha[v];
+        __threadfence();
+        B::sync();
+    }
+
     // 5. dual solution / ray and the scenario's cut contribution
     int64_t rhs = 0, dual = 0;
     bool ok = true;
@@ -1231,6 +1464,17 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
                                         (k == ray_chain) ? ray_q : -1, ok);
             rhs += c.rhs;
             dual += c.obj;
+            if (save) {
+                const uint64_t ca = W.ra(k);
+                const int x = ch_x(W.rb(k));
+                if (x && ch_t(ca) >= 0 && ch_h(ca) >= 0)
+                    for (int e = a, len = 0; e >= 0 && len < kMaxChain; len++) {
+                        xs[e] = (int16_t)x;
+                        if (!N.vbar[N.head[e]]) break;
+                        const int d = dec_of(N, io, poff, plen, e);
+                        e = d >= 0 ? d : -1;
+                    }
+            }
         });
         rhs = B::all(rhs, [](int64_t x, int64_t y) { return x + y; }, W.red);
         dual = B::all(dual, [](int64_t x, int64_t y) { return x + y; }, W.red);
@@ -1306,13 +1550,75 @@ __global__ void __launch_bounds__(256) k_sub_reduce(SubNet N, SubIO io) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Warm-start donors (WarmRing): one workgroup per path of the launch.  Every valid ring slot
+// outside this launch's destinations [ptr, ptr + n) is a candidate; the distance is the
+// number of DD layers whose decisions differ (a missing entry counts as -1); ties go to the
+// lowest slot.  Then the path is recorded in its destination slot (ptr + p) mod R.
+__global__ void __launch_bounds__(256) k_warm_pick(SubIO io, WarmRing wr, int ptr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    LDS int16_t *sp = (LDS int16_t *)smem_raw;                       // [Lcap]
+    LDS unsigned long long *red = (LDS unsigned long long *)(smem_raw + (((size_t)wr.Lcap * 2 + 15) & ~(size_t)15));
+    const int p = blockIdx.x;
+    const int n = io.n_paths;
+    if (p >= n) return;
+    int64_t poff, plen;
+    if (io.path_slot) {
+        const int sl = io.path_slot[p];
+        poff = (int64_t)sl * io.path_stride;
+        plen = io.path_len[sl];
+    } else {
+        poff = io.path_off[p];
+        plen = io.path_off[p + 1] - poff;
+    }
+    if (plen > wr.Lcap) plen = wr.Lcap;
+    for (int l = threadIdx.x; l < wr.Lcap; l += blockDim.x) sp[l] = l < plen ? io.paths[poff + l] : (int16_t)-1;
+    __syncthreads();
+    unsigned long long best = ~0ull;
+    for (int c = threadIdx.x; c < wr.R; c += blockDim.x) {
+        const int rel = (c - ptr % wr.R + wr.R) % wr.R;
+        if (rel < n || !wr.valid[c]) continue;
+        const GBL int16_t *q = wr.path + (size_t)c * wr.Lcap;
+        const int ql = wr.plen[c];
+        const int L = ql > (int)plen ? ql : (int)plen;
+        int d = 0;
+        for (int l = 0; l < L; l++) d += (l < ql ? (int)q[l] : -1) != (int)sp[l];
+        const unsigned long long key = (unsigned long long)d << 32 | (unsigned)c;
+        best = key < best ? key : best;
+    }
+    red[threadIdx.x] = best;
+    __syncthreads();
+    for (int h = blockDim.x / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) red[threadIdx.x] = red[threadIdx.x + h] < red[threadIdx.x] ? red[threadIdx.x + h] : red[threadIdx.x];
+        __syncthreads();
+    }
+    const int dst = (ptr + p) % wr.R;
+    if (threadIdx.x == 0) {
+        const unsigned long long b = red[0];
+        const int d = b == ~0ull ? -1 : (int)(b >> 32);
+        wr.src[p] = (d >= 0 && d <= wr.max_dist) ? (int)(b & 0xFFFFFFFFull) : -1;
+        wr.dst[p] = dst;
+        wr.dist[p] = d;
+        wr.plen[dst] = (uint16_t)plen;
+        wr.valid[dst] = 1;
+    }
+    for (int l = threadIdx.x; l < wr.Lcap; l += blockDim.x) wr.path[(size_t)dst * wr.Lcap + l] = sp[l];
+}
+
+hipError_t launch_warm_pick(const SubIO &io, const WarmRing &wr, int ptr, hipStream_t st) {
+    if (io.n_paths <= 0) return hipSuccess;
+    const size_t lds = (((size_t)wr.Lcap * 2 + 15) & ~(size_t)15) + 256 * 8;
+    hipLaunchKernelGGL(k_warm_pick, dim3((unsigned)io.n_paths), dim3(256), lds, st, io, wr, ptr);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
 size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw, int kbytes) {
     size_t off[kSubLdsParts];
     return sub_lds_layout(n, m, nct_cap, nz, nw, off, kbytes);
 }
 
 namespace {
-template <typename KT>
+template <typename KT, bool WARM>
 hipError_t launch_scenarios(const SubNet &N, const SubIO &io, hipStream_t st) {
     constexpr int kb = (int)sizeof(KT);
     size_t lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, 1, kb);
@@ -1329,17 +1635,17 @@ hipError_t launch_scenarios(const SubNet &N, const SubIO &io, hipStream_t st) {
     if (large && !(ev && atoi(ev) == 1)) {
         lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, kLargeWaves, kb);
         if (io.nct_cap <= kRegGroupsLarge * kLargeWaves * kWave && !N.preds_lds)
-            hipLaunchKernelGGL((k_sub_scenario<kRegGroupsLarge, int32_t, kLargeWaves, KT, true>),
+            hipLaunchKernelGGL((k_sub_scenario<kRegGroupsLarge, int32_t, kLargeWaves, KT, true, WARM>),
                                dim3((unsigned)io.n_paths * N.S), dim3(kWave * kLargeWaves), lds, st, N, io);
         else
-            hipLaunchKernelGGL((k_sub_scenario<kRegGroupsLarge, int32_t, kLargeWaves, KT, false>),
+            hipLaunchKernelGGL((k_sub_scenario<kRegGroupsLarge, int32_t, kLargeWaves, KT, false, WARM>),
                                dim3((unsigned)io.n_paths * N.S), dim3(kWave * kLargeWaves), lds, st, N, io);
     } else if (io.nct_cap <= kRegGroupsSmall * kWave && !N.preds_lds) {
         // register groups hold key increments: 64-bit with 64-bit keys, 32-bit with 32-bit keys
-        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsSmall, KT, 1, KT, true>), dim3((unsigned)io.n_paths * N.S),
+        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsSmall, KT, 1, KT, true, WARM>), dim3((unsigned)io.n_paths * N.S),
                            dim3(kWave), lds, st, N, io);
     } else {
-        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsSmall, KT, 1, KT, false>), dim3((unsigned)io.n_paths * N.S),
+        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsSmall, KT, 1, KT, false, WARM>), dim3((unsigned)io.n_paths * N.S),
                            dim3(kWave), lds, st, N, io);
     }
     return hipGetLastError();
@@ -1351,8 +1657,11 @@ hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st) {
     // 32-bit keys (N.key32, host: no lower bound in any scenario, sum_a |r_a| < 2^18, n + 2 <
     // 2^11); SGUFP_SUB_KEY64=1 forces the 64-bit keys (A/B)
     const char *ek = getenv("SGUFP_SUB_KEY64");
-    const hipError_t e = (N.key32 && !(ek && atoi(ek) == 1)) ? launch_scenarios<int32_t>(N, io, st)
-                                                           : launch_scenarios<int64_t>(N, io, st);
+    // warm starts (io.warm_src / warm_dst) only in the 32-bit-key kernels: no lower bounds
+    const bool k32 = N.key32 && !(ek && atoi(ek) == 1);
+    const bool warm = k32 && (io.warm_src || io.warm_dst);
+    const hipError_t e = !k32 ? launch_scenarios<int64_t, false>(N, io, st)
+                              : (warm ? launch_scenarios<int32_t, true>(N, io, st) : launch_scenarios<int32_t, false>(N, io, st));
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_sub_reduce, dim3((unsigned)io.n_paths), dim3(256), 0, st, N, io);
     return hipGetLastError();

@@ -37,6 +37,7 @@ EXPORTS = [
     "sgufp_frontier_peek_size", "sgufp_frontier_peek", "sgufp_balance_plan", "sgufp_comm_allgather_i64",
     "sgufp_dd_build", "sgufp_dd_apply", "sgufp_dd_solution", "sgufp_dd_cutset",
     "sgufp_loopback_create", "sgufp_loopback_destroy", "sgufp_comm_init_loopback",
+    "sgufp_subproblem_warm", "sgufp_subproblem_stats",
 ]
 
 
@@ -155,6 +156,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.sgufp_restricted_paths.argtypes = [P, P, P]
     lib.sgufp_restricted_cutset_size.argtypes = [P, P, P, P]
     lib.sgufp_restricted_cutset.argtypes = [P, P, P, P, P, P, P, P, P]
+    lib.sgufp_subproblem_warm.argtypes = [P, C.c_int, P, P, P, P, P, P, P, P]
+    lib.sgufp_subproblem_stats.argtypes = [P, P, P]
     lib.sgufp_loopback_create.restype = P
     lib.sgufp_loopback_create.argtypes = [C.c_int]
     lib.sgufp_loopback_destroy.restype = None
@@ -514,8 +517,11 @@ class Engine:
             out.append((int(st[k]), int(ex[k]), float(lb[k]), [int(x) for x in buf[off[k]:off[k + 1]]], kids))
         return out
 
-    def subproblem(self, paths: Sequence[Sequence[int]]):
-        """GuroSolver::solveSubProblem for each path on the device.
+    def subproblem(self, paths: Sequence[Sequence[int]], warm_src: Optional[Sequence[int]] = None,
+                   warm_dst: Optional[Sequence[int]] = None):
+        """GuroSolver::solveSubProblem for each path on the device; with warm_src / warm_dst,
+        path k starts from ring slot warm_src[k] and stores its state in warm_dst[k]
+        (sgufp_subproblem_warm).
 
         Returns (type[n], rhs[n], rows[n, n_slots + 1], obj_mean[n]); type 0 optimality,
         1 feasibility, -1 error."""
@@ -530,9 +536,24 @@ class Engine:
         rhs = np.zeros(max(n, 1), dtype=np.float64)
         rows = np.zeros((max(n, 1), self.info.n_slots + 1), dtype=np.float64)
         obj = np.zeros(max(n, 1), dtype=np.float64)
-        self._check(self.lib.sgufp_subproblem(self.ctx, n, _ptr(off), _ptr(flat), _ptr(typ), _ptr(rhs), _ptr(rows),
-                                              _ptr(obj)))
+        if warm_src is None:
+            self._check(self.lib.sgufp_subproblem(self.ctx, n, _ptr(off), _ptr(flat), _ptr(typ), _ptr(rhs),
+                                                  _ptr(rows), _ptr(obj)))
+        else:
+            src = np.asarray(warm_src, dtype=np.int32)
+            dst = np.asarray(warm_dst, dtype=np.int32)
+            self._check(self.lib.sgufp_subproblem_warm(self.ctx, n, _ptr(off), _ptr(flat), _ptr(src), _ptr(dst),
+                                                       _ptr(typ), _ptr(rhs), _ptr(rows), _ptr(obj)))
         return typ[:n], rhs[:n], rows[:n], obj[:n]
+
+    def subproblem_stats(self, n: int):
+        """Per (path, scenario) of the last call: augmenting paths (negative: a warm start fell
+        back cold) and Bellman-Ford passes, each [n, S]."""
+        S = self.info.scenarios
+        a = np.zeros(max(n * S, 1), dtype=np.int32)
+        p = np.zeros(max(n * S, 1), dtype=np.int32)
+        self._check(self.lib.sgufp_subproblem_stats(self.ctx, _ptr(a), _ptr(p)))
+        return a[:n * S].reshape(n, S), p[:n * S].reshape(n, S)
 
     def subproblem_detail(self, n: int):
         """Per (path, scenario) status / primal objective / dual objective of the last call."""

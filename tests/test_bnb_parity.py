@@ -75,6 +75,19 @@ def test_bnb_parity_c5():
     assert seen["relaxed"] > 0 and seen["subproblems"] > 0
 
 
+def test_bnb_parity_c4_at_timed_pool_size():
+    """The pool sizes the timed B&B legs run against (10^4 cuts, not the 10^2-10^3 of the
+    round-by-round checks above): the seeded C4 / 256 search with uncapped refinement loops
+    until its optimality list holds 20 000 cuts, then the next 1 024-record batch on the device
+    -- exact records through the cut-parallel phase, non-exact survivors through the batched
+    sweeps -- against ref_dd relaxp on the same pool, bit for bit, 8 records of each outcome."""
+    rep = bp.check_large_pool("C4", 1, 128, min_opt_cuts=20000, per_kind=8)
+    assert not rep["failures"], "\n".join(rep["failures"][:10])
+    assert rep["pool_optimality"] >= 20000, rep
+    assert rep["sampled"]["exact"] >= 1 and rep["sampled"]["survivor"] >= 1, rep
+    assert rep["checked"] >= 8
+
+
 @pytest.mark.parametrize("knob,value", [("SGUFP_EXACT_FAST", "0"), ("SGUFP_EXACT_LAZY", "1"),
                                         ("SGUFP_EXACT_SCREEN", "64")])
 def test_bnb_parity_exact_phase_variants(monkeypatch, knob, value):

@@ -291,3 +291,50 @@ def test_kernel_variants_agree(cfg, seed, S, n_paths, tmp_path):
             np.testing.assert_array_equal(a[k], b[k], err_msg=name)
         for k in ("rhs", "rows", "obj_mean", "obj", "dual"):
             np.testing.assert_array_equal(a[k].view(np.uint64), b[k].view(np.uint64), err_msg=f"{name}: {k}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,seed,S,n_paths", [("C3", 4, 8, 12), ("C4", 1, 256, 4), ("C5", 4, 2, 4)])
+@pytest.mark.parametrize("lib", ["prod", "verify"])
+def test_warm_start_matches_cold(cfg, seed, S, n_paths, lib, tmp_path):
+    """Warm-started subproblems (sgufp_subproblem_warm; the B&B's refinement loops use them):
+    neighbours of solved paths -- the decisions of their last DD layers redrawn, as the exact
+    leaves the B&B solves one after another differ -- start from the stored optimal flow and
+    potentials and repair the imbalance.  Every scenario's status and objective must equal
+    the cold solve's exactly (integral data), the dual objective must equal the primal (the
+    kernel's certificate), the cut must be tight at its path, and the repair must take fewer
+    augmenting paths than the cold solve.  The verify build re-solves every repaired scenario
+    cold inside the kernel and flags any objective difference as an error."""
+    import subprocess
+    import sys
+    from sgufp_solver_amd import engine as E
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    helper = os.path.join(here, "tests", "helpers", "sub_run.py")
+    env = dict(os.environ)
+    env.pop("SGUFP_LIB_PATH", None)
+    if lib == "verify":
+        env["SGUFP_LIB_PATH"] = os.path.join(here, "sgufp_solver_amd", "lib_verify", "libsgufp_hip.so")
+    out = str(tmp_path / "warm.npz")
+    subprocess.run([sys.executable, helper, cfg, str(seed), str(S), str(n_paths), out, "warm"], env=env, check=True,
+                   timeout=240)
+    r = np.load(out)
+    assert (r["seed_st"] == 0).all()
+    assert (r["st"] == 0).all(), f"warm statuses {np.unique(r['st'])} (2 = error / verify mismatch)"
+    assert (r["cold_st"] == 0).all()
+    np.testing.assert_array_equal(r["obj"], r["cold_obj"])
+    np.testing.assert_array_equal(r["dual"], r["obj"])
+    assert (r["typ"] == 0).all()
+    np.testing.assert_array_equal(r["obj_mean"].view(np.uint64), r["cold_obj_mean"].view(np.uint64))
+    aug, cold = r["warm_aug"], r["cold_aug"]
+    if lib == "prod":
+        assert (aug[:-1] >= 0).all(), "a warm start fell back to the cold solve"
+        assert aug[:-1].mean() < 0.5 * cold[:-1].mean(), (aug.mean(), cold.mean())
+    # the warm cut is tight at its path (RHS + coef . y-bar == mean objective)
+    inst, path, net = _net(cfg, seed, S, True)
+    eng = E.Engine(path, 0, 8)
+    keys = _keys(eng)
+    eng.close()
+    for k in range(n_paths):
+        y = so.ybar_of_path(net, [int(x) for x in r["paths"][k]])
+        v = _cut_at(r["rhs"][k], r["rows"][k], keys, y)
+        assert abs(v - r["obj_mean"][k]) <= 1e-7 * max(1.0, abs(r["obj_mean"][k])), (k, v, r["obj_mean"][k])

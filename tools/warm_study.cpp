@@ -319,6 +319,48 @@ int main(int argc, char **argv) {
     }
     np = min(np, maxp);
     const bool scen = argc > 5 && argv[5][0] == 's';   // warm from the previous scenario of the same path
+    const bool nearest = argc > 5 && argv[5][0] == 'n';   // warm from the nearest of the last 256 paths
+    if (nearest) {
+        Counts warm2;
+        ll nsolve2 = 0, ndist = 0;
+        for (int s = s0; s < s0 + ns && s < I.S; s++) {
+            std::vector<State> ring(256);
+            std::vector<int> ring_p(256, -1);
+            for (int p = 0; p < np; p++) {
+                const auto ch = chains_of(I, paths[p], s);
+                int best = -1, bd = INT_MAX;
+                for (int r = 0; r < 256; r++) {
+                    if (ring_p[r] < 0) continue;
+                    const auto &a = paths[ring_p[r]], &b = paths[p];
+                    int d = 0;
+                    for (size_t i = 0; i < max(a.size(), b.size()); i++)
+                        d += (i < a.size() ? a[i] : -1) != (i < b.size() ? b[i] : -1);
+                    if (d < bd) { bd = d; best = r; }
+                }
+                Flow F;
+                vector<int> ca, zs, zt;
+                if (best >= 0) {
+                    ll it = 0;
+                    solve_warm(I, ch, ring[best], F, ca, zs, zt, warm2, &it);
+                    nsolve2++;
+                    ndist += bd;
+                } else {
+                    Flow Fs;
+                    vector<int> ca_s;
+                    Counts tmp;
+                    solve_cold(I, ch, Fs, ca_s, tmp);
+                    cold_to_merged(I, ch, Fs, ca_s, F, ca, zs, zt);
+                }
+                const int slot = p % 256;
+                save_state(I, ch, F, ca, zs, zt, ring[slot]);
+                ring_p[slot] = p;
+            }
+        }
+        const double k = nsolve2 ? (double)nsolve2 : 1.0;
+        printf("{\"mode\": \"nearest\", \"solves\": %lld, \"warm_sp\": %.2f, \"warm_aug\": %.2f, \"dist\": %.2f}\n",
+               nsolve2, warm2.sp / k, warm2.aug / k, ndist / k);
+        return 0;
+    }
     Counts cold, warm;
     if (scen) {
         ll imb = 0, nsolve = 0;

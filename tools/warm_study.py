@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--ns", type=int, default=2)
     ap.add_argument("--max-paths", type=int, default=200)
     ap.add_argument("--first", type=int, default=0, help="skip the first paths")
-    ap.add_argument("--mode", choices=["path", "scen"], default="path",
+    ap.add_argument("--mode", choices=["path", "scen", "nearest"], default="path",
                     help="path: warm from the previous path (same scenario); scen: from the previous scenario")
     ap.add_argument("--order", choices=["solve", "record"], default="solve",
                     help="solve: the B&B's order; record: grouped by (round, record)")
