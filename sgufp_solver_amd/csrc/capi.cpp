@@ -119,6 +119,8 @@ bool sgufp_ctx::init() {
     if (const char *e = getenv("SGUFP_SUB_WARM")) warm_on = atoi(e) != 0;   // warm-started subproblems (A/B)
     if (const char *e = getenv("SGUFP_EXACT_SCREEN")) exact_screen = std::max(0, std::min(kExactScreen, atoi(e)));
     if (const char *e = getenv("SGUFP_EXACT_LAZY")) exact_lazy = std::max(0, atoi(e));
+    if (const char *e = getenv("SGUFP_NX")) nx_on = atoi(e) != 0;
+    if (const char *e = getenv("SGUFP_NX_MIN")) nx_min = std::max(1, atoi(e));
     int64_t acap = std::max<int64_t>(1, (int64_t)std::max(0, L - 4) * (kRelaxedMaxWidth - 1) * maxU);
     if (ncap > (int64_t)kParentMask || acap > (int64_t)0x7FFFFFFF) { err = "DD capacity beyond 22-bit indices"; return false; }
     sc.Ncap = (int)ncap;
@@ -325,8 +327,9 @@ bool sgufp_ctx::exact_prepare() {
         ocap = cap;
     }
     if (!d_pslot && (!alloc(d_pslot, (size_t)max_batch, "exact pending") || !alloc(d_pbase, (size_t)max_batch, "exact pending") ||
-                     !alloc(d_ectr, 6, "exact pending") || !alloc(d_pidx, (size_t)max_batch, "exact pending")))
+                     !alloc(d_ectr, 10, "exact pending") || !alloc(d_pidx, (size_t)max_batch, "exact pending")))
         return false;
+    if (!nx_prepare(no)) return false;
     if (o_built < no) {
         if (!hip_ok(launch_exact_cols(d_rows, d_rhs, d_oorder, no, o_built, net.n_slots + 1, net.n_slots, ocap, d_coefO,
                                       1, stream), "k_exact_cols"))
@@ -345,7 +348,7 @@ bool sgufp_ctx::exact_prepare() {
     }
     ex.coefS = d_coefS;
     ex.RS = d_RS;
-    if (!hip_ok(hipMemsetAsync(d_ectr, 0, 6 * sizeof(unsigned long long), stream), "memset") ||
+    if (!hip_ok(hipMemsetAsync(d_ectr, 0, 10 * sizeof(unsigned long long), stream), "memset") ||
         !hip_ok(hipMemsetAsync(d_pidx, 0xFF, (size_t)max_batch * sizeof(int32_t), stream), "memset"))
         return false;
     ex.lazy = ex.nsc == 0 ? exact_lazy : 0;
@@ -357,6 +360,39 @@ bool sgufp_ctx::exact_prepare() {
     ex.pend_slot = d_pslot;
     ex.pend_base = d_pbase;
     ex.ctr = d_ectr;
+    return true;
+}
+
+// Buffers of the non-exact hand-off (ExactIO::nx): per pending entry its kind and pruning
+// position, per (entry, O cut) the pruning gap and maxState (as wide as the root folds), a
+// small header per slot.  Only under pools of nx_min O cuts or more, with the batched sweeps
+// (aligned records, packed topology); a device without the memory runs every record in
+// k_relax (same results).
+bool sgufp_ctx::nx_prepare(int no) {
+    ex.nx = 0;
+    ex.redo = 0;
+    ex.nx_min = nx_min;
+    ex.pkind = nullptr;
+    if (!nx_on || no < nx_min || cb <= 1) return true;
+    const size_t B = (size_t)max_batch;
+    if (!d_nxh && (!alloc(d_nxh, B * 4, "nx header") || !alloc(d_pkind, B, "nx pending") || !alloc(d_P, B, "nx pending")))
+        return false;
+    if (nx_cap < ocap) {
+        size_t fr = 0, tot = 0;
+        const size_t have = (size_t)nx_cap * B * 16;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && (size_t)ocap * B * 16 > (fr + have) / 2) return true;
+        if (d_G) release(d_G);
+        if (d_MS) release(d_MS);
+        nx_cap = 0;
+        if (!alloc(d_G, B * (size_t)ocap, "nx gaps") || !alloc(d_MS, B * (size_t)ocap, "nx maxState")) return false;
+        nx_cap = ocap;
+    }
+    ex.nx = 1;
+    ex.pkind = d_pkind;
+    ex.P = d_P;
+    ex.G = d_G;
+    ex.MS = d_MS;
+    ex.nxh = d_nxh;
     return true;
 }
 
@@ -381,19 +417,19 @@ bool sgufp_ctx::emit_current(const BatchIn &in, const Pool &p) {
         if (!download(&tot[0], d_coff + in.n, 1) || !download(&tot[1], d_soff + in.n, 1)) return false;
     }
     if (!sync()) return false;
-    static const bool estats = [] {
-        const char *e = std::getenv("SGUFP_EXACT_STATS");
-        return e && e[0] == '1';
-    }();
+    const char *es = std::getenv("SGUFP_EXACT_STATS");   // diagnostics (tests read them from stderr)
+    const bool estats = es && es[0] == '1';
     if (estats && ex.enabled) {
-        unsigned long long c[6];
-        if (download(c, d_ectr, 6) && sync())
+        unsigned long long c[10];
+        if (download(c, d_ectr, 10) && sync())
             std::fprintf(stderr,
                          "[exact] pending %llu passes %llu blocks swept %llu of %llu (no %d, screen %d, lazy %d: "
-                         "%llu resolves, %llu blocks)\n",
+                         "%llu resolves, %llu blocks); non-exact: dag items %llu, fallbacks %llu, kept back "
+                         "(ranks %llu, tail %llu, segment %llu, program %llu, other %llu)\n",
                          c[0] >> 32, c[0] & 0xFFFFFFFFull, c[3],
                          (c[0] & 0xFFFFFFFFull) * (unsigned long long)((ex.no + 63) / 64 + (ex.nsc + 63) / 64), ex.no,
-                         ex.nsc, ex.lazy, c[4], c[5]);
+                         ex.nsc, ex.lazy, c[4], c[5], c[6], c[7], c[9] & 1023, (c[9] >> 10) & 1023, (c[9] >> 20) & 1023,
+                         (c[9] >> 30) & 1023, (c[9] >> 40) & 1023);
     }
     total_children = (int64_t)tot[0];
     total_csol = (int64_t)tot[1];

@@ -24,7 +24,7 @@ namespace sgufp {
 struct Transport;   // shard.cpp
 // dd_kernels.hip
 size_t relax_lds_bytes(int Tcap, int Lcap, int cb, int us);
-size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw, int kbytes = 8);
+size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw, int kbytes = 8, bool warm = false);
 hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st);
 hipError_t launch_warm_pick(const SubIO &io, const WarmRing &wr, int ptr, hipStream_t st);
 hipError_t launch_relax(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &, double, int,
@@ -245,6 +245,14 @@ struct sgufp_ctx {
     unsigned long long *d_ectr = nullptr;
     int32_t *d_pidx = nullptr;
     int exact_lazy = 0;                       // ExactIO::lazy (SGUFP_EXACT_LAZY)
+    // the same for non-exact DDs under large pools (nx_kernels: SGUFP_NX=0 off, SGUFP_NX_MIN)
+    bool nx_on = false;
+    int nx_min = 2048;
+    int32_t *d_pkind = nullptr, *d_P = nullptr, *d_nxh = nullptr;
+    double *d_G = nullptr;
+    unsigned long long *d_MS = nullptr;
+    int nx_cap = 0;                           // columns of G / MS allocated
+    bool nx_prepare(int no);
     bool exact_prepare();
 
     bool timing = false;

@@ -39,6 +39,10 @@ constexpr uint8_t kInAlive = 2;    // its (single, exact-layer) incoming arc is 
 constexpr uint8_t kKill = 4;       // scheduled for deletion in the current cascade
 constexpr uint8_t kLazy = 8;       // exact DD leaf: tw is an upper bound (ExactIO::lazy), see exact_resolve
 
+// packed topology word of a narrow layer (Scratch::tmir, build_stream in dd_kernels.hip):
+// parent:7 | rank:5 | alive | in-arc alive
+constexpr uint16_t kMirParent = 127, kMirRankShift = 7, kMirAlive = 1u << 12, kMirIn = 1u << 13;
+
 // topology word: parent index inside the previous layer (22 bits) | decision rank (6 bits)
 constexpr uint32_t kParentMask = (1u << 22) - 1;
 constexpr uint32_t kRankShift = 22;
@@ -209,8 +213,9 @@ struct ExactIO {
     double SGUFP_GBL *R;                  // [max_batch][ostride]: root folds, pending index x newest-first position
     int32_t SGUFP_GBL *pend_slot;         // [max_batch] batch slot of pending record i
     uint32_t SGUFP_GBL *pend_base;        // [max_batch] first leaf pass of pending record i
-    unsigned long long SGUFP_GBL *ctr;    // [6]: (pending << 32 | leaf passes), root work, leaf work,
-                                          // blocks swept, lazy resolves, blocks they swept
+    unsigned long long SGUFP_GBL *ctr;    // [10]: (pending << 32 | leaf passes), root work, leaf work,
+                                          // blocks swept, lazy resolves, blocks they swept, non-exact:
+                                          // DAG work, fallbacks, leaf work
     // Lazy terminal weights: a leaf pass sweeps at most `lazy` cut blocks (the newest 64 x lazy
     // O cuts); when that leaves some leaf above optimalLB the pass's leaves keep the partial
     // minimum (an upper bound of the terminal weight) flagged kLazy, and the argmax scans
@@ -225,8 +230,33 @@ struct ExactIO {
     int nsc;
     const double SGUFP_GBL *coefS;        // [n_slots + 2][kExactScreen]
     double SGUFP_GBL *RS;                 // [max_batch][kExactScreen]
+    // Cut-parallel optimality phase of NON-exact DDs (nx_kernels.hip, see kNxPending): pending
+    // entries of both kinds share the index space, root folds and leaf passes above.
+    int nx;                               // 1: k_relax hands such records off
+    int nx_min;                           // ... when the pool holds at least this many O cuts
+    int redo;                             // k_relax re-run: only the kNxFallback slots, no hand-off
+    int32_t SGUFP_GBL *pkind;             // [max_batch] per pending entry: -1 exact, else the DAG's last width-1 layer k0
+    int32_t SGUFP_GBL *P;                 // [max_batch] first pruning position (max over leaves of the first cut <= optimalLB)
+    double SGUFP_GBL *G;                  // [max_batch][ostride] width-1 pruning gap per cut (k_nx_dag), lowered by its error bound
+    unsigned long long SGUFP_GBL *MS;     // [max_batch][ostride] maxState per cut (order-preserving key, atomic max)
+    int32_t SGUFP_GBL *nxh;               // [nslots][4] per handed-off slot: k0, packed node words, k0's node
 };
 constexpr int kExactScreen = 256;
+
+// Non-exact DDs (nx_kernels.hip).  Past the feasibility phase an optimality cut edits a
+// non-exact DD only when a width-1 layer's arc pruning fires (DD.cpp:3986-4022); a pool that
+// fires nowhere leaves the optimality phase order-free like an exact DD's: per-leaf running
+// minima, the terminal state non-increasing, so the record is pruned at the first cut where
+// every leaf's minimum is <= optimalLB, else ub = the last terminal state.  Below the last
+// width-1 layer k0 the DD is a tree (merged layers have one node), so the leaf passes of
+// k_exact_leaf apply with the value at k0 as their root; above it k_nx_dag sweeps each cut's
+// values through the DAG (lanes = node groups x cuts) into that root value and a conservative
+// per-cut gap of the width-1 pruning test.  k_nx_fin checks that no cut before the pruning position can
+// fire; a record where one might (status kNxFallback) is re-run by k_relax in order.
+constexpr int32_t kNxPending = 6;
+constexpr int32_t kNxFallback = 7;
+constexpr int kNxRanks = 4;     // nonzero state ranks (ustride <= 5)
+constexpr int kNxCuts = 16;     // cuts per k_nx_dag work item (lanes = 4 node groups x 16 cuts)
 
 // Seen-path lists of the exact DDs' refinement loops (bnb_kernels.hip), per batch slot.
 struct SeenLists {

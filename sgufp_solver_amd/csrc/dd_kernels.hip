@@ -114,7 +114,6 @@ constexpr int kTopoEntries = 512;    // topology staging ring: u16 entries per s
 constexpr int kStageLayers = 16;     // at most this many layers per staging group
 constexpr int kMaxRun = 5;           // exact layers folded in registers per narrow-sweep step (odd)
 constexpr uint32_t kNarrowMax = 127;  // widest narrow layer; value slot 127 holds the NaN sentinel
-constexpr uint16_t kMirParent = 127, kMirRankShift = 7, kMirAlive = 1u << 12, kMirIn = 1u << 13;
 
 // Packed topology of the narrow layers (HBM, per DD slot): node word = parent:7 | rank:5 |
 // alive | in-arc alive for nodes [0, Nn), merged-arc word = parent:7 | rank:5 | alive for
@@ -1828,6 +1827,51 @@ struct LoopState {
 #endif
 };
 
+// ------------------------------------------------------------------------------------
+// Hand-off of a non-exact DD to the cut-parallel optimality phase (kNxPending, see
+// dd_device.hpp).  k_nx_dag sweeps the layers 1 .. k0 (k0 = the last width-1 layer <= T-2)
+// layer by layer with lanes = (node group, cut) from the packed topology words build_stream
+// left in the slot (tmir: every layer below kg has <= 127 nodes); the leaf passes take the
+// tree below k0.  Kept back (the record stays in k_relax): k0 at or past kg, more than
+// kNxRanks + 1 state ranks, or a deeper / wider tail than the leaf passes stage.
+// diagnostics: ExactIO::ctr[9] counts the DDs kept back, 10 bits per reason
+__device__ __forceinline__ bool nx_refuse(const ExactIO &ex, int why) {
+    if (lane() == 0) atomicAdd(&ex.ctr[9], 1ull << (10 * why));
+    return false;
+}
+
+__device__ bool nx_compile(const DD &d, const Scratch &sc, const ExactIO &ex, int slot, int &k0_out) {
+    const int T = d.T;
+    if (T < 3 || d.us > kNxRanks + 1 || !d.stream) return nx_refuse(ex, 0);
+    int k0 = 0;
+    for (int base = 0; base <= T - 2; base += kWave) {
+        const int k = base + lane();
+        const uint64_t b = __ballot(k <= T - 2 && d.nalive[k] == 1u);
+        if (b) k0 = base + 63 - __clzll((long long)b);
+    }
+    k0 = uni(k0);
+    const int D = T - 1 - k0;
+    if (D < 1 || D > kExactMaxT - 1 || D * d.us > kExactMaxEntries) return nx_refuse(ex, 1);
+    if (k0 >= d.kg) return nx_refuse(ex, 2);
+    // the single alive node of layer k0 (its index: the leaf passes' root)
+    const uint32_t noff = uni(d.noff[k0]), n = uni(d.nn[k0]);
+    uint32_t q = 0xFFFFFFFFu;
+    for (uint32_t base = 0; base < n && q == 0xFFFFFFFFu; base += kWave) {
+        const uint32_t i = base + lane();
+        const uint64_t b = __ballot(i < n && (d.nflag[noff + i] & kAlive));
+        if (b) q = base + (uint32_t)(__ffsll((unsigned long long)b) - 1);
+    }
+    if (q == 0xFFFFFFFFu) return nx_refuse(ex, 3);
+    if (lane() == 0) {
+        GBL int32_t *h = ex.nxh + (size_t)slot * 4;
+        h[0] = k0;
+        h[1] = (int32_t)d.Nn;
+        h[2] = (int32_t)q;
+    }
+    k0_out = k0;
+    return true;
+}
+
 // one cut at a time from pool position s onwards; efast: an exact DD leaves at the first
 // optimality cut for the cut-parallel kernels (kExactPending, exact_kernels.hip)
 __device__ __forceinline__ void cut_loop_single(const NetDev &net, DD &d, const Pool &pool, double incumbent, int s, LoopState &st,
@@ -2153,7 +2197,8 @@ __device__ __forceinline__ bool screen_opt(const NetDev &net, DD &d, BatchView &
 
 template <int CB>
 __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const Scratch &sc, BatchView &bv, const Pool &pool,
-                                 double incumbent, LoopState &st, bool efast) {
+                                 double incumbent, LoopState &st, bool efast, const ExactIO *nx = nullptr, int slot = 0,
+                                 int *nx_k0 = nullptr) {
     const int total = pool.nf + pool.no;
     const int last = d.T - 1;
     bv.gbase = uni(d.noff[d.kg]);
@@ -2172,6 +2217,11 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
             if (pruned) { st.status = kPrunedOptimality; return; }
         }
         if (!feas && efast) { st.status = kExactPending; return; }
+        // a non-exact DD under a large pool: the cut-parallel phase takes it from here (once)
+        if (!feas && nx && s == pool.nf) {
+            if (nx_compile(d, sc, *nx, slot, *nx_k0)) { st.status = kNxPending; return; }
+            nx = nullptr;
+        }
         const int nb = min(CB, (feas ? pool.nf : total) - s);
         if (lane() < nb) bv.ids[lane()] = seq_id(pool, s + lane());
         for (int k = lane(); k < d.T; k += kWave) bv.w1[k] = ((d.nalive[k]) == 1) ? 1 : 0;
@@ -2293,6 +2343,9 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
     LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
     if ((int)blockIdx.x >= in.n) return;
     const int slot = in.perm ? in.perm[blockIdx.x] : (int)blockIdx.x;
+    // the re-run after the cut-parallel phase of non-exact DDs: only the records it could
+    // not settle (kNxFallback), in order, from scratch
+    if (ex.redo && out.status[slot] != kNxFallback) return;
 #ifdef SGUFP_PHASES
     const uint64_t t_start = wall_clock64();
 #endif
@@ -2316,6 +2369,7 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
     double lb = DMIN;
     uint32_t nchild = 0, n_nodes = 0, n_arcs = 0, n_merged = 0;
     bool efast = false;
+    int nx_k0 = -1;
     d.T = 1; d.exact = 1;
 
     if (!in.valid[slot] || d.len > d.g || d.g > net.L || d.len > sc.Lcap) {
@@ -2371,7 +2425,8 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
         bv.sm = sc.sm + (size_t)slot * sc.Tcap * CB;
         bv.xm = sc.xm + (size_t)slot * sc.Tcap * CB;
         build_stream(d, n_merged, CB * pool.ustride);   // tmir_cap = Ncap + Acap >= Nn + Amir
-        if (d.stream) cut_loop_batched<CB>(net, d, sc, bv, pool, incumbent, st, efast);
+        const bool nxtry = ex.enabled && ex.nx && !ex.redo && !d.exact && pool.no >= ex.nx_min;
+        if (d.stream) cut_loop_batched<CB>(net, d, sc, bv, pool, incumbent, st, efast, nxtry ? &ex : nullptr, slot, &nx_k0);
         else cut_loop_single(net, d, pool, incumbent, 0, st, efast);
 #if defined(SGUFP_PROF) && defined(SGUFP_PHASES)
         st.ph[6] += bv.prof[0];
@@ -2381,10 +2436,11 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
         cut_loop_single(net, d, pool, incumbent, 0, st, efast);
     }
     st.stamp(6);
-    if (st.status == kExactPending) {
+    if (st.status == kExactPending || st.status == kNxPending) {
         // hand-off: the root solution's slots for k_exact_root, then one pending entry and
         // this record's leaf passes (a single 64-bit atomic keeps the pass bases ascending
-        // with the entry index, which k_exact_leaf's item search relies on)
+        // with the entry index, which k_exact_leaf's item search relies on); a non-exact DD
+        // also records its tail's root layer k0 and starts its pruning position at 0
         GBL int32_t *rs = sc.rslot + (size_t)slot * sc.Lcap;
         for (int t = lane(); t < d.len; t += kWave) rs[t] = (int32_t)d.rslot[t];
         if (lane() == 0) {
@@ -2395,6 +2451,10 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
             ex.pend_slot[i] = slot;
             ex.pend_base[i] = (uint32_t)(old & 0xFFFFFFFFull);
             ex.pidx[slot] = i;
+            if (ex.pkind) {
+                ex.pkind[i] = st.status == kNxPending ? nx_k0 : -1;
+                ex.P[i] = 0;
+            }
         }
     }
     if (st.status == kSuccess) {
@@ -2806,6 +2866,7 @@ __global__ void __launch_bounds__(kWave) k_exact_fin(NetDev net, Scratch sc, Bat
     const int i = blockIdx.x;
     if (i >= (int)(ex.ctr[0] >> 32)) return;
     const int slot = ex.pend_slot[i];
+    if (out.status[slot] != kExactPending) return;   // a non-exact entry: k_nx_fin's
     DD d;
     dd_bind(d, smem, sc, slot);
     load_meta_layers(d, sc, slot);
@@ -2830,6 +2891,116 @@ __global__ void __launch_bounds__(kWave) k_exact_fin(NetDev net, Scratch sc, Bat
         out.sweeps[slot] += (uint32_t)pool.no;
     }
     store_meta_layers(d, sc, slot, last_cut, status, 0, ub);
+}
+
+// ------------------------------------------------------------------------------------
+// Kernel 5: end of the cut-parallel optimality phase of non-exact DDs (kNxPending, see
+// dd_device.hpp).  p = the first pool position where every leaf's running minimum is <=
+// optimalLB (the terminal state, a maximum of those minima, only decreases, so the reference
+// prunes there: applyOptimalityCut returns it and process stops, NodeExplorer.cpp:975-983).
+// The width-1 pruning of DD.cpp:3986-4022 runs at a cut only when its terminal state is >
+// optimalLB, i.e. at the positions before p; it removes an arc iff fl(fl(s + w) + gain) <=
+// optimalLB - 0.01, i.e. (rounding is monotone) fl(xmin + fl(maxState - state2)) <= it for
+// some width-1 layer.  k_nx_dag's per-cut gap G (a lower bound of min over the layers of
+// xmin - state2 up to rounding) and the leaf passes' maxState decide conservatively: if no
+// position before p can fire, no edit happened and the cut-parallel result is the
+// reference's; otherwise the record is marked kNxFallback for k_relax's in-order re-run.
+// Pruned: PRUNED_BY_OPTIMALITY_CUT at p.  Not pruned: ub = smin(last terminal state, ub)
+// (the running smin over non-increasing states keeps the last), the DD's state2 set by the
+// last (oldest) optimality cut's sweep for getCutset, and the cutset as k_relax's finish.
+__device__ __forceinline__ double nx_unkey(unsigned long long k) {
+    const unsigned long long b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+    return __longlong_as_double((long long)b);
+}
+
+__global__ void __launch_bounds__(kWave) k_nx_fin(NetDev net, Scratch sc, BatchIn in, Pool pool, BatchOut out,
+                                                  ExactIO ex, double incumbent) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    LDS uint8_t *smem = (LDS uint8_t *)smem_raw;
+    const int i = blockIdx.x;
+    if (i >= (int)(ex.ctr[0] >> 32)) return;
+    const int slot = ex.pend_slot[i];
+    if (out.status[slot] != kNxPending) return;
+    const int p = ex.P[i];
+    const int lim = p < pool.no ? p : pool.no;
+    const double thresh = incumbent - 0.01;
+    const size_t base = (size_t)i * ex.ostride;
+    bool fire = false;
+    for (int c0 = 0; c0 < lim && !fire; c0 += kWave) {
+        const int c = c0 + lane();
+        bool f = false;
+        if (c < lim) {
+            const double gv = ex.G[base + c];
+            const double M = nx_unkey(ex.MS[base + c]);
+            f = !((gv + M) - 1e-12 * (fabs(M) + fabs(thresh) + 1.0) > thresh);   // NaN: may fire
+        }
+        fire = __ballot(f) != 0;
+    }
+    GBL int32_t *meta = sc.meta + (size_t)slot * 8;
+    if (fire) {
+        if (lane() == 0) {
+            out.status[slot] = kNxFallback;
+            atomicAdd(&ex.ctr[7], 1ull);
+        }
+        return;
+    }
+    if (p < pool.no) {
+        if (lane() == 0) {
+            out.status[slot] = kPrunedOptimality;
+            out.lb[slot] = DMIN;
+            out.ub[slot] = DMIN;
+            out.sweeps[slot] += (uint32_t)(p + 1);
+            meta[5] = pool.o_order[p];
+            meta[6] = kPrunedOptimality;
+            sc.ubv[slot] = DMIN;
+        }
+        return;
+    }
+    DD d;
+    dd_bind(d, smem, sc, slot);
+    load_meta_layers(d, sc, slot);
+    const VP best = exact_argmax(net, d, ex, -1, incumbent);
+    const double term = (best.p == INT_MIN) ? DMIN : smax(DMIN, best.v);
+    double ub = smin(term, sc.ubv[slot]);
+    int status = kSuccess, cut_layer = 0;
+    uint32_t nchild = 0;
+    const int last_cut = pool.o_order[pool.no - 1];
+    if (ub <= incumbent) {
+        status = kPrunedOptimality;   // not reached: p says some leaf stays above optimalLB
+    } else {
+        const GBL int32_t *rs = sc.rslot + (size_t)slot * sc.Lcap;
+        for (int t = lane(); t < d.len; t += kWave) d.rslot[t] = (int16_t)rs[t];
+        wave_lds_sync();
+        const GBL double *row = pool.rows + (size_t)last_cut * pool.stride;
+        dd_sweep(net, d, row, root_fold(row, pool.rhs[last_cut], d));
+        int k = 3;
+        while (k < d.T && uni(d.nalive[k]) != 1) k++;
+        if (k >= d.T) {
+            status = kErrCutset;
+        } else {
+            cut_layer = k;
+            const uint32_t M = layer_single(d, k);
+            if (uni(d.acnt[k])) {
+                const uint32_t aoff = uni(d.aoff[k]), acnt = uni(d.acnt[k]);
+                for (uint32_t b = 0; b < acnt; b += kWave) {
+                    const uint32_t a = b + lane();
+                    nchild += wave_sum((a < acnt && (d.aflag[aoff + a] & kAlive)) ? 1u : 0u);
+                }
+            } else {
+                nchild = (d.nflag[M] & kInAlive) ? 1u : 0u;
+            }
+        }
+    }
+    if (status != kSuccess) ub = DMIN;
+    if (lane() == 0) {
+        out.status[slot] = status;
+        out.lb[slot] = DMIN;
+        out.ub[slot] = ub;
+        out.nchild[slot] = nchild;
+        out.sol_need[slot] = nchild * (uint32_t)(d.len + cut_layer);
+        out.sweeps[slot] += (uint32_t)pool.no;
+    }
+    store_meta_layers(d, sc, slot, last_cut, status, cut_layer, ub);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2881,6 +3052,19 @@ hipError_t launch_relax(const NetDev &net, const Scratch &sc, const BatchIn &in,
     if ((e = launch_exact(net, sc, ex, incumbent, cus, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_exact_fin, dim3(in.n), dim3(kWave), relax_lds_bytes(sc.Tcap, sc.Lcap, 1, sc.us), st, net, sc, in,
                        pool, out, ex, incumbent);
+    if ((e = hipGetLastError()) != hipSuccess || !ex.nx || !ex.pkind) return e;
+    // non-exact DDs: outcome, then k_relax again over the records whose pruning might have fired
+    hipLaunchKernelGGL(k_nx_fin, dim3(in.n), dim3(kWave), relax_lds_bytes(sc.Tcap, sc.Lcap, 1, sc.us), st, net, sc, in,
+                       pool, out, ex, incumbent);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    ExactIO rx = ex;
+    rx.redo = 1;
+    switch (cb) {
+        case 4: hipLaunchKernelGGL(k_relax<4>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent, rx); break;
+        case 8: hipLaunchKernelGGL(k_relax<8>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent, rx); break;
+        case 16: hipLaunchKernelGGL(k_relax<16>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent, rx); break;
+        default: hipLaunchKernelGGL(k_relax<1>, dim3(in.n), dim3(kWave), lds, st, net, sc, in, pool, out, incumbent, rx); break;
+    }
     return hipGetLastError();
 }
 

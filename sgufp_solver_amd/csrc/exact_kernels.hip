@@ -30,6 +30,7 @@
 #define SGUFP_MULTI_WAVE_TU 1
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cstdint>
 
 #include "dd_device.hpp"
@@ -177,6 +178,7 @@ __global__ void __launch_bounds__(kRootWaves * kWave) k_exact_root(NetDev net, S
 struct LeafWave {
     uint8_t info[kLeavesPerWave][kExactMaxT];
     uint8_t dv[kLeavesPerWave];
+    int32_t fle[kLeavesPerWave];   // non-exact entries: first cut <= optimalLB per leaf
 };
 
 struct LeafShared {
@@ -186,6 +188,13 @@ struct LeafShared {
     double vb[kLeafWaves][kExactMaxT - 1][kWave];   // ancestor values of the current leaf (layers 0 .. T - 2), per wave
     int32_t item, flags[kLeafWaves];
 };
+
+// order-preserving key of a double (unsigned compare = numeric order, -0 below +0): the
+// per-cut maxState of a non-exact record is an atomic max over its leaf passes
+__device__ __forceinline__ unsigned long long nx_key(double x) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
 
 // running min of a lane's cuts meeting a path value (std::min(w, v): keeps w on ties)
 __device__ __forceinline__ double rmin(double w, double v) { return (v < w) ? v : w; }
@@ -230,6 +239,9 @@ __device__ double first_zero(const NetDev &net, const ExactIO &ex, LeafShared &S
 #ifndef SGUFP_LEAF_MIN_WAVES
 #define SGUFP_LEAF_MIN_WAVES 6   // three 8-wave workgroups per CU (VGPRs <= 85)
 #endif
+// NX: the instantiation for the non-exact entries (k_nx_dag's roots), which pulls its items
+// from its own counter and skips the exact ones (and the other way round)
+template <bool NX>
 __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_exact_leaf(NetDev net, Scratch sc, ExactIO ex, double incumbent) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LeafShared &S = *(LeafShared *)smem_raw;
@@ -242,7 +254,7 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
     const int nblk = nbs + (ex.no + kWave - 1) / kWave;
     const int us = sc.us;
     for (;;) {
-        if (tid == 0) S.item = (int32_t)atomicAdd(&ex.ctr[2], 1ull);
+        if (tid == 0) S.item = (int32_t)atomicAdd(&ex.ctr[NX ? 8 : 2], 1ull);
         __syncthreads();
         const uint32_t item = (uint32_t)uni(S.item);
         __syncthreads();
@@ -258,14 +270,23 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
         const int slot = ex.pend_slot[i];
         const int pass = (int)(item - ex.pend_base[i]);
         const GBL int32_t *meta = sc.meta + (size_t)slot * 8;
-        const int g = uni(meta[0]), len = uni(meta[1]), T = uni(meta[2]), aligned = uni(meta[4]);
+        const int g = uni(meta[0]), len = uni(meta[1]), Tdd = uni(meta[2]), aligned = uni(meta[4]);
+        // a non-exact record (k_nx_dag): the tree below its last width-1 layer k0, rooted at
+        // the value k_nx_dag left in R; layers are counted from k0 (local layer k = DD layer
+        // k0 + k), and the pass also reports per cut maxState and per leaf the first cut <=
+        // optimalLB (nx_kernels.hip)
+        const int k0 = ex.pkind ? uni(ex.pkind[i]) : -1;
+        if ((k0 >= 0) != NX) continue;   // the other instantiation's entry
+        constexpr bool nx = NX;
+        const int kb = nx ? k0 : 0;
+        const int T = Tdd - kb;
         const GBL uint32_t *lay = sc.lay + (size_t)slot * sc.Tcap * 5;
-        const uint32_t lnoff = uni(lay[T - 1]), lnn = uni(lay[sc.Tcap + T - 1]);
+        const uint32_t lnoff = uni(lay[Tdd - 1]), lnn = uni(lay[sc.Tcap + Tdd - 1]);
         const size_t N = (size_t)slot * sc.Ncap;
         const int E = (T - 1) * us;
         for (int e = tid; e < E; e += kLeafWaves * kWave) {
             const int k = e / us + 1, r = e % us;
-            S.stab[e] = r == 0 ? -1 : slot_of(net, g, len, aligned, k, r);
+            S.stab[e] = r == 0 ? -1 : slot_of(net, g, len, aligned, kb + k, r);
         }
         // this wave's leaves: ancestry tables and alive mask
         const int j0 = pass * kLeafPass + w * kLeavesPerWave;
@@ -285,7 +306,7 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
                         const uint8_t f = sc.nflag[N + node];
                         S.lw[w].info[j][k] = (uint8_t)(((t >> kRankShift) & 63u) | ((f & kInAlive) ? 128u : 0u));
                         anc[k] = node;
-                        node = lay[k - 1] + (t & kParentMask);
+                        node = lay[kb + k - 1] + (t & kParentMask);
                     }
                 }
             }
@@ -320,12 +341,20 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
         uint32_t done = 0;
         int nb_done = 0;
         bool finished = false;   // every leaf of the pass <= optimalLB
+        // non-exact: pool order only (no screening columns, no lazy passes); the pass may stop
+        // early only when it is the record's only one (maxState needs every leaf's value at
+        // every cut before the pruning position)
+        const int nbs_r = nx ? 0 : nbs;
+        const int nblk_r = nx ? (ex.no + kWave - 1) / kWave : nblk;
+        const bool single_pass = lnn <= (uint32_t)kLeafPass;
         // lazy passes stop after ex.lazy blocks (the newest cuts); see ExactIO::lazy
-        const int nlim = (ex.lazy > 0 && nbs == 0) ? min(nblk, ex.lazy) : nblk;
+        const int nlim = (!nx && ex.lazy > 0 && nbs == 0) ? min(nblk, ex.lazy) : nblk_r;
+        // non-exact: per leaf the first cut (pool position) with value <= optimalLB
+        if (nx && lane() < kLeavesPerWave) S.lw[w].fle[lane()] = INT_MAX;
         for (int bb = 0; bb < nlim; bb++) {
             nb_done = bb + 1;
-            const bool scr = bb < nbs;
-            const int b = scr ? bb : bb - nbs;
+            const bool scr = bb < nbs_r;
+            const int b = scr ? bb : bb - nbs_r;
             const int ncut = scr ? ex.nsc : ex.no;
             const GBL double *cm = scr ? ex.coefS : ex.coefO;
             const size_t cs = scr ? (size_t)kExactScreen : (size_t)ex.ostride;
@@ -339,9 +368,11 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
             __syncthreads();
             const int s = b * kWave + lane();
             const bool vc = s < ncut;
-            if (cnt > 0 && (done & alive) != alive) {
+            double ms = -INFINITY;   // non-exact: max over this wave's alive leaves, this lane's cut
+            if (cnt > 0 && (nx || (done & alive) != alive)) {
                 const double root = vc ? (scr ? ex.RS[(size_t)i * kExactScreen + s] : ex.R[(size_t)i * ex.ostride + s]) : 0.0;
                 const uint32_t open = alive & ~done;
+                const uint32_t need = nx ? alive : open;
                 double par = root;
 #pragma unroll
                 for (int j = 0; j < kLeavesPerWave; j++) {
@@ -349,36 +380,59 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
                         const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)lp, j);
                         const int dj = (int)(x >> 8);
                         if (dj < T - 1 || j == 0) par = walk_down(S, w, j, dj, T, us, root);
-                        if ((open >> j) & 1u) {
+                        if ((need >> j) & 1u) {
                             const uint32_t row = x & 0x7Fu;
                             double v;
                             if (row == kRowDead) v = EDMIN;
                             else if (row == kRowNoAdd) v = par;
                             else v = par + S.C[row][lane()];
-                            if (vc) m[j] = rmin(m[j], v);
+                            if (vc && ((open >> j) & 1u)) m[j] = rmin(m[j], v);
+                            if (nx) {
+                                ms = (vc && v > ms) ? v : ms;
+                                if ((open >> j) & 1u) {
+                                    const uint64_t hit = __ballot(vc && v <= incumbent);
+                                    if (hit) {
+                                        if (lane() == 0) S.lw[w].fle[j] = b * kWave + (int)(__ffsll((unsigned long long)hit) - 1);
+                                        done |= 1u << j;
+                                    }
+                                }
+                            }
                         }
                     }
                 }
                 // every fourth block (and the last): leaves some lane already took to <= optimalLB
-                if ((bb & 3) == 3 || bb == nlim - 1) {
+                if (!nx && ((bb & 3) == 3 || bb == nlim - 1)) {
 #pragma unroll
                     for (int j = 0; j < kLeavesPerWave; j++)
                         if ((open >> j) & 1u)
                             if (__ballot(vc && m[j] <= incumbent)) done |= 1u << j;
                 }
             }
+            if (nx) S.vb[w][0][lane()] = ms;   // free until the next block's walks
             if (lane() == 0) S.flags[w] = ((done & alive) == alive) ? 1 : 0;
             __syncthreads();
             int all = 1;
 #pragma unroll
             for (int q = 0; q < kLeafWaves; q++) all &= S.flags[q];
+            if (nx && w == 0 && vc) {
+                double mx = -INFINITY;
+#pragma unroll
+                for (int q = 0; q < kLeafWaves; q++) mx = S.vb[q][0][lane()] > mx ? S.vb[q][0][lane()] : mx;
+                if (mx != -INFINITY) atomicMax(&ex.MS[(size_t)i * ex.ostride + s], nx_key(mx));
+            }
             __syncthreads();
-            if (all) {
+            if (all && (!nx || single_pass)) {
                 finished = true;
                 break;
             }
         }
-        const bool lazy = !finished && nlim < nblk;
+        if (nx) {
+            // the pass's pruning position: max over its alive leaves of their first cut <= optimalLB
+            const int fl = (lane() < kLeavesPerWave && ((alive >> lane()) & 1u)) ? S.lw[w].fle[lane()] : 0;
+            const int pm = lane_reduce<1>(fl, [](int a, int b) { return a > b ? a : b; });
+            if (lane() == 0 && cnt > 0) atomicMax(&ex.P[i], pm);
+        }
+        const bool lazy = !nx && !finished && nlim < nblk;
         if (tid == 0) atomicAdd(&ex.ctr[3], (unsigned long long)nb_done);   // diagnostics: cut blocks swept
         // terminal weights: min over the lanes
 #pragma unroll
@@ -398,6 +452,166 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
 
 size_t exact_leaf_lds_bytes() { return sizeof(LeafShared); }
 
+// ---- k_nx_dag: the DAG part of non-exact records (kNxPending) ------------------------------
+// One wave per work item (pending record, block of kNxCuts cuts), blocks outermost so that the
+// waves in flight read the same coefO columns.  Lanes = 4 node groups x 16 cuts: the wave
+// sweeps layers 1 .. k0 like dd_sweep, four nodes (or merged arcs) of a layer per step, from
+// the packed topology words of the slot (tmir, build_stream: parent:7 | rank:5 | alive |
+// in-arc alive; every layer below kg has <= 127 nodes), the previous and the current layer's
+// values in this wave's LDS ([2][128][16] doubles), the layer's per-rank coefficients in
+// registers (the next layer's load meanwhile).  A merged node folds its arcs per group, then
+// the four partial (value, priority) maxima combine -- the fold is order-free given the
+// priorities (DD.cpp:3952-3973).  Out: R = the value at k0 (the leaf passes' root), G = min
+// over the width-1 pruning layers (3 <= k < T - 2) of fl(xmin - state2) lowered by 1e-12
+// (|xmin| + |state2| + 1) (the reference tests fl(xmin + fl(maxState - state2)) <= thresh;
+// the two differ by a few ulp of those magnitudes), -inf when such a layer holds a non-finite
+// or DOUBLE_MIN/MAX value; MS cleared for the leaf passes' atomic max.
+constexpr int kNxGroups = kWave / kNxCuts;
+struct NxShared {
+    double V[2][128][kNxCuts];
+    int32_t item;
+};
+
+__device__ __forceinline__ double nx_pick(uint32_t r, const double (&cf)[kNxRanks]) {
+    return r == 1u ? cf[0] : (r == 2u ? cf[1] : (r == 3u ? cf[2] : cf[3]));
+}
+
+__device__ void nx_dag_item(const NetDev &net, const Scratch &sc, const ExactIO &ex, NxShared &X, int i, int b) {
+    const int slot = uni(ex.pend_slot[i]);
+    const GBL int32_t *meta = sc.meta + (size_t)slot * 8;
+    const int g = uni(meta[0]), len = uni(meta[1]), T = uni(meta[2]), aligned = uni(meta[4]);
+    const GBL int32_t *h = ex.nxh + (size_t)slot * 4;
+    const int k0 = uni(h[0]);
+    const uint32_t Nn = (uint32_t)uni(h[1]), q0 = (uint32_t)uni(h[2]);
+    const GBL uint32_t *lay = sc.lay + (size_t)slot * sc.Tcap * 5;
+    const GBL uint16_t *tm = sc.tmir + (size_t)slot * sc.tmir_cap;
+    const int q = lane() / kNxCuts, c = lane() % kNxCuts;
+    const int s = b * kNxCuts + c;
+    const bool vc = s < ex.no;
+    const int col = vc ? ex.no - 1 - s : 0;
+    const size_t os = (size_t)ex.ostride;
+    auto load_coef = [&](int k, double (&dst)[kNxRanks]) {
+#pragma unroll
+        for (int r = 0; r < kNxRanks; r++) {
+            const int sl = slot_of(net, g, len, aligned, k, r + 1);
+            dst[r] = (sl >= 0 && vc) ? ex.coefO[(size_t)sl * os + col] : 0.0;
+        }
+    };
+    double cf[kNxRanks], nf[kNxRanks];
+    load_coef(1, cf);
+    const double root = vc ? ex.R[(size_t)i * os + s] : 0.0;
+    if (q == 0) X.V[0][0][c] = root;
+    wave_lds_sync();
+    int cur = 0;
+    double gap = INFINITY, mag = 0.0;
+    bool unc = false;
+    auto summary = [&](double val, double xm) {
+        if (!(fabs(val) < 1e300) || !(fabs(xm) < 1e300)) unc = true;
+        else {
+            gap = fmin(gap, xm - val);
+            mag = fmax(mag, fabs(xm) + fabs(val));
+        }
+    };
+    for (int k = 1; k <= k0; k++) {
+        if (k < k0) load_coef(k + 1, nf);
+        const uint32_t noff = uni(lay[k]), n = uni(lay[sc.Tcap + k]), nal = uni(lay[2 * sc.Tcap + k]);
+        const uint32_t aoff = uni(lay[3 * sc.Tcap + k]), acnt = uni(lay[4 * sc.Tcap + k]);
+        const bool summ = nal == 1u && k >= 3 && k <= T - 3;
+        if (acnt == 0) {
+            // exact layer: words of nodes lane and lane + 64 (n <= 127), node base + q per step
+            const uint32_t w0 = lane() < (int)n ? (uint32_t)tm[noff + lane()] : 0u;
+            const uint32_t w1 = lane() + kWave < (int)n ? (uint32_t)tm[noff + kWave + lane()] : 0u;
+            for (uint32_t base = 0; base < n; base += kNxGroups) {
+                const uint32_t idx = base + (uint32_t)q;
+                const int src = (int)(idx & (kWave - 1));
+                const uint32_t wa = (uint32_t)__shfl((int)w0, src, kWave), wb = (uint32_t)__shfl((int)w1, src, kWave);
+                const uint32_t w = idx < (uint32_t)kWave ? wa : wb;
+                const bool ok = idx < n && (w & kMirAlive);
+                const uint32_t p = w & 127u, r = (w >> 7) & 31u;
+                const double px = X.V[cur][p][c];
+                const bool inal = (w & kMirIn) != 0;
+                const double x = !inal ? EDMIN : (r ? px + nx_pick(r, cf) : px);
+                if (ok) {
+                    X.V[cur ^ 1][idx][c] = x;
+                    if (summ) summary(x, !inal ? EDMAX : (r ? x : px + 0.0));
+                }
+            }
+        } else {
+            // merged node: its alive in-arcs, four per step, per-group (value, priority) fold
+            double bv = 0.0, xmin = EDMAX;
+            int bp = INT_MIN;
+            for (uint32_t a0 = 0; a0 < acnt; a0 += kWave) {
+                const uint32_t wl = a0 + lane() < acnt ? (uint32_t)tm[Nn + aoff + a0 + lane()] : 0u;
+                const uint32_t m = min((uint32_t)kWave, acnt - a0);
+                for (uint32_t base = 0; base < m; base += kNxGroups) {
+                    const uint32_t j = base + (uint32_t)q;
+                    const uint32_t w = (uint32_t)__shfl((int)wl, (int)(j & (kWave - 1)), kWave);
+                    if (j < m && (w & kMirAlive)) {
+                        const uint32_t p = w & 127u, r = (w >> 7) & 31u;
+                        const double px = X.V[cur][p][c];
+                        const double cand = r ? px + nx_pick(r, cf) : px;
+                        const int a = (int)(a0 + j);
+                        const int pr = r ? a : -a - 2;
+                        const bool take = (bp == INT_MIN) | ((cand > bv) | (!(bv > cand) & (pr > bp)));
+                        bv = take ? cand : bv;
+                        bp = take ? pr : bp;
+                        xmin = fmin(xmin, r ? cand : px + 0.0);
+                    }
+                }
+            }
+#pragma unroll
+            for (int sh = kNxCuts; sh < kWave; sh <<= 1) {
+                const double ov = __shfl_xor(bv, sh, kWave);
+                const int op = __shfl_xor(bp, sh, kWave);
+                const bool take = (bp == INT_MIN) | ((op != INT_MIN) & ((ov > bv) | (!(bv > ov) & (op > bp))));
+                bv = take ? ov : bv;
+                bp = take ? op : bp;
+                xmin = fmin(xmin, __shfl_xor(xmin, sh, kWave));
+            }
+            const double val = (bp == INT_MIN) ? EDMIN : smax(bv, EDMIN);
+            if (q == 0) X.V[cur ^ 1][0][c] = val;
+            if (summ && q == 0) summary(val, xmin);
+        }
+        wave_lds_sync();
+        cur ^= 1;
+        if (k < k0) {
+#pragma unroll
+            for (int r = 0; r < kNxRanks; r++) cf[r] = nf[r];
+        }
+    }
+    const double v0 = X.V[cur][q0][c];
+#pragma unroll
+    for (int sh = kNxCuts; sh < kWave; sh <<= 1) {
+        gap = fmin(gap, __shfl_xor(gap, sh, kWave));
+        mag = fmax(mag, __shfl_xor(mag, sh, kWave));
+        unc = unc | (__shfl_xor((int)unc, sh, kWave) != 0);
+    }
+    wave_lds_sync();   // every lane read the last layer before the next item overwrites it
+    if (q == 0 && vc) {
+        ex.R[(size_t)i * os + s] = v0;
+        ex.G[(size_t)i * os + s] = unc ? -INFINITY : gap - 1e-12 * (mag + 1.0);
+        ex.MS[(size_t)i * os + s] = 0ull;
+    }
+}
+
+__global__ void __launch_bounds__(kWave) k_nx_dag(NetDev net, Scratch sc, ExactIO ex) {
+    __shared__ NxShared S;
+    const int npend = (int)(ex.ctr[0] >> 32);
+    if (npend == 0) return;
+    const long long nblk = (ex.no + kNxCuts - 1) / kNxCuts;
+    const long long total = nblk * npend;
+    for (;;) {
+        if (lane() == 0) S.item = (int32_t)atomicAdd(&ex.ctr[6], 1ull);
+        __builtin_amdgcn_wave_barrier();
+        const long long item = (long long)uni(S.item);
+        __builtin_amdgcn_wave_barrier();
+        if (item >= total) break;
+        const int b = (int)(item / npend), i = (int)(item % npend);
+        if (uni(ex.pkind[i]) < 0) continue;
+        nx_dag_item(net, sc, ex, S, i, b);
+    }
+}
+
 hipError_t launch_exact_cols(const double *rows, const double *rhs, const int32_t *o_order, int no, int first,
                              int stride, int n_slots, int ostride, double *coefO, int reverse, hipStream_t st) {
     if (no <= first) return hipSuccess;
@@ -407,12 +621,20 @@ hipError_t launch_exact_cols(const double *rows, const double *rhs, const int32_
 }
 
 // the pending records' root folds and terminal weights; k_exact_fin (dd_kernels.hip) ends them
+// (with non-exact records: k_nx_dag between the root folds and the leaf passes, k_nx_fin after)
 hipError_t launch_exact(const NetDev &net, const Scratch &sc, const ExactIO &ex, double incumbent, int cus,
                         hipStream_t st) {
     hipLaunchKernelGGL(k_exact_root, dim3(4 * cus), dim3(kRootWaves * kWave), 0, st, net, sc, ex);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_exact_leaf, dim3(4 * cus), dim3(kLeafWaves * kWave), sizeof(LeafShared), st, net, sc, ex,
+    if (ex.nx && ex.pkind) {
+        hipLaunchKernelGGL(k_nx_dag, dim3(5 * cus), dim3(kWave), 0, st, net, sc, ex);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_exact_leaf<false>, dim3(4 * cus), dim3(kLeafWaves * kWave), sizeof(LeafShared), st, net, sc, ex,
+                       incumbent);
+    if ((e = hipGetLastError()) != hipSuccess || !ex.nx || !ex.pkind) return e;
+    hipLaunchKernelGGL(k_exact_leaf<true>, dim3(4 * cus), dim3(kLeafWaves * kWave), sizeof(LeafShared), st, net, sc, ex,
                        incumbent);
     return hipGetLastError();
 }

@@ -197,7 +197,8 @@ struct Blk {
 // LDS: chains, then a union -- phases 1-2: chosen and dec (int16 [m] each);
 // phases 3-5: key (alpha), pred, plist -- then the free-node list and flags.
 constexpr int kSubLdsParts = 12;
-__host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int nz, int nw, size_t *off, int kbytes = 8) {
+__host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int nz, int nw, size_t *off, int kbytes = 8,
+                                                 bool warm = false) {
     size_t o = 0;
     off[1] = o; o = a16(o + (size_t)nct_cap * 8);
     // b words: 8 bytes, 4 with 32-bit keys, none in the single-wave kernel's 8-byte records
@@ -206,8 +207,11 @@ __host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int 
     off[3] = o; o = a16(o + (size_t)(n + 2) * kbytes);   // key | chosen
     off[4] = o; o = a16(o + (size_t)(n + 2) * 4);   // pred
     off[8] = o; o = a16(o + (size_t)(n + 2) * 2);   // plist
-    off[0] = a16(u0 + (size_t)m * 2);               // dec, after chosen; then the warm start's
-    const size_t dsz = (size_t)m * 2 > (size_t)(n + 2) * 4 ? (size_t)m * 2 : (size_t)(n + 2) * 4;   // node imbalances
+    off[0] = a16(u0 + (size_t)m * 2);               // dec, after chosen
+    // warm starts: dec's space then holds the node imbalances, which live through the
+    // repair's Bellman-Fords -- so past key / pred / plist, not over them
+    if (warm && off[0] < o) off[0] = o;
+    const size_t dsz = warm && (size_t)m * 2 < (size_t)(n + 2) * 4 ? (size_t)(n + 2) * 4 : (size_t)m * 2;
     if (o < a16(off[0] + dsz)) o = a16(off[0] + dsz);
     off[5] = o;
     off[6] = o; o = a16(o + (size_t)nz * 4);
@@ -737,25 +741,6 @@ __device__ __forceinline__ void invalidate_subtrees(const SubNet &N, const WS &W
 }
 
 // ---------------------------------------------------------------------------------------
-// Warm start.  The chains of a new path start from an earlier optimal state of the same
-// scenario (flow per arc, potentials alpha): a chain keeps the smallest earlier flow of its
-// arcs, then its reduced reward E = R - alpha(h) + alpha(t) under the old potentials fixes it
-// -- E > 0: x = U, E < 0: x = 0, E = 0: kept within [0, U] -- so every residual arc has a
-// non-negative reduced cost (no negative cycle: the pseudoflow is optimal for its imbalances).
-// Chains that did not change keep their flow, so only the nodes around the changed V-bar
-// matchings are out of balance.  The repair is successive shortest paths from the excess to
-// the deficit nodes (potential mode: every free node is tied to Z both ways at cost 0, so
-// free supply / demand absorbs anything):
-//   stage 0: multi-source Bellman-Ford from every excess node (key 0), augment towards the
-//            closest deficit node or Z (absorbed by a free node);
-//   stage 1: from Z (free supply) to the remaining deficit nodes.
-// Each augmentation is a shortest path of the extended network (super source -> sources at
-// cost 0, targets -> super sink at cost 0), so the residual stays free of negative cycles and
-// the repaired flow is optimal.  Between augmentations the Bellman-Ford resumes from its
-// labels as the cold SSP does: the heads of used-up arcs and a source whose excess is gone
-// restart at infinity with their predecessor subtrees (invalidate_subtrees).  Returns false
-// (the caller falls back to the cold SSP) if a target is unreachable or the augmentation
-// bound is hit; neither happens with lower bounds 0.
 __device__ __forceinline__ bool is_cons(const SubNet &N, int v) { return N.inner[v] && !N.vbar[v]; }
 
 // Warm start.  The chains of a new path start from an earlier optimal state of the same
@@ -776,11 +761,12 @@ __device__ __forceinline__ bool is_cons(const SubNet &N, int v) { return N.inner
 // labels as the cold SSP does: the heads of used-up arcs and a source whose excess is gone
 // restart at infinity with their predecessor subtrees (invalidate_subtrees).  Returns false
 // (the caller falls back to the cold SSP) if a target is unreachable or the augmentation
-// bound is hit; neither happens with lower bounds 0.  Only the WARM instantiation of
+// bound is hit (why: 1 Bellman-Ford, 2 unreachable, 3 path, 4 bound); neither happens with
+// lower bounds 0.  Only the WARM instantiation of
 // k_sub_scenario carries it (launches with warm starts); the cold one is unchanged.
 template <int RG, typename WT, int NW, class WS>
 __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nct, int nz, int64_t M,
-                                                      LDS int32_t *imb, int64_t max_aug, int &augs) {
+                                                      LDS int32_t *imb, int64_t max_aug, int &augs, int &why) {
     using B = Blk<NW>;
     using KT = typename WS::Key;
     constexpr KT kKInf = WS::kKInf;
@@ -803,7 +789,7 @@ __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nc
                 B::sync();
                 fresh = false;
             }
-            if (!bellman_ford<RG, WT, NW>(N, W, nct, nz, kPotPlain, M, true, true)) return false;
+            if (!bellman_ford<RG, WT, NW>(N, W, nct, nz, kPotPlain, M, true, true)) { why = 1; return false; }
             // the closest target (key, then node id): deficit nodes, and Z in stage 0
             int64_t best = INT64_MAX;
             for (int v = tid; v <= n; v += T) {
@@ -815,7 +801,27 @@ __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nc
                 }
             }
             best = B::all(best, [](int64_t x, int64_t y) { return x < y ? x : y; }, W.red);
-            if (best == INT64_MAX) return false;
+#ifdef SGUFP_WARM_DEBUG
+            if (best == INT64_MAX) {
+                int fin = 0, nsrc = 0, ndef = 0, fsrc = 0, ninc = 0;
+                for (int v = tid; v < n; v += T) {
+                    fin += W.key[v] < kKInf;
+                    if (is_cons(N, v) && imb[v] > 0) { nsrc++; fsrc += W.key[v] < kKInf; }
+                    if (is_cons(N, v) && imb[v] < 0) ndef++;
+                    if (!is_cons(N, v) && imb[v] != 0) ninc++;
+                }
+                fin = (int)B::all((int64_t)fin, [](int64_t x, int64_t y) { return x + y; }, W.red);
+                nsrc = (int)B::all((int64_t)nsrc, [](int64_t x, int64_t y) { return x + y; }, W.red);
+                fsrc = (int)B::all((int64_t)fsrc, [](int64_t x, int64_t y) { return x + y; }, W.red);
+                ndef = (int)B::all((int64_t)ndef, [](int64_t x, int64_t y) { return x + y; }, W.red);
+                ninc = (int)B::all((int64_t)ninc, [](int64_t x, int64_t y) { return x + y; }, W.red);
+                if (tid == 0 && blockIdx.x < 6)
+                    printf("WARMDBG blk=%d stage=%d augs=%d n=%d nct=%d nz=%d finite=%d src=%d src_finite=%d def=%d "
+                           "noncons_imb=%d keyZ=%d\n", (int)blockIdx.x, stage, augs, n, nct, nz, fin, nsrc, fsrc, ndef, ninc,
+                           (int)W.key[n]);
+            }
+#endif
+            if (best == INT64_MAX) { why = 2; return false; }
             const int tgt = (int)(best & 4095);
             if (tid == 0) {
                 int v = tgt, len = 0;
@@ -843,7 +849,7 @@ __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nc
             delta = B::all(delta, [](int64_t p, int64_t q) { return p < q ? p : q; }, W.red);
             if (stage == 0 && src_ok) delta = (int64_t)imb[src] < delta ? (int64_t)imb[src] : delta;
             if (tgt < n) delta = (int64_t)(-imb[tgt]) < delta ? (int64_t)(-imb[tgt]) : delta;
-            if (!src_ok || plen >= n + 2 || delta <= 0 || delta >= kInf) return false;
+            if (!src_ok || plen >= n + 2 || delta <= 0 || delta >= kInf) { why = 3; return false; }
             B::sync();   // every lane read the imbalances before they change
             for (int i = tid; i < plen; i += T) {
                 const int code = W.plist[i];
@@ -864,7 +870,15 @@ __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nc
             }
             B::sync();
             invalidate_subtrees<NW>(N, W);
-            if (++augs > max_aug) return false;
+            // a source reached from another source (cheaper than its own key 0) hangs in that
+            // one's predecessor tree: when that source runs dry the invalidation drops it too,
+            // so every remaining source (and Z) restarts from 0 at most
+            for (int v = tid; v <= n; v += T) {
+                const bool src = stage == 0 ? (v < n && is_cons(N, v) && imb[v] > 0) : v == n;
+                if (src && W.key[v] > (KT)0) W.key[v] = (KT)0;
+            }
+            B::sync();
+            if (++augs > max_aug) { why = 4; return false; }
         }
     }
     return true;
@@ -1087,7 +1101,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
     const int p = blockIdx.x / S, s = blockIdx.x - p * S;
     if (p >= io.n_paths) return;
     size_t off[kSubLdsParts];
-    sub_lds_layout(N.n, N.m, io.nct_cap, N.nz, NW, off, (int)sizeof(KT));
+    sub_lds_layout(N.n, N.m, io.nct_cap, N.nz, NW, off, (int)sizeof(KT), WARM && sizeof(KT) == 4);
     WS W;
     W.dec = (LDS int16_t *)(smem + off[0]);
     W.cta = (LDS uint64_t *)(smem + off[1]);
@@ -1296,7 +1310,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
 #define SUB_T1(acc)
 #endif
         int iters = 0;
-        int warm_augs = 0;
+        int warm_augs = 0, why = 0;
         bool repaired = false, fell_back = false;
 #ifdef SGUFP_SUB_VERIFY
         int64_t verify_primal = INT64_MIN;
@@ -1306,7 +1320,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
             for (int v = tid; v < n; v += T)
                 if (is_cons(N, v)) imb_tot += imb[v] > 0 ? imb[v] : -imb[v];
             imb_tot = B::all(imb_tot, [](int64_t x, int64_t y) { return x + y; }, W.red);
-            repaired = warm_repair<RG, WT, NW>(N, W, nct, nz, M, imb, imb_tot + 2 * (int64_t)nct + 8, warm_augs);
+            repaired = warm_repair<RG, WT, NW>(N, W, nct, nz, M, imb, imb_tot + 2 * (int64_t)nct + 8, warm_augs, why);
 #ifdef SGUFP_SUB_VERIFY
             if (repaired) {   // debug build: the cold SSP below must reach the same objective
                 int64_t pw = 0;
@@ -1415,7 +1429,8 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         }
 #endif
         if (io.wstat && tid == 0) {
-            io.wstat[2 * b] = repaired ? warm_augs : (fell_back ? -iters - 1 : iters);
+            // fell back: -(why * 100000 + cold augmentations) - 1
+            io.wstat[2 * b] = repaired ? warm_augs : (fell_back ? -(why * 100000 + iters) - 1 : iters);
             io.wstat[2 * b + 1] = W.misc[5];
         }
         if (status == kSubOptimal) {
@@ -1612,16 +1627,17 @@ hipError_t launch_warm_pick(const SubIO &io, const WarmRing &wr, int ptr, hipStr
 }
 
 // ---------------------------------------------------------------------------------------
-size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw, int kbytes) {
+size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw, int kbytes, bool warm) {
     size_t off[kSubLdsParts];
-    return sub_lds_layout(n, m, nct_cap, nz, nw, off, kbytes);
+    return sub_lds_layout(n, m, nct_cap, nz, nw, off, kbytes, warm);
 }
 
 namespace {
 template <typename KT, bool WARM>
 hipError_t launch_scenarios(const SubNet &N, const SubIO &io, hipStream_t st) {
     constexpr int kb = (int)sizeof(KT);
-    size_t lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, 1, kb);
+    constexpr bool kw = WARM && kb == 4;   // the warm layout (k_sub_scenario's)
+    size_t lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, 1, kb, kw);
 #ifdef SGUFP_SUB_LDS_MIN
     if (lds < SGUFP_SUB_LDS_MIN) lds = SGUFP_SUB_LDS_MIN;   // occupancy experiments
 #endif
@@ -1629,11 +1645,11 @@ hipError_t launch_scenarios(const SubNet &N, const SubIO &io, hipStream_t st) {
     // LDS allows at most two scenarios per CU (in its own layout: the single-wave 8-byte
     // records would bring C5 under the bar and back to one wave per scenario, 4x slower) and
     // the big-M costs fit 32 bits (host bound)
-    const bool large = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, kLargeWaves, kb) > 64 * 1024 &&
+    const bool large = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, kLargeWaves, kb, false) > 64 * 1024 &&
                        io.nct_cap > kRegGroupsSmall * kWave && N.cost_bound < ((int64_t)1 << 30);
     const char *ev = getenv("SGUFP_SUB_WAVES");
     if (large && !(ev && atoi(ev) == 1)) {
-        lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, kLargeWaves, kb);
+        lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, kLargeWaves, kb, kw);
         if (io.nct_cap <= kRegGroupsLarge * kLargeWaves * kWave && !N.preds_lds)
             hipLaunchKernelGGL((k_sub_scenario<kRegGroupsLarge, int32_t, kLargeWaves, KT, true, WARM>),
                                dim3((unsigned)io.n_paths * N.S), dim3(kWave * kLargeWaves), lds, st, N, io);
