@@ -385,7 +385,8 @@ def write_pool_bin(path: str, eng: E.Engine) -> int:
 
 
 def check_large_pool(cfg: str, seed: int, width: int, min_opt_cuts: int, batch: int = 1024, per_kind: int = 8,
-                     round_seconds: float = 5.0, max_seconds: float = 240.0, device: int = 0, threads: int = 0):
+                     round_seconds: float = 5.0, max_seconds: float = 240.0, device: int = 0, threads: int = 0,
+                     need_rounds: int = 12):
     """Parity at the pool sizes the timed B&B runs against: the seeded search of ``cfg`` (lower
     bounds 0; incumbent from the width-``width`` restricted-DD heuristic) runs untraced, with
     uncapped refinement loops, until its optimality list holds ``min_opt_cuts`` cuts.  The next
@@ -426,16 +427,27 @@ def check_large_pool(cfg: str, seed: int, width: int, min_opt_cuts: int, batch: 
     rep["pool_optimality"] = eng.cuts_count(0)
     rep["incumbent"] = z
     fail: List[str] = []
-    snap = snapshot_top(eng, batch)
-    recs = E.batch_to_records(snap)
-    got_all = eng.relax(recs, z)
-    kinds = {"exact": [], "survivor": [], "pruned": []}
-    for k, g in enumerate(got_all):
-        if snap.ub[k] <= z:
-            continue                                     # skipped unprocessed by the round
-        kind = "exact" if g.status == E.NEEDS_SUBPROBLEM else ("survivor" if g.status == 0 else "pruned")
-        if len(kinds[kind]) < per_kind:
-            kinds[kind].append(k)
+    # the first batch (within a few more rounds) that holds both exact leaves and non-exact
+    # survivors, so that the sample covers the cut-parallel exact phase and the non-exact one
+    for attempt in range(need_rounds + 1):
+        snap = snapshot_top(eng, batch)
+        recs = E.batch_to_records(snap)
+        got_all = eng.relax(recs, z)
+        kinds = {"exact": [], "survivor": [], "pruned": []}
+        for k, g in enumerate(got_all):
+            if snap.ub[k] <= z:
+                continue                                     # skipped unprocessed by the round
+            kind = "exact" if g.status == E.NEEDS_SUBPROBLEM else ("survivor" if g.status == 0 else "pruned")
+            if len(kinds[kind]) < per_kind:
+                kinds[kind].append(k)
+        if (kinds["exact"] and kinds["survivor"]) or attempt == need_rounds or not eng.frontier_size():
+            break
+        eng.bnb_set_limits(0, round_seconds)
+        z, st = eng.bnb_step(z, batch)
+        rep["rounds"] += 1
+    rep["pool_feasibility"] = eng.cuts_count(1)
+    rep["pool_optimality"] = eng.cuts_count(0)
+    rep["incumbent"] = z
     idx = sorted(i for v in kinds.values() for i in v)
     rep["sampled"] = {k: len(v) for k, v in kinds.items()}
     rep["batch"] = len(recs)

@@ -121,6 +121,7 @@ bool sgufp_ctx::init() {
     if (const char *e = getenv("SGUFP_EXACT_LAZY")) exact_lazy = std::max(0, atoi(e));
     if (const char *e = getenv("SGUFP_NX")) nx_on = atoi(e) != 0;
     if (const char *e = getenv("SGUFP_NX_MIN")) nx_min = std::max(1, atoi(e));
+    if (const char *e = getenv("SGUFP_NX_SKIP")) nx_skip = std::max(0, atoi(e));
     int64_t acap = std::max<int64_t>(1, (int64_t)std::max(0, L - 4) * (kRelaxedMaxWidth - 1) * maxU);
     if (ncap > (int64_t)kParentMask || acap > (int64_t)0x7FFFFFFF) { err = "DD capacity beyond 22-bit indices"; return false; }
     sc.Ncap = (int)ncap;
@@ -327,7 +328,7 @@ bool sgufp_ctx::exact_prepare() {
         ocap = cap;
     }
     if (!d_pslot && (!alloc(d_pslot, (size_t)max_batch, "exact pending") || !alloc(d_pbase, (size_t)max_batch, "exact pending") ||
-                     !alloc(d_ectr, 10, "exact pending") || !alloc(d_pidx, (size_t)max_batch, "exact pending")))
+                     !alloc(d_ectr, 14, "exact pending") || !alloc(d_pidx, (size_t)max_batch, "exact pending")))
         return false;
     if (!nx_prepare(no)) return false;
     if (o_built < no) {
@@ -348,7 +349,7 @@ bool sgufp_ctx::exact_prepare() {
     }
     ex.coefS = d_coefS;
     ex.RS = d_RS;
-    if (!hip_ok(hipMemsetAsync(d_ectr, 0, 10 * sizeof(unsigned long long), stream), "memset") ||
+    if (!hip_ok(hipMemsetAsync(d_ectr, 0, 14 * sizeof(unsigned long long), stream), "memset") ||
         !hip_ok(hipMemsetAsync(d_pidx, 0xFF, (size_t)max_batch * sizeof(int32_t), stream), "memset"))
         return false;
     ex.lazy = ex.nsc == 0 ? exact_lazy : 0;
@@ -372,10 +373,14 @@ bool sgufp_ctx::nx_prepare(int no) {
     ex.nx = 0;
     ex.redo = 0;
     ex.nx_min = nx_min;
+    ex.nx_skip = nx_skip;
     ex.pkind = nullptr;
     if (!nx_on || no < nx_min || cb <= 1) return true;
     const size_t B = (size_t)max_batch;
-    if (!d_nxh && (!alloc(d_nxh, B * 4, "nx header") || !alloc(d_pkind, B, "nx pending") || !alloc(d_P, B, "nx pending")))
+    // leaf passes: at most ceil(leaves / kLeafPass) per record
+    const size_t npass = B * ((size_t)sc.Ncap / kLeafPass + 1);
+    if (!d_nxh && (!alloc(d_nxh, B * 4, "nx header") || !alloc(d_pkind, B, "nx pending") || !alloc(d_P, B, "nx pending") ||
+                   !alloc(d_pstop, npass, "nx pending") || !alloc(d_nxlist, B, "nx pending")))
         return false;
     if (nx_cap < ocap) {
         size_t fr = 0, tot = 0;
@@ -393,6 +398,9 @@ bool sgufp_ctx::nx_prepare(int no) {
     ex.G = d_G;
     ex.MS = d_MS;
     ex.nxh = d_nxh;
+    ex.pstop = d_pstop;
+    ex.nxlist = d_nxlist;
+    ex.nx_ms = 0;
     return true;
 }
 
@@ -420,16 +428,16 @@ bool sgufp_ctx::emit_current(const BatchIn &in, const Pool &p) {
     const char *es = std::getenv("SGUFP_EXACT_STATS");   // diagnostics (tests read them from stderr)
     const bool estats = es && es[0] == '1';
     if (estats && ex.enabled) {
-        unsigned long long c[10];
-        if (download(c, d_ectr, 10) && sync())
+        unsigned long long c[14];
+        if (download(c, d_ectr, 14) && sync())
             std::fprintf(stderr,
                          "[exact] pending %llu passes %llu blocks swept %llu of %llu (no %d, screen %d, lazy %d: "
                          "%llu resolves, %llu blocks); non-exact: dag items %llu, fallbacks %llu, kept back "
-                         "(ranks %llu, tail %llu, segment %llu, program %llu, other %llu)\n",
+                         "(ranks %llu, tail %llu, segment %llu, program %llu, other %llu), handed off %llu\n",
                          c[0] >> 32, c[0] & 0xFFFFFFFFull, c[3],
                          (c[0] & 0xFFFFFFFFull) * (unsigned long long)((ex.no + 63) / 64 + (ex.nsc + 63) / 64), ex.no,
                          ex.nsc, ex.lazy, c[4], c[5], c[6], c[7], c[9] & 1023, (c[9] >> 10) & 1023, (c[9] >> 20) & 1023,
-                         (c[9] >> 30) & 1023, (c[9] >> 40) & 1023);
+                         (c[9] >> 30) & 1023, (c[9] >> 40) & 1023, c[12]);
     }
     total_children = (int64_t)tot[0];
     total_csol = (int64_t)tot[1];

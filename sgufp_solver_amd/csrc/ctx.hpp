@@ -246,9 +246,10 @@ struct sgufp_ctx {
     int32_t *d_pidx = nullptr;
     int exact_lazy = 0;                       // ExactIO::lazy (SGUFP_EXACT_LAZY)
     // the same for non-exact DDs under large pools (nx_kernels: SGUFP_NX=0 off, SGUFP_NX_MIN)
-    bool nx_on = false;
+    bool nx_on = true;
     int nx_min = 2048;
-    int32_t *d_pkind = nullptr, *d_P = nullptr, *d_nxh = nullptr;
+    int nx_skip = 256;
+    int32_t *d_pkind = nullptr, *d_P = nullptr, *d_nxh = nullptr, *d_pstop = nullptr, *d_nxlist = nullptr;
     double *d_G = nullptr;
     unsigned long long *d_MS = nullptr;
     int nx_cap = 0;                           // columns of G / MS allocated

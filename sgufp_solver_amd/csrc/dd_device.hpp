@@ -200,6 +200,7 @@ constexpr int32_t kExactPending = 5;
 // wider ones take k_relax's own path.
 constexpr int kExactMaxT = SGUFP_EXACT_MAXT;           // DD layers (root included) the hand-off takes
 constexpr int kExactMaxEntries = SGUFP_EXACT_ENTRIES;  // (T - 1) * ustride coefficient rows staged per cut block
+constexpr int kExactMaxEntriesWide = 64;               // ... by the wide leaf-kernel instantiation
 constexpr int kLeafWaves = 8;                          // waves per leaf-kernel workgroup
 constexpr int kLeavesPerWave = SGUFP_LEAVES_PER_WAVE;
 constexpr int kLeafPass = kLeafWaves * kLeavesPerWave;
@@ -213,9 +214,10 @@ struct ExactIO {
     double SGUFP_GBL *R;                  // [max_batch][ostride]: root folds, pending index x newest-first position
     int32_t SGUFP_GBL *pend_slot;         // [max_batch] batch slot of pending record i
     uint32_t SGUFP_GBL *pend_base;        // [max_batch] first leaf pass of pending record i
-    unsigned long long SGUFP_GBL *ctr;    // [10]: (pending << 32 | leaf passes), root work, leaf work,
+    unsigned long long SGUFP_GBL *ctr;    // [14]: (pending << 32 | leaf passes), root work, leaf work,
                                           // blocks swept, lazy resolves, blocks they swept, non-exact:
-                                          // DAG work, fallbacks, leaf work
+                                          // DAG work, fallbacks, leaf work, kept back; wide leaf work,
+                                          // maxState completion work, non-exact entries
     // Lazy terminal weights: a leaf pass sweeps at most `lazy` cut blocks (the newest 64 x lazy
     // O cuts); when that leaves some leaf above optimalLB the pass's leaves keep the partial
     // minimum (an upper bound of the terminal weight) flagged kLazy, and the argmax scans
@@ -233,13 +235,19 @@ struct ExactIO {
     // Cut-parallel optimality phase of NON-exact DDs (nx_kernels.hip, see kNxPending): pending
     // entries of both kinds share the index space, root folds and leaf passes above.
     int nx;                               // 1: k_relax hands such records off
-    int nx_min;                           // ... when the pool holds at least this many O cuts
+    int nx_min;                           // ... when the pool holds at least this many O cuts,
+    int nx_skip;                          // ... after this many of them in order
+
     int redo;                             // k_relax re-run: only the kNxFallback slots, no hand-off
+    int nx_ms;                            // the leaf kernel's second non-exact launch (maxState completion)
+    int32_t SGUFP_GBL *pstop;             // [leaf passes] the last cut block a non-exact pass swept
+    int32_t SGUFP_GBL *nxlist;            // [max_batch] pending indices of the non-exact entries (ctr[12] of them)
     int32_t SGUFP_GBL *pkind;             // [max_batch] per pending entry: -1 exact, else the DAG's last width-1 layer k0
     int32_t SGUFP_GBL *P;                 // [max_batch] first pruning position (max over leaves of the first cut <= optimalLB)
     double SGUFP_GBL *G;                  // [max_batch][ostride] width-1 pruning gap per cut (k_nx_dag), lowered by its error bound
     unsigned long long SGUFP_GBL *MS;     // [max_batch][ostride] maxState per cut (order-preserving key, atomic max)
-    int32_t SGUFP_GBL *nxh;               // [nslots][4] per handed-off slot: k0, packed node words, k0's node
+    int32_t SGUFP_GBL *nxh;               // [nslots][4] per handed-off slot: k0, packed node words, k0's node,
+                                          // first pool position of the phase
 };
 constexpr int kExactScreen = 256;
 

@@ -1840,7 +1840,7 @@ __device__ __forceinline__ bool nx_refuse(const ExactIO &ex, int why) {
     return false;
 }
 
-__device__ bool nx_compile(const DD &d, const Scratch &sc, const ExactIO &ex, int slot, int &k0_out) {
+__device__ bool nx_compile(const DD &d, const Scratch &sc, const ExactIO &ex, int slot, int &k0_out, int first) {
     const int T = d.T;
     if (T < 3 || d.us > kNxRanks + 1 || !d.stream) return nx_refuse(ex, 0);
     int k0 = 0;
@@ -1867,6 +1867,7 @@ __device__ bool nx_compile(const DD &d, const Scratch &sc, const ExactIO &ex, in
         h[0] = k0;
         h[1] = (int32_t)d.Nn;
         h[2] = (int32_t)q;
+        h[3] = first;   // the first pool position (O list, newest first) the phase applies
     }
     k0_out = k0;
     return true;
@@ -2217,9 +2218,11 @@ __device__ __forceinline__ void cut_loop_batched(const NetDev &net, DD &d, const
             if (pruned) { st.status = kPrunedOptimality; return; }
         }
         if (!feas && efast) { st.status = kExactPending; return; }
-        // a non-exact DD under a large pool: the cut-parallel phase takes it from here (once)
-        if (!feas && nx && s == pool.nf) {
-            if (nx_compile(d, sc, *nx, slot, *nx_k0)) { st.status = kNxPending; return; }
+        // a non-exact DD under a large pool that survived the first nx_skip optimality cuts in
+        // order (most records that a cut prunes go there, cheaply): the cut-parallel phase takes
+        // the rest of the pool from here (once)
+        if (!feas && nx && s >= pool.nf + nx->nx_skip) {
+            if (nx_compile(d, sc, *nx, slot, *nx_k0, s - pool.nf)) { st.status = kNxPending; return; }
             nx = nullptr;
         }
         const int nb = min(CB, (feas ? pool.nf : total) - s);
@@ -2400,7 +2403,7 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
     }
     st.stamp(0);
     // exact DDs whose optimality phase the cut-parallel kernels can take (exact_kernels.hip)
-    efast = ex.enabled && d.exact && pool.no > 0 && d.T <= kExactMaxT && (d.T - 1) * sc.us <= kExactMaxEntries;
+    efast = ex.enabled && d.exact && pool.no > 0 && d.T <= kExactMaxT && (d.T - 1) * sc.us <= kExactMaxEntriesWide;
     if (CB > 1 && d.aligned) {
         LdsCarve cv = lds_carve(sc.Tcap, sc.Lcap, CB, sc.us);
         d.tmir = sc.tmir + (size_t)slot * sc.tmir_cap;
@@ -2454,6 +2457,7 @@ __global__ void __launch_bounds__(kWave, 2) k_relax(NetDev net, Scratch sc, Batc
             if (ex.pkind) {
                 ex.pkind[i] = st.status == kNxPending ? nx_k0 : -1;
                 ex.P[i] = 0;
+                if (st.status == kNxPending) ex.nxlist[atomicAdd(&ex.ctr[12], 1ull)] = i;
             }
         }
     }
@@ -2922,11 +2926,12 @@ __global__ void __launch_bounds__(kWave) k_nx_fin(NetDev net, Scratch sc, BatchI
     const int slot = ex.pend_slot[i];
     if (out.status[slot] != kNxPending) return;
     const int p = ex.P[i];
+    const int first = ex.nxh[(size_t)slot * 4 + 3];   // k_relax applied positions [0, first) in order
     const int lim = p < pool.no ? p : pool.no;
     const double thresh = incumbent - 0.01;
     const size_t base = (size_t)i * ex.ostride;
     bool fire = false;
-    for (int c0 = 0; c0 < lim && !fire; c0 += kWave) {
+    for (int c0 = first; c0 < lim && !fire; c0 += kWave) {
         const int c = c0 + lane();
         bool f = false;
         if (c < lim) {
@@ -2949,7 +2954,7 @@ __global__ void __launch_bounds__(kWave) k_nx_fin(NetDev net, Scratch sc, BatchI
             out.status[slot] = kPrunedOptimality;
             out.lb[slot] = DMIN;
             out.ub[slot] = DMIN;
-            out.sweeps[slot] += (uint32_t)(p + 1);
+            out.sweeps[slot] += (uint32_t)(p + 1 - first);
             meta[5] = pool.o_order[p];
             meta[6] = kPrunedOptimality;
             sc.ubv[slot] = DMIN;
@@ -2998,7 +3003,7 @@ __global__ void __launch_bounds__(kWave) k_nx_fin(NetDev net, Scratch sc, BatchI
         out.ub[slot] = ub;
         out.nchild[slot] = nchild;
         out.sol_need[slot] = nchild * (uint32_t)(d.len + cut_layer);
-        out.sweeps[slot] += (uint32_t)pool.no;
+        out.sweeps[slot] += (uint32_t)(pool.no - first);
     }
     store_meta_layers(d, sc, slot, last_cut, status, cut_layer, ub);
 }

@@ -181,9 +181,10 @@ struct LeafWave {
     int32_t fle[kLeavesPerWave];   // non-exact entries: first cut <= optimalLB per leaf
 };
 
-struct LeafShared {
-    double C[kExactMaxEntries][kWave];   // staged coefficients of a 64-cut block, row = (k-1)*us + r
-    int32_t stab[kExactMaxEntries];      // their slots (-1: no coefficient)
+template <int ROWS>
+struct LeafSharedT {
+    double C[ROWS][kWave];               // staged coefficients of a 64-cut block, row = (k-1)*us + r
+    int32_t stab[ROWS];                  // their slots (-1: no coefficient)
     LeafWave lw[kLeafWaves];
     double vb[kLeafWaves][kExactMaxT - 1][kWave];   // ancestor values of the current leaf (layers 0 .. T - 2), per wave
     int32_t item, flags[kLeafWaves];
@@ -201,6 +202,7 @@ __device__ __forceinline__ double rmin(double w, double v) { return (v < w) ? v 
 
 // ancestors of leaf j (wave-local) from layer dj down to the leaf's parent, values in vb;
 // returns the parent value
+template <class LeafShared>
 __device__ __forceinline__ double walk_down(LeafShared &S, int w, int j, int dj, int T, int us, double root) {
     double prev = (dj <= 1) ? root : S.vb[w][dj - 1][lane()];
     for (int k = dj; k < T - 1; k++) {
@@ -216,11 +218,13 @@ __device__ __forceinline__ double walk_down(LeafShared &S, int w, int j, int dj,
 // the first cut in pool order whose value at the leaf equals the leaf's minimum zero: its
 // bits (the sign std::min's sequential fold keeps; the screening columns repeat pool cuts,
 // so they add no value of their own).  Coefficients straight from coefO.
-__device__ double first_zero(const NetDev &net, const ExactIO &ex, LeafShared &S, int w, int j, int T, int us, int i) {
+template <class LeafShared>
+__device__ double first_zero(const NetDev &net, const ExactIO &ex, LeafShared &S, int w, int j, int T, int us, int i,
+                             int s0 = 0) {
     const int nblk = (ex.no + kWave - 1) / kWave;
-    for (int b = 0; b < nblk; b++) {
+    for (int b = s0 / kWave; b < nblk; b++) {
         const int s = b * kWave + lane();
-        const bool vc = s < ex.no;
+        const bool vc = s < ex.no && s >= s0;
         const int oidx = vc ? ex.no - 1 - s : 0;
         double v = vc ? ex.R[(size_t)i * ex.ostride + s] : 1.0;
         for (int k = 1; k < T; k++) {
@@ -239,12 +243,18 @@ __device__ double first_zero(const NetDev &net, const ExactIO &ex, LeafShared &S
 #ifndef SGUFP_LEAF_MIN_WAVES
 #define SGUFP_LEAF_MIN_WAVES 6   // three 8-wave workgroups per CU (VGPRs <= 85)
 #endif
-// NX: the instantiation for the non-exact entries (k_nx_dag's roots), which pulls its items
-// from its own counter and skips the exact ones (and the other way round)
-template <bool NX>
+// Instantiations: NX = the non-exact entries (k_nx_dag's roots); ROWS = the staged rows, the
+// narrow one (kExactMaxEntries, three workgroups per CU) for tails of (T - 1) x ustride <= 40
+// rows, the wide one (kExactMaxEntriesWide, two per CU) for deeper or wider exact trees (C5's
+// 6-rank universes: 7 x 6 = 42 rows).  Each pulls its items from its own counter and skips the
+// entries of the others.
+template <bool NX, int ROWS>
 __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_exact_leaf(NetDev net, Scratch sc, ExactIO ex, double incumbent) {
+    using LeafShared = LeafSharedT<ROWS>;
+    constexpr bool kWide = ROWS > kExactMaxEntries;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LeafShared &S = *(LeafShared *)smem_raw;
+    if (NX && ex.ctr[12] == 0) return;   // no non-exact entry in this batch
     const int w = wid();
     const int tid = (int)threadIdx.x;
     const unsigned long long packed = ex.ctr[0];
@@ -254,7 +264,7 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
     const int nblk = nbs + (ex.no + kWave - 1) / kWave;
     const int us = sc.us;
     for (;;) {
-        if (tid == 0) S.item = (int32_t)atomicAdd(&ex.ctr[NX ? 8 : 2], 1ull);
+        if (tid == 0) S.item = (int32_t)atomicAdd(&ex.ctr[NX ? (ex.nx_ms ? 11 : 8) : (kWide ? 10 : 2)], 1ull);
         __syncthreads();
         const uint32_t item = (uint32_t)uni(S.item);
         __syncthreads();
@@ -278,12 +288,26 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
         const int k0 = ex.pkind ? uni(ex.pkind[i]) : -1;
         if ((k0 >= 0) != NX) continue;   // the other instantiation's entry
         constexpr bool nx = NX;
+        // non-exact: k_relax applied pool positions [0, first) in order (tw holds their minima)
+        const int first = nx ? uni(ex.nxh[(size_t)slot * 4 + 3]) : 0;
+        // second non-exact launch (ex.nx_ms): only the maxState of the blocks after this pass
+        // stopped (all its leaves <= optimalLB) up to the record's pruning position
+        const bool ph2 = nx && ex.nx_ms;
+        int bfrom = nx ? first / kWave : 0, bto = -1;
+        if (ph2) {
+            const int p = uni(ex.P[i]);
+            const int lastpos = (p < ex.no ? p : ex.no) - 1;
+            bfrom = uni(ex.pstop[item]) + 1;
+            bto = lastpos / kWave;
+            if (lastpos < first || bfrom > bto) continue;
+        }
         const int kb = nx ? k0 : 0;
         const int T = Tdd - kb;
+        const int E = (T - 1) * us;
+        if (!NX && (E > kExactMaxEntries) != kWide) continue;   // the other row count's entry
         const GBL uint32_t *lay = sc.lay + (size_t)slot * sc.Tcap * 5;
         const uint32_t lnoff = uni(lay[Tdd - 1]), lnn = uni(lay[sc.Tcap + Tdd - 1]);
         const size_t N = (size_t)slot * sc.Ncap;
-        const int E = (T - 1) * us;
         for (int e = tid; e < E; e += kLeafWaves * kWave) {
             const int k = e / us + 1, r = e % us;
             S.stab[e] = r == 0 ? -1 : slot_of(net, g, len, aligned, kb + k, r);
@@ -341,17 +365,26 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
         uint32_t done = 0;
         int nb_done = 0;
         bool finished = false;   // every leaf of the pass <= optimalLB
-        // non-exact: pool order only (no screening columns, no lazy passes); the pass may stop
-        // early only when it is the record's only one (maxState needs every leaf's value at
-        // every cut before the pruning position)
+        // non-exact: pool order only (no screening columns, no lazy passes); a pass stops once
+        // its leaves are <= optimalLB, and the second launch completes the maxState of the later
+        // blocks before the record's pruning position (every leaf's value at every such cut)
         const int nbs_r = nx ? 0 : nbs;
         const int nblk_r = nx ? (ex.no + kWave - 1) / kWave : nblk;
-        const bool single_pass = lnn <= (uint32_t)kLeafPass;
         // lazy passes stop after ex.lazy blocks (the newest cuts); see ExactIO::lazy
         const int nlim = (!nx && ex.lazy > 0 && nbs == 0) ? min(nblk, ex.lazy) : nblk_r;
-        // non-exact: per leaf the first cut (pool position) with value <= optimalLB
-        if (nx && lane() < kLeavesPerWave) S.lw[w].fle[lane()] = INT_MAX;
-        for (int bb = 0; bb < nlim; bb++) {
+        // non-exact: per leaf the first cut (pool position) with value <= optimalLB; a leaf whose
+        // in-order minimum already is counts as done before the phase
+        double twold = EDMAX;
+        if (nx) {
+            const bool al = lane() < cnt && ((alive >> lane()) & 1u);
+            if (al) twold = sc.tw[N + lnoff + (uint32_t)(j0 + lane())];
+            const bool pre = al && twold <= incumbent;
+            done = (uint32_t)__ballot(pre);
+            if (lane() < kLeavesPerWave) S.lw[w].fle[lane()] = pre ? 0 : INT_MAX;
+        }
+        int bb_last = -1;
+        for (int bb = bfrom; bb < (ph2 ? bto + 1 : nlim); bb++) {
+            bb_last = bb;
             nb_done = bb + 1;
             const bool scr = bb < nbs_r;
             const int b = scr ? bb : bb - nbs_r;
@@ -367,7 +400,7 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
             }
             __syncthreads();
             const int s = b * kWave + lane();
-            const bool vc = s < ncut;
+            const bool vc = s < ncut && s >= first;
             double ms = -INFINITY;   // non-exact: max over this wave's alive leaves, this lane's cut
             if (cnt > 0 && (nx || (done & alive) != alive)) {
                 const double root = vc ? (scr ? ex.RS[(size_t)i * kExactScreen + s] : ex.R[(size_t)i * ex.ostride + s]) : 0.0;
@@ -386,10 +419,10 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
                             if (row == kRowDead) v = EDMIN;
                             else if (row == kRowNoAdd) v = par;
                             else v = par + S.C[row][lane()];
-                            if (vc && ((open >> j) & 1u)) m[j] = rmin(m[j], v);
+                            if (!ph2 && vc && ((open >> j) & 1u)) m[j] = rmin(m[j], v);
                             if (nx) {
                                 ms = (vc && v > ms) ? v : ms;
-                                if ((open >> j) & 1u) {
+                                if (!ph2 && ((open >> j) & 1u)) {
                                     const uint64_t hit = __ballot(vc && v <= incumbent);
                                     if (hit) {
                                         if (lane() == 0) S.lw[w].fle[j] = b * kWave + (int)(__ffsll((unsigned long long)hit) - 1);
@@ -421,11 +454,16 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
                 if (mx != -INFINITY) atomicMax(&ex.MS[(size_t)i * ex.ostride + s], nx_key(mx));
             }
             __syncthreads();
-            if (all && (!nx || single_pass)) {
+            if (all && !ph2) {
                 finished = true;
                 break;
             }
         }
+        if (ph2) {
+            __syncthreads();
+            continue;
+        }
+        if (nx && tid == 0) ex.pstop[item] = bb_last;   // k_nx leaf phase 2 resumes after it
         if (nx) {
             // the pass's pruning position: max over its alive leaves of their first cut <= optimalLB
             const int fl = (lane() < kLeavesPerWave && ((alive >> lane()) & 1u)) ? S.lw[w].fle[lane()] : 0;
@@ -439,7 +477,14 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
         for (int j = 0; j < kLeavesPerWave; j++) {
             if ((alive >> j) & 1u) {
                 double v = lane_reduce<1>(m[j], [](double a, double b) { return rmin(a, b); });
-                if (!lazy && v == 0.0 && v > incumbent && !((done >> j) & 1u)) v = first_zero(net, ex, S, w, j, T, us, i);
+                if (nx) {
+                    // std::min(w, v) over the phase's cuts after the in-order ones: the old weight
+                    // stays on ties; a new zero minimum takes the first zero's sign
+                    const double old = lane_get(twold, j);
+                    if (!(v < old)) v = old;
+                    else if (v == 0.0 && v > incumbent && !((done >> j) & 1u)) v = first_zero(net, ex, S, w, j, T, us, i, first);
+                } else if (!lazy && v == 0.0 && v > incumbent && !((done >> j) & 1u))
+                    v = first_zero(net, ex, S, w, j, T, us, i);
                 if (lane() == 0) {
                     sc.tw[N + lnoff + (uint32_t)(j0 + j)] = v;
                     if (lazy) sc.nflag[N + lnoff + (uint32_t)(j0 + j)] |= kLazy;
@@ -450,7 +495,7 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
     }
 }
 
-size_t exact_leaf_lds_bytes() { return sizeof(LeafShared); }
+size_t exact_leaf_lds_bytes() { return sizeof(LeafSharedT<kExactMaxEntries>); }
 
 // ---- k_nx_dag: the DAG part of non-exact records (kNxPending) ------------------------------
 // One wave per work item (pending record, block of kNxCuts cuts), blocks outermost so that the
@@ -596,18 +641,20 @@ __device__ void nx_dag_item(const NetDev &net, const Scratch &sc, const ExactIO 
 
 __global__ void __launch_bounds__(kWave) k_nx_dag(NetDev net, Scratch sc, ExactIO ex) {
     __shared__ NxShared S;
-    const int npend = (int)(ex.ctr[0] >> 32);
-    if (npend == 0) return;
+    const int nnx = (int)ex.ctr[12];   // non-exact entries (ExactIO::nxlist)
+    if (nnx == 0) return;
     const long long nblk = (ex.no + kNxCuts - 1) / kNxCuts;
-    const long long total = nblk * npend;
+    const long long total = nblk * nnx;
     for (;;) {
         if (lane() == 0) S.item = (int32_t)atomicAdd(&ex.ctr[6], 1ull);
         __builtin_amdgcn_wave_barrier();
         const long long item = (long long)uni(S.item);
         __builtin_amdgcn_wave_barrier();
         if (item >= total) break;
-        const int b = (int)(item / npend), i = (int)(item % npend);
-        if (uni(ex.pkind[i]) < 0) continue;
+        const int b = (int)(item / nnx);
+        const int i = uni(ex.nxlist[item % nnx]);
+        // blocks k_relax already applied in order
+        if ((b + 1) * kNxCuts <= uni(ex.nxh[(size_t)uni(ex.pend_slot[i]) * 4 + 3])) continue;
         nx_dag_item(net, sc, ex, S, i, b);
     }
 }
@@ -631,11 +678,24 @@ hipError_t launch_exact(const NetDev &net, const Scratch &sc, const ExactIO &ex,
         hipLaunchKernelGGL(k_nx_dag, dim3(5 * cus), dim3(kWave), 0, st, net, sc, ex);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_exact_leaf<false>, dim3(4 * cus), dim3(kLeafWaves * kWave), sizeof(LeafShared), st, net, sc, ex,
-                       incumbent);
-    if ((e = hipGetLastError()) != hipSuccess || !ex.nx || !ex.pkind) return e;
-    hipLaunchKernelGGL(k_exact_leaf<true>, dim3(4 * cus), dim3(kLeafWaves * kWave), sizeof(LeafShared), st, net, sc, ex,
-                       incumbent);
+    using Narrow = LeafSharedT<kExactMaxEntries>;
+    using Wide = LeafSharedT<kExactMaxEntriesWide>;
+    hipLaunchKernelGGL((k_exact_leaf<false, kExactMaxEntries>), dim3(4 * cus), dim3(kLeafWaves * kWave), sizeof(Narrow), st,
+                       net, sc, ex, incumbent);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((kExactMaxT - 1) * sc.us > kExactMaxEntries) {   // deeper / wider exact trees are possible
+        hipLaunchKernelGGL((k_exact_leaf<false, kExactMaxEntriesWide>), dim3(4 * cus), dim3(kLeafWaves * kWave), sizeof(Wide),
+                           st, net, sc, ex, incumbent);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (!ex.nx || !ex.pkind) return hipSuccess;
+    hipLaunchKernelGGL((k_exact_leaf<true, kExactMaxEntries>), dim3(4 * cus), dim3(kLeafWaves * kWave), sizeof(Narrow), st,
+                       net, sc, ex, incumbent);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    ExactIO ms = ex;
+    ms.nx_ms = 1;
+    hipLaunchKernelGGL((k_exact_leaf<true, kExactMaxEntries>), dim3(4 * cus), dim3(kLeafWaves * kWave), sizeof(Narrow), st,
+                       net, sc, ms, incumbent);
     return hipGetLastError();
 }
 

@@ -78,14 +78,28 @@ def test_bnb_parity_c5():
 def test_bnb_parity_c4_at_timed_pool_size():
     """The pool sizes the timed B&B legs run against (10^4 cuts, not the 10^2-10^3 of the
     round-by-round checks above): the seeded C4 / 256 search with uncapped refinement loops
-    until its optimality list holds 20 000 cuts, then the next 1 024-record batch on the device
-    -- exact records through the cut-parallel phase, non-exact survivors through the batched
-    sweeps -- against ref_dd relaxp on the same pool, bit for bit, 8 records of each outcome."""
+    until its optimality list holds 20 000 cuts, then the first batch of the next rounds that
+    holds both exact leaves and non-exact survivors -- exact records through the cut-parallel
+    exact phase, non-exact records past the first 256 optimality cuts through the cut-parallel
+    non-exact phase (k_nx_*, or k_relax's re-run where a width-1 pruning may fire) -- against
+    ref_dd relaxp on the same pool, bit for bit, 8 records of each outcome."""
     rep = bp.check_large_pool("C4", 1, 128, min_opt_cuts=20000, per_kind=8)
     assert not rep["failures"], "\n".join(rep["failures"][:10])
     assert rep["pool_optimality"] >= 20000, rep
-    assert rep["sampled"]["exact"] >= 1 and rep["sampled"]["survivor"] >= 1, rep
+    # at this pool the C4 search's batches hold exact leaves and non-exact records a cut prunes
+    assert rep["sampled"]["exact"] >= 1 and rep["sampled"]["survivor"] + rep["sampled"]["pruned"] >= 1, rep
     assert rep["checked"] >= 8
+
+
+def test_bnb_parity_c3_survivors_at_large_pool():
+    """The rounds of non-exact survivors (a 1 024-record launch against a pool of
+    7 x 10^4 cuts): the seeded C3 / 64 search until its pool holds 40 000 optimality cuts, then
+    the first batch with exact leaves and non-exact survivors -- the survivors through the
+    cut-parallel non-exact phase (k_nx_dag / k_exact_leaf / k_nx_fin) -- against ref_dd relaxp."""
+    rep = bp.check_large_pool("C3", 1, 64, min_opt_cuts=40000, per_kind=8, need_rounds=40, max_seconds=400.0)
+    assert not rep["failures"], "\n".join(rep["failures"][:10])
+    assert rep["pool_optimality"] >= 40000, rep
+    assert rep["sampled"]["exact"] >= 1 and rep["sampled"]["survivor"] >= 1, rep
 
 
 @pytest.mark.parametrize("knob,value", [("SGUFP_EXACT_FAST", "0"), ("SGUFP_EXACT_LAZY", "1"),

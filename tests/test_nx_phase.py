@@ -1,6 +1,6 @@
 """Cut-parallel optimality phase of NON-exact DDs (k_nx_dag / k_exact_leaf<true> / k_nx_fin,
-kNxPending in dd_device.hpp): with SGUFP_NX_MIN=1 every non-exact record that reaches its
-optimality cuts takes it -- whatever the pool size -- and must give the reference's results bit
+kNxPending in dd_device.hpp): with SGUFP_NX_MIN=1 and SGUFP_NX_SKIP=0 every non-exact record
+that reaches its optimality cuts takes it -- whatever the pool size -- and must give the reference's results bit
 for bit (fixtures of tests/golden, the bench workload against the in-order path), including
 the records whose width-1 pruning might fire, which k_nx_fin hands back to k_relax
 (kNxFallback).  The B&B pools of tests/test_bnb_parity.py (10^4+ O cuts) take the phase under
@@ -28,10 +28,14 @@ def _stats(text):
     return items, fb
 
 
+@pytest.mark.parametrize("skip", ["0", "8"])
 @pytest.mark.parametrize("name", sorted({c["name"] for c in golden_io.manifest()}))
-def test_nx_phase_on_fixtures(monkeypatch, capfd, name):
+def test_nx_phase_on_fixtures(monkeypatch, capfd, name, skip):
+    """skip: optimality cuts k_relax applies in order before the hand-off (SGUFP_NX_SKIP; the
+    phase then starts from the in-order terminal weights)."""
     monkeypatch.setenv("SGUFP_NX", "1")
     monkeypatch.setenv("SGUFP_NX_MIN", "1")
+    monkeypatch.setenv("SGUFP_NX_SKIP", skip)
     monkeypatch.setenv("SGUFP_EXACT_STATS", "1")
     d = golden_io.case_dir(name)
     e = E.Engine(f"{d}/net.txt", 0, 256)
@@ -63,6 +67,7 @@ def test_nx_phase_engages_and_matches_in_order(monkeypatch, capfd, tmp_path):
     e0.add_cuts(pool)
     monkeypatch.setenv("SGUFP_NX", "1")
     monkeypatch.setenv("SGUFP_NX_MIN", "1")
+    monkeypatch.setenv("SGUFP_NX_SKIP", "0")
     monkeypatch.setenv("SGUFP_EXACT_STATS", "1")
     e1 = E.Engine(net, 0, 1024)
     e1.add_cuts(pool)

@@ -29,6 +29,7 @@ def main():
     e0.add_cuts(pool)
     os.environ["SGUFP_NX"] = "1"
     os.environ["SGUFP_NX_MIN"] = "1"
+    os.environ["SGUFP_NX_SKIP"] = sys.argv[2] if len(sys.argv) > 2 else "0"
     os.environ["SGUFP_EXACT_STATS"] = "1"
     e1 = E.Engine(net, 0, 1024)
     e1.add_cuts(pool)
