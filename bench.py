@@ -67,7 +67,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-sample", type=int, default=2048)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--profile-tag", default="r04")
+    ap.add_argument("--profile-tag", default="r05")
     ap.add_argument("--sub-paths", type=int, default=32, help="subproblem leg: random full-matching paths (0: skip)")
     ap.add_argument("--cpu-sub-seconds", type=float, default=8.0)
     ap.add_argument("--c5-nodes", type=int, default=4096,
@@ -227,6 +227,64 @@ def pmc_issue(tag: str, workload: str, kernel: str = "k_relax"):
             "issue_stall_frac": round(c.get("SQ_WAIT_INST_ANY", 0.0) / wc, 4),
             "cycles_per_wave_instruction": round(4.0 * wc / max(1.0, c.get("SQ_INSTS_VALU", 0.0) +
                                                                  c.get("SQ_INSTS_SALU", 0.0)), 2)}
+
+
+def bnb_profile_block(tag: str):
+    """The north-star loop's own profile: for the seeded B&B leg's command
+    (bench.py --mode bnb, C4 / 256, seeded by the width-128 heuristic), from
+    profiles/<tag>_bnbs_stats (rocprofv3 --kernel-trace --stats: every kernel's share of the GPU
+    time) and profiles/<tag>_bnbs_pmc_issue (rocprofv3 --pmc SQ_*: issue, wait and LDS counters
+    summed over every dispatch of the dominant kernels), only when they were collected with this
+    very library (lib.sha256 next to them); else None."""
+    import csv
+    d = os.path.join(ROOT, "profiles", f"{tag}_bnbs_stats")
+    dp = os.path.join(ROOT, "profiles", f"{tag}_bnbs_pmc_issue")
+    if profile_matches(d) != "library":
+        return None
+    shares = {}
+    for path in glob.glob(os.path.join(d, "*kernel_stats.csv")):
+        with open(path) as fh:
+            for r in csv.DictReader(fh):
+                name = r["Name"].split("(")[0].replace("void ", "").strip()
+                shares[name] = shares.get(name, 0.0) + float(r["TotalDurationNs"])
+    if not shares:
+        return None
+    tot = sum(shares.values())
+    top = sorted(shares.items(), key=lambda kv: -kv[1])
+    out = {"source": f"profiles/{tag}_bnbs_stats (rocprofv3 --kernel-trace --stats of bench.py --mode bnb "
+                     f"--bnb-config C4 --bnb-heuristic 128, libsgufp_hip.so sha256 {lib_sha256()[:16]})",
+           "gpu_seconds": round(tot * 1e-9, 3),
+           "kernel_shares": {k: round(v / tot, 4) for k, v in top[:6]},
+           "dominant_kernel": top[0][0], "dominant_share": round(top[0][1] / tot, 4)}
+    if profile_matches(dp) == "library":
+        acc = {}
+        for path in glob.glob(os.path.join(dp, "*counter_collection.csv")):
+            with open(path) as fh:
+                for r in csv.DictReader(fh):
+                    name = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
+                    acc.setdefault(name, {}).setdefault(r["Counter_Name"], 0.0)
+                    acc[name][r["Counter_Name"]] += float(r["Counter_Value"])
+        per = {}
+        for k, _ in top[:3]:
+            c = acc.get(k)
+            if not c or not c.get("SQ_WAVE_CYCLES"):
+                continue
+            wc = c["SQ_WAVE_CYCLES"]
+            insts = c.get("SQ_INSTS_VALU", 0.0) + c.get("SQ_INSTS_SALU", 0.0)
+            per[k] = {"active_frac": round(c.get("SQ_ACTIVE_INST_ANY", 0.0) / wc, 4),
+                      "wait_frac": round(c.get("SQ_WAIT_ANY", 0.0) / wc, 4),
+                      "lds_active_frac": round(c.get("SQ_ACTIVE_INST_LDS", 0.0) / wc, 4),
+                      "lds_bank_conflict_frac": round(c.get("SQ_LDS_BANK_CONFLICT", 0.0) /
+                                                      max(1.0, c.get("SQ_ACTIVE_INST_LDS", 0.0)), 4),
+                      "valu_insts": c.get("SQ_INSTS_VALU"), "salu_insts": c.get("SQ_INSTS_SALU"),
+                      "lds_insts": c.get("SQ_INSTS_LDS"),
+                      "cycles_per_wave_instruction": round(4.0 * wc / max(1.0, insts), 2)}
+        out["issue"] = per
+        out["issue_source"] = (f"profiles/{tag}_bnbs_pmc_issue (rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY "
+                               f"SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS "
+                               f"SQ_LDS_BANK_CONFLICT, same command and library; wave cycles in quad-cycles)")
+    out["bound"] = "issue/latency (waves parked on dependent LDS / memory round trips; see issue)"
+    return out
 
 
 def _native_comm(eng, world, rank):
@@ -578,6 +636,7 @@ def main():
             line["bnb_seeded"] = bnb_run(args.config, args.seed, "zero", args.bnb_leg_seconds, 1024,
                                          args.round_seconds, work, device=local, progress=0.0, tag="legs",
                                          heuristic=args.bnb_seeded_width)
+            line["bnb_seeded"]["roofline"] = bnb_profile_block(args.profile_tag)
     if rank == 0 and world == 1 and args.bnb_parity_rounds > 0:
         line["bnb_parity"] = bnb_parity_leg(args)
     if rank == 0 and world == 1 and args.config == "C4" and args.c5_nodes > 0:

@@ -328,7 +328,7 @@ bool sgufp_ctx::exact_prepare() {
         ocap = cap;
     }
     if (!d_pslot && (!alloc(d_pslot, (size_t)max_batch, "exact pending") || !alloc(d_pbase, (size_t)max_batch, "exact pending") ||
-                     !alloc(d_ectr, 14, "exact pending") || !alloc(d_pidx, (size_t)max_batch, "exact pending")))
+                     !alloc(d_ectr, 16, "exact pending") || !alloc(d_pidx, (size_t)max_batch, "exact pending")))
         return false;
     if (!nx_prepare(no)) return false;
     if (o_built < no) {
@@ -349,7 +349,7 @@ bool sgufp_ctx::exact_prepare() {
     }
     ex.coefS = d_coefS;
     ex.RS = d_RS;
-    if (!hip_ok(hipMemsetAsync(d_ectr, 0, 14 * sizeof(unsigned long long), stream), "memset") ||
+    if (!hip_ok(hipMemsetAsync(d_ectr, 0, 16 * sizeof(unsigned long long), stream), "memset") ||
         !hip_ok(hipMemsetAsync(d_pidx, 0xFF, (size_t)max_batch * sizeof(int32_t), stream), "memset"))
         return false;
     ex.lazy = ex.nsc == 0 ? exact_lazy : 0;
@@ -428,16 +428,17 @@ bool sgufp_ctx::emit_current(const BatchIn &in, const Pool &p) {
     const char *es = std::getenv("SGUFP_EXACT_STATS");   // diagnostics (tests read them from stderr)
     const bool estats = es && es[0] == '1';
     if (estats && ex.enabled) {
-        unsigned long long c[14];
-        if (download(c, d_ectr, 14) && sync())
+        unsigned long long c[16];
+        if (download(c, d_ectr, 16) && sync())
             std::fprintf(stderr,
                          "[exact] pending %llu passes %llu blocks swept %llu of %llu (no %d, screen %d, lazy %d: "
                          "%llu resolves, %llu blocks); non-exact: dag items %llu, fallbacks %llu, kept back "
-                         "(ranks %llu, tail %llu, segment %llu, program %llu, other %llu), handed off %llu\n",
+                         "(ranks %llu, tail %llu, segment %llu, program %llu, other %llu), handed off %llu; exact "
+                         "leaves %llu, open after 16 blocks %llu, after 64 %llu\n",
                          c[0] >> 32, c[0] & 0xFFFFFFFFull, c[3],
                          (c[0] & 0xFFFFFFFFull) * (unsigned long long)((ex.no + 63) / 64 + (ex.nsc + 63) / 64), ex.no,
                          ex.nsc, ex.lazy, c[4], c[5], c[6], c[7], c[9] & 1023, (c[9] >> 10) & 1023, (c[9] >> 20) & 1023,
-                         (c[9] >> 30) & 1023, (c[9] >> 40) & 1023, c[12]);
+                         (c[9] >> 30) & 1023, (c[9] >> 40) & 1023, c[12], c[15], c[14], c[13]);
     }
     total_children = (int64_t)tot[0];
     total_csol = (int64_t)tot[1];

@@ -214,10 +214,11 @@ struct ExactIO {
     double SGUFP_GBL *R;                  // [max_batch][ostride]: root folds, pending index x newest-first position
     int32_t SGUFP_GBL *pend_slot;         // [max_batch] batch slot of pending record i
     uint32_t SGUFP_GBL *pend_base;        // [max_batch] first leaf pass of pending record i
-    unsigned long long SGUFP_GBL *ctr;    // [14]: (pending << 32 | leaf passes), root work, leaf work,
+    unsigned long long SGUFP_GBL *ctr;    // [16]: (pending << 32 | leaf passes), root work, leaf work,
                                           // blocks swept, lazy resolves, blocks they swept, non-exact:
                                           // DAG work, fallbacks, leaf work, kept back; wide leaf work,
-                                          // maxState completion work, non-exact entries
+                                          // maxState completion work, non-exact entries;
+                                          // diagnostics: exact leaves open after 64 / 16 blocks, alive
     // Lazy terminal weights: a leaf pass sweeps at most `lazy` cut blocks (the newest 64 x lazy
     // O cuts); when that leaves some leaf above optimalLB the pass's leaves keep the partial
     // minimum (an upper bound of the terminal weight) flagged kLazy, and the argmax scans

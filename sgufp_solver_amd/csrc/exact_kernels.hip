@@ -240,6 +240,12 @@ __device__ double first_zero(const NetDev &net, const ExactIO &ex, LeafShared &S
     return 0.0;
 }
 
+#ifndef SGUFP_LEAF_REGS
+#define SGUFP_LEAF_REGS 0   // 1: ancestor values in registers (spills at the 6-wave bound; measured slower)
+#endif
+#ifndef SGUFP_LEAF_PIPE
+#define SGUFP_LEAF_PIPE 1   // the next cut block's coefficients load while this one is swept
+#endif
 #ifndef SGUFP_LEAF_MIN_WAVES
 #define SGUFP_LEAF_MIN_WAVES 6   // three 8-wave workgroups per CU (VGPRs <= 85)
 #endif
@@ -375,6 +381,7 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
         // non-exact: per leaf the first cut (pool position) with value <= optimalLB; a leaf whose
         // in-order minimum already is counts as done before the phase
         double twold = EDMAX;
+        if (!nx && !ex.nx_ms && lane() == 0) atomicAdd(&ex.ctr[15], (unsigned long long)__popc(alive));
         if (nx) {
             const bool al = lane() < cnt && ((alive >> lane()) & 1u);
             if (al) twold = sc.tw[N + lnoff + (uint32_t)(j0 + lane())];
@@ -383,12 +390,45 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
             if (lane() < kLeavesPerWave) S.lw[w].fle[lane()] = pre ? 0 : INT_MAX;
         }
         int bb_last = -1;
-        for (int bb = bfrom; bb < (ph2 ? bto + 1 : nlim); bb++) {
+        const int bend = ph2 ? bto + 1 : nlim;
+#if SGUFP_LEAF_PIPE
+        // a block's coefficients are loaded into registers while the previous block is swept
+        // (every load of a block issued at once), stored to LDS at the top of its iteration --
+        // the end of the previous iteration's barriers found every wave done with the old ones
+        constexpr int kSU = (ROWS * kWave + kLeafWaves * kWave - 1) / (kLeafWaves * kWave);
+        double stg[kSU];
+        auto stage_load = [&](int bbx) {
+            const bool scrx = bbx < nbs_r;
+            const int bx = scrx ? bbx : bbx - nbs_r;
+            const int ncx = scrx ? ex.nsc : ex.no;
+            const GBL double *cmx = scrx ? ex.coefS : ex.coefO;
+            const size_t csx = scrx ? (size_t)kExactScreen : (size_t)ex.ostride;
+#pragma unroll
+            for (int u = 0; u < kSU; u++) {
+                const int x = tid + u * kLeafWaves * kWave;
+                const int e = x >> 6, l = x & (kWave - 1);
+                const int sx = bx * kWave + l;
+                const int sl = x < E * kWave ? S.stab[e] : -1;
+                stg[u] = (sl >= 0 && sx < ncx) ? cmx[(size_t)sl * csx + (scrx ? sx : ncx - 1 - sx)] : 0.0;
+            }
+        };
+        if (bfrom < bend) stage_load(bfrom);
+#endif
+        for (int bb = bfrom; bb < bend; bb++) {
             bb_last = bb;
             nb_done = bb + 1;
             const bool scr = bb < nbs_r;
             const int b = scr ? bb : bb - nbs_r;
             const int ncut = scr ? ex.nsc : ex.no;
+#if SGUFP_LEAF_PIPE
+#pragma unroll
+            for (int u = 0; u < kSU; u++) {
+                const int x = tid + u * kLeafWaves * kWave;
+                if (x < E * kWave) S.C[x >> 6][x & (kWave - 1)] = stg[u];
+            }
+            __syncthreads();
+            if (bb + 1 < bend) stage_load(bb + 1);
+#else
             const GBL double *cm = scr ? ex.coefS : ex.coefO;
             const size_t cs = scr ? (size_t)kExactScreen : (size_t)ex.ostride;
             // stage the block's coefficients: row e = (layer, rank), lane = cut
@@ -399,6 +439,7 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
                 S.C[e][l] = (sl >= 0 && s < ncut) ? cm[(size_t)sl * cs + (scr ? s : ncut - 1 - s)] : 0.0;
             }
             __syncthreads();
+#endif
             const int s = b * kWave + lane();
             const bool vc = s < ncut && s >= first;
             double ms = -INFINITY;   // non-exact: max over this wave's alive leaves, this lane's cut
@@ -407,12 +448,37 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
                 const uint32_t open = alive & ~done;
                 const uint32_t need = nx ? alive : open;
                 double par = root;
+#if SGUFP_LEAF_REGS
+                // ancestor values in registers (anc[k] = local layer k): a leaf recomputes the
+                // levels from its first ancestor that differs from the previous leaf's (dv), the
+                // same adds in the same order as walk_down, without its LDS round trip per level
+                double anc[kExactMaxT - 1];
+                anc[0] = root;
+#pragma unroll
+                for (int k = 1; k < kExactMaxT - 1; k++) anc[k] = root;
+#endif
 #pragma unroll
                 for (int j = 0; j < kLeavesPerWave; j++) {
                     if (j < cnt) {
                         const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)lp, j);
                         const int dj = (int)(x >> 8);
+#if SGUFP_LEAF_REGS
+                        if (dj < T - 1 || j == 0) {
+#pragma unroll
+                            for (int k = 1; k < kExactMaxT - 1; k++) {
+                                if (k < T - 1 && k >= dj) {
+                                    const uint32_t bq = uni((uint32_t)S.lw[w].info[j][k]);
+                                    const uint32_t r = bq & 63u;
+                                    anc[k] = !(bq & 128u) ? EDMIN : (r ? anc[k - 1] + S.C[(k - 1) * us + r][lane()] : anc[k - 1]);
+                                }
+                            }
+                            par = anc[0];
+#pragma unroll
+                            for (int k = 1; k < kExactMaxT - 1; k++) par = (k == T - 2) ? anc[k] : par;
+                        }
+#else
                         if (dj < T - 1 || j == 0) par = walk_down(S, w, j, dj, T, us, root);
+#endif
                         if ((need >> j) & 1u) {
                             const uint32_t row = x & 0x7Fu;
                             double v;
@@ -439,6 +505,9 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
                     for (int j = 0; j < kLeavesPerWave; j++)
                         if ((open >> j) & 1u)
                             if (__ballot(vc && m[j] <= incumbent)) done |= 1u << j;
+                    // diagnostics: leaves still open after 16 / 64 blocks
+                    if (lane() == 0 && (bb == 15 || bb == 63))
+                        atomicAdd(&ex.ctr[bb == 15 ? 14 : 13], (unsigned long long)__popc(alive & ~done));
                 }
             }
             if (nx) S.vb[w][0][lane()] = ms;   // free until the next block's walks
