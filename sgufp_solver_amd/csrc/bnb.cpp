@@ -694,6 +694,7 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
             }
             if (!ctx->hip_ok(launch_subproblem(ctx->sn, io, ctx->stream), "subproblem launch")) return SGUFP_ERR_HIP;
             ctx->sub_last_n = nf;
+            if (ctx->sub_stats) ctx->sub_stats_add(nf);
             const int first = ctx->n_rows;
             if (!ctx->hip_ok(launch_append_cuts(io.cut_type, io.cut_rhs, io.cut_row, nf, stride, first, ctx->d_rows,
                                                 ctx->d_rhs, ctx->d_coefT, ctx->nd.slot_tab, ctx->net.L, ctx->ustride,

@@ -120,6 +120,7 @@ bool sgufp_ctx::init() {
     if (const char *e = getenv("SGUFP_EXACT_SCREEN")) exact_screen = std::max(0, std::min(kExactScreen, atoi(e)));
     if (const char *e = getenv("SGUFP_EXACT_LAZY")) exact_lazy = std::max(0, atoi(e));
     if (const char *e = getenv("SGUFP_NX")) nx_on = atoi(e) != 0;
+    if (const char *e = getenv("SGUFP_SUB_STATS")) sub_stats = atoi(e) != 0;
     if (const char *e = getenv("SGUFP_NX_MIN")) nx_min = std::max(1, atoi(e));
     if (const char *e = getenv("SGUFP_NX_SKIP")) nx_skip = std::max(0, atoi(e));
     int64_t acap = std::max<int64_t>(1, (int64_t)std::max(0, L - 4) * (kRelaxedMaxWidth - 1) * maxU);
@@ -362,6 +363,25 @@ bool sgufp_ctx::exact_prepare() {
     ex.pend_base = d_pbase;
     ex.ctr = d_ectr;
     return true;
+}
+
+void sgufp_ctx::sub_stats_add(int n_paths) {
+    const size_t n = (size_t)n_paths * (size_t)sn.S;
+    std::vector<int32_t> w(2 * n);
+    if (!sio.wstat || !download(w.data(), sio.wstat, 2 * n) || !sync()) return;
+    ss[0] += 1;
+    ss[1] += (double)n;
+    for (size_t k = 0; k < n; k++) {
+        const int a = w[2 * k], p = w[2 * k + 1];
+        if (a < 0) ss[6] += 1;
+        else ss[3] += a;
+        ss[4] += p & 0xFFFFF;
+        ss[5] += (p >> 20) & 2047;
+    }
+    if ((int)ss[0] % 200 == 0)
+        std::fprintf(stderr, "[sub] launches %.0f scenarios %.0f: augmentations %.2f, flow passes %.2f, potential passes "
+                             "%.2f per scenario, fallbacks %.0f\n",
+                     ss[0], ss[1], ss[3] / ss[1], ss[4] / ss[1], ss[5] / ss[1], ss[6]);
 }
 
 // Buffers of the non-exact hand-off (ExactIO::nx): per pending entry its kind and pruning

@@ -203,6 +203,11 @@ struct sgufp_ctx {
     int16_t *d_wx = nullptr;
     int32_t *d_wa = nullptr;
     bool warm_reserve(int paths_per_launch);  // false: no ring (cold subproblems)
+    // SGUFP_SUB_STATS=1: the B&B's subproblem launches' augmentations and Bellman-Ford passes
+    // (io.wstat), summed and printed to stderr every 200 launches (diagnostics; syncs per launch)
+    bool sub_stats = false;
+    double ss[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // launches, scenarios, warm, augs, flow passes, potential passes, fallbacks, cold augs
+    void sub_stats_add(int n_paths);
     bool sub_init();
     bool sub_grow(int n, size_t total);
     bool append_rows(int is_feasibility, int n_cuts, const double *rhs, const std::vector<double> &rows);

@@ -304,6 +304,10 @@ constexpr int kLargeWaves = SGUFP_LARGE_WAVES;
 // Blk<NW>::all and the chain-numbering scan write one `red` slot per wave (8 in the layout)
 static_assert(kLargeWaves >= 1 && kLargeWaves <= 8, "the cross-wave reduction array holds 8 waves");
 constexpr int kRegGroupsSmall = 16, kRegGroupsLarge = (80 + kLargeWaves - 1) / kLargeWaves;
+#ifndef SGUFP_REG_GROUPS_WARM
+#define SGUFP_REG_GROUPS_WARM 13
+#endif
+constexpr int kRegGroupsWarm = SGUFP_REG_GROUPS_WARM;
 
 template <typename KT>
 struct ChainArcs {
@@ -742,6 +746,10 @@ __device__ __forceinline__ void invalidate_subtrees(const SubNet &N, const WS &W
 
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ bool is_cons(const SubNet &N, int v) { return N.inner[v] && !N.vbar[v]; }
+#ifndef SGUFP_REPAIR_MULTI
+#define SGUFP_REPAIR_MULTI 16   // augmentations along one predecessor tree (1: one per Bellman-Ford)
+#endif
+constexpr int kRepairMulti = SGUFP_REPAIR_MULTI;
 
 // Warm start.  The chains of a new path start from an earlier optimal state of the same
 // scenario (flow per arc, potentials alpha): a chain keeps the smallest earlier flow of its
@@ -790,85 +798,83 @@ __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nc
                 fresh = false;
             }
             if (!bellman_ford<RG, WT, NW>(N, W, nct, nz, kPotPlain, M, true, true)) { why = 1; return false; }
-            // the closest target (key, then node id): deficit nodes, and Z in stage 0
-            int64_t best = INT64_MAX;
-            for (int v = tid; v <= n; v += T) {
-                const bool tgt = v < n ? (is_cons(N, v) && imb[v] < 0) : stage == 0;
-                const KT k = W.key[v];
-                if (tgt && k < kKInf) {
-                    const int64_t c = (int64_t)k * 4096 + v;   // compact keys < 2^30, ids < 2^11 (host)
-                    best = c < best ? c : best;
+            // every target the predecessor tree reaches, closest first (key, then node id):
+            // deficit nodes, and Z in stage 0.  The first one's tree path is a shortest path of
+            // the extended network; the labels stay feasible potentials after it (its reverse
+            // arcs come back tight), so the tree paths of the further targets -- tight arcs --
+            // are shortest paths as well as long as every arc on them still has residual
+            // capacity and their source still has excess (the primal-dual step of several
+            // augmentations per Bellman-Ford); one whose path ran dry waits for the next one.
+            int64_t last = INT64_MIN;
+            for (int rep = 0; rep < kRepairMulti; rep++) {
+                int64_t best = INT64_MAX;
+                for (int v = tid; v <= n; v += T) {
+                    const bool tgt = v < n ? (is_cons(N, v) && imb[v] < 0) : stage == 0;
+                    const KT k = W.key[v];
+                    if (tgt && k < kKInf) {
+                        const int64_t c = (int64_t)k * 4096 + v;   // compact keys < 2^30, ids < 2^11 (host)
+                        if (c > last) best = c < best ? c : best;
+                    }
                 }
-            }
-            best = B::all(best, [](int64_t x, int64_t y) { return x < y ? x : y; }, W.red);
-#ifdef SGUFP_WARM_DEBUG
-            if (best == INT64_MAX) {
-                int fin = 0, nsrc = 0, ndef = 0, fsrc = 0, ninc = 0;
-                for (int v = tid; v < n; v += T) {
-                    fin += W.key[v] < kKInf;
-                    if (is_cons(N, v) && imb[v] > 0) { nsrc++; fsrc += W.key[v] < kKInf; }
-                    if (is_cons(N, v) && imb[v] < 0) ndef++;
-                    if (!is_cons(N, v) && imb[v] != 0) ninc++;
+                best = B::all(best, [](int64_t x, int64_t y) { return x < y ? x : y; }, W.red);
+                if (best == INT64_MAX) {
+                    if (rep == 0) { why = 2; return false; }
+                    break;
                 }
-                fin = (int)B::all((int64_t)fin, [](int64_t x, int64_t y) { return x + y; }, W.red);
-                nsrc = (int)B::all((int64_t)nsrc, [](int64_t x, int64_t y) { return x + y; }, W.red);
-                fsrc = (int)B::all((int64_t)fsrc, [](int64_t x, int64_t y) { return x + y; }, W.red);
-                ndef = (int)B::all((int64_t)ndef, [](int64_t x, int64_t y) { return x + y; }, W.red);
-                ninc = (int)B::all((int64_t)ninc, [](int64_t x, int64_t y) { return x + y; }, W.red);
-                if (tid == 0 && blockIdx.x < 6)
-                    printf("WARMDBG blk=%d stage=%d augs=%d n=%d nct=%d nz=%d finite=%d src=%d src_finite=%d def=%d "
-                           "noncons_imb=%d keyZ=%d\n", (int)blockIdx.x, stage, augs, n, nct, nz, fin, nsrc, fsrc, ndef, ninc,
-                           (int)W.key[n]);
-            }
-#endif
-            if (best == INT64_MAX) { why = 2; return false; }
-            const int tgt = (int)(best & 4095);
-            if (tid == 0) {
-                int v = tgt, len = 0;
-                while (len < n + 2) {
-                    const int32_t pr = W.pred[v];
-                    if (pr == kNoPred) break;
-                    W.plist[len++] = (uint16_t)(pr >> 15);
-                    v = (int)(pr & 0x7FFF);
+                last = best;
+                const int tgt = (int)(best & 4095);
+                if (tid == 0) {
+                    int v = tgt, len = 0;
+                    while (len < n + 2) {
+                        const int32_t pr = W.pred[v];
+                        if (pr == kNoPred) break;
+                        W.plist[len++] = (uint16_t)(pr >> 15);
+                        v = (int)(pr & 0x7FFF);
+                    }
+                    W.misc[3] = len;
+                    W.misc[4] = v;
                 }
-                W.misc[3] = len;
-                W.misc[4] = v;
-            }
-            B::sync();
-            const int plen = W.misc[3], src = W.misc[4];
-            const bool src_ok = stage == 0 ? (src < n && is_cons(N, src) && imb[src] > 0) : src == n;
-            int64_t delta = kInf;
-            for (int i = tid; i < plen; i += T) {
-                const int code = W.plist[i];
-                if (code >= 2 * m) continue;   // Z arcs: uncapacitated
-                const uint64_t cb = W.rb(code >> 1);
-                const int64_t x = ch_x(cb), U = ch_U(cb);
-                const int64_t cap = (code & 1) ? x : U - x;
-                delta = cap < delta ? cap : delta;
-            }
-            delta = B::all(delta, [](int64_t p, int64_t q) { return p < q ? p : q; }, W.red);
-            if (stage == 0 && src_ok) delta = (int64_t)imb[src] < delta ? (int64_t)imb[src] : delta;
-            if (tgt < n) delta = (int64_t)(-imb[tgt]) < delta ? (int64_t)(-imb[tgt]) : delta;
-            if (!src_ok || plen >= n + 2 || delta <= 0 || delta >= kInf) { why = 3; return false; }
-            B::sync();   // every lane read the imbalances before they change
-            for (int i = tid; i < plen; i += T) {
-                const int code = W.plist[i];
-                if (code >= 2 * m) continue;
-                const int k = code >> 1;
-                const uint64_t ca = W.ra(k), cb = W.rb(k);
-                const int64_t x = ch_x(cb), U = ch_U(cb);
-                const int64_t cap = (code & 1) ? x : U - x;
-                W.add_x(k, (int)((code & 1) ? -delta : delta));
-                if (cap == delta) W.key[(code & 1) ? ch_t(ca) : ch_h(ca)] = kKInf;   // segment used up
-            }
-            if (tid == 0) {
-                if (stage == 0) {
-                    imb[src] -= (int32_t)delta;
-                    if (imb[src] == 0) W.key[src] = kKInf;   // no longer a source
+                B::sync();
+                const int plen = W.misc[3], src = W.misc[4];
+                const bool src_ok = stage == 0 ? (src < n && is_cons(N, src) && imb[src] > 0) : src == n;
+                int64_t delta = kInf;
+                for (int i = tid; i < plen; i += T) {
+                    const int code = W.plist[i];
+                    if (code >= 2 * m) continue;   // Z arcs: uncapacitated
+                    const uint64_t cb = W.rb(code >> 1);
+                    const int64_t x = ch_x(cb), U = ch_U(cb);
+                    const int64_t cap = (code & 1) ? x : U - x;
+                    delta = cap < delta ? cap : delta;
                 }
-                if (tgt < n) imb[tgt] += (int32_t)delta;
+                delta = B::all(delta, [](int64_t p, int64_t q) { return p < q ? p : q; }, W.red);
+                if (stage == 0 && src_ok) delta = (int64_t)imb[src] < delta ? (int64_t)imb[src] : delta;
+                if (tgt < n) delta = (int64_t)(-imb[tgt]) < delta ? (int64_t)(-imb[tgt]) : delta;
+                if (!src_ok || plen >= n + 2 || delta <= 0 || delta >= kInf) {
+                    if (rep == 0) { why = 3; return false; }
+                    B::sync();
+                    continue;
+                }
+                B::sync();   // every lane read the imbalances before they change
+                for (int i = tid; i < plen; i += T) {
+                    const int code = W.plist[i];
+                    if (code >= 2 * m) continue;
+                    const int k = code >> 1;
+                    const uint64_t ca = W.ra(k), cb = W.rb(k);
+                    const int64_t x = ch_x(cb), U = ch_U(cb);
+                    const int64_t cap = (code & 1) ? x : U - x;
+                    W.add_x(k, (int)((code & 1) ? -delta : delta));
+                    if (cap == delta) W.key[(code & 1) ? ch_t(ca) : ch_h(ca)] = kKInf;   // segment used up
+                }
+                if (tid == 0) {
+                    if (stage == 0) {
+                        imb[src] -= (int32_t)delta;
+                        if (imb[src] == 0) W.key[src] = kKInf;   // no longer a source
+                    }
+                    if (tgt < n) imb[tgt] += (int32_t)delta;
+                }
+                B::sync();
+                if (++augs > max_aug) { why = 4; return false; }
             }
-            B::sync();
             invalidate_subtrees<NW>(N, W);
             // a source reached from another source (cheaper than its own key 0) hangs in that
             // one's predecessor tree: when that source runs dry the invalidation drops it too,
@@ -878,7 +884,6 @@ __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nc
                 if (src && W.key[v] > (KT)0) W.key[v] = (KT)0;
             }
             B::sync();
-            if (++augs > max_aug) { why = 4; return false; }
         }
     }
     return true;
@@ -1137,6 +1142,13 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
     const GBL int16_t *xprev = wsrc >= 0 ? io.wst_x + ((size_t)wsrc * S + s) * m : nullptr;
     const GBL int32_t *aprev = wsrc >= 0 ? io.wst_a + ((size_t)wsrc * S + s) * n : nullptr;
 
+#ifdef SGUFP_SUB_PHASES
+    uint64_t tph[6];
+    tph[0] = wall_clock64();
+#define SUB_PH(k) tph[k] = wall_clock64()
+#else
+#define SUB_PH(k)
+#endif
     // 1. decisions and matching
     if (tid < 8) W.misc[tid] = 0;
     for (int a = tid; a < m; a += T) {
@@ -1298,6 +1310,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         for (int v = tid; v <= n; v += T) W.alpha[v] = 0;
         B::sync();
     } else {
+        SUB_PH(1);
         // 3. successive shortest paths (max reward) from the sources to the sinks
 #ifdef SGUFP_SUB_TRACE
         const uint64_t tr0 = wall_clock64();
@@ -1428,11 +1441,13 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
             err_site = 9;
         }
 #endif
+        const int passes_flow = W.misc[5];
         if (io.wstat && tid == 0) {
             // fell back: -(why * 100000 + cold augmentations) - 1
             io.wstat[2 * b] = repaired ? warm_augs : (fell_back ? -(why * 100000 + iters) - 1 : iters);
-            io.wstat[2 * b + 1] = W.misc[5];
+            io.wstat[2 * b + 1] = passes_flow;
         }
+        SUB_PH(2);
         if (status == kSubOptimal) {
             // 4. potentials of the final residual: plain costs (optimal duals) or big-M
             //    costs (their M-multiple is a dual ray, case (iii))
@@ -1452,6 +1467,8 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
                 W.alpha[v] = (KT)((N.inner[v] && !N.vbar[v]) ? al : 0);
             }
             B::sync();
+            // passes: the flow's (bits 0-19) and the potentials' (bits 20-30)
+            if (io.wstat && tid == 0) io.wstat[2 * b + 1] = passes_flow | (min(W.misc[5] - passes_flow, 2047) << 20);
         }
     }
 
@@ -1467,6 +1484,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         B::sync();
     }
 
+    SUB_PH(3);
     // 5. dual solution / ray and the scenario's cut contribution
     int64_t rhs = 0, dual = 0;
     bool ok = true;
@@ -1509,6 +1527,13 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         io.dual[b] = status == kSubError ? -(double)err_site : (double)dual;
         io.rhs[b] = (double)rhs;
     }
+#ifdef SGUFP_SUB_PHASES
+    SUB_PH(4);
+    if (tid == 0 && blockIdx.x % 2047 == 0)
+        printf("SUBPH warm=%d chains %llu flow %llu potentials %llu dual %llu (ticks)\n", xprev != nullptr,
+               (unsigned long long)(tph[1] - tph[0]), (unsigned long long)(tph[2] - tph[1]),
+               (unsigned long long)(tph[3] - tph[2]), (unsigned long long)(tph[4] - tph[3]));
+#endif
 }
 
 // Per path, in scenario order: the first infeasible scenario's ray (grb.cpp:288-350,
@@ -1656,6 +1681,11 @@ hipError_t launch_scenarios(const SubNet &N, const SubIO &io, hipStream_t st) {
         else
             hipLaunchKernelGGL((k_sub_scenario<kRegGroupsLarge, int32_t, kLargeWaves, KT, false, WARM>),
                                dim3((unsigned)io.n_paths * N.S), dim3(kWave * kLargeWaves), lds, st, N, io);
+    } else if (WARM && io.nct_cap <= kRegGroupsWarm * kWave && !N.preds_lds) {
+        // warm starts: the repair's code needs registers too; 13 groups (the 1k-arc networks'
+        // ~800 chains) keep the all-in-registers kernel without the 16-group one's spills
+        hipLaunchKernelGGL((k_sub_scenario<kRegGroupsWarm, KT, 1, KT, true, WARM>), dim3((unsigned)io.n_paths * N.S),
+                           dim3(kWave), lds, st, N, io);
     } else if (io.nct_cap <= kRegGroupsSmall * kWave && !N.preds_lds) {
         // register groups hold key increments: 64-bit with 64-bit keys, 32-bit with 32-bit keys
         hipLaunchKernelGGL((k_sub_scenario<kRegGroupsSmall, KT, 1, KT, true, WARM>), dim3((unsigned)io.n_paths * N.S),
