@@ -757,14 +757,25 @@ bool sgufp_ctx::sub_init() {
             ub[(size_t)s * m + a] = N.ub[(size_t)a * S + s];
         }
     }
+    // rank of head(b) among the distinct heads of tail(b)'s out-arcs (network.cpp's slot order)
+    std::vector<int16_t> orank(m, 0);
+    for (int v = 0; v < n; v++) {
+        std::vector<int32_t> hs;
+        for (int a : N.out_arcs[v]) {
+            const auto it = std::find(hs.begin(), hs.end(), N.head[a]);
+            orank[a] = (int16_t)(it - hs.begin());
+            if (it == hs.end()) hs.push_back(N.head[a]);
+        }
+    }
     int32_t *d_tail, *d_head, *d_layer, *d_lb, *d_ub, *d_rew, *d_ioff, *d_il, *d_ooff, *d_ol, *d_soff, *d_shead, *d_z, *d_topo;
     uint8_t *d_vb, *d_inner;
+    int16_t *d_orank;
     if (!alloc(d_tail, m, "sub") || !alloc(d_head, m, "sub") || !alloc(d_layer, m, "sub") ||
         !alloc(d_lb, (size_t)S * m, "sub") || !alloc(d_ub, (size_t)S * m, "sub") || !alloc(d_rew, m, "sub") ||
         !alloc(d_ioff, n + 1, "sub") || !alloc(d_il, m, "sub") || !alloc(d_ooff, n + 1, "sub") ||
         !alloc(d_ol, m, "sub") || !alloc(d_soff, N.L + 1, "sub") || !alloc(d_shead, N.n_slots, "sub") ||
         !alloc(d_vb, n, "sub") || !alloc(d_inner, n, "sub") || !alloc(d_z, std::max(nz, 1), "sub") ||
-        !alloc(d_topo, m, "sub"))
+        !alloc(d_topo, m, "sub") || !alloc(d_orank, m, "sub"))
         return false;
     if (!upload(d_tail, N.tail.data(), m) || !upload(d_head, N.head.data(), m) || !upload(d_layer, arc_layer.data(), m) ||
         !upload(d_lb, lb.data(), lb.size()) || !upload(d_ub, ub.data(), ub.size()) || !upload(d_rew, rew.data(), m) ||
@@ -772,9 +783,9 @@ bool sgufp_ctx::sub_init() {
         !upload(d_ooff, out_off.data(), out_off.size()) || !upload(d_ol, out_list.data(), out_list.size()) ||
         !upload(d_soff, N.slot_off.data(), N.slot_off.size()) || !upload(d_shead, N.slot_head.data(), N.slot_head.size()) ||
         !upload(d_vb, vb.data(), n) || !upload(d_inner, in8.data(), n) || (nz && !upload(d_z, zlist.data(), nz)) || !upload(d_topo, arc_topo.data(), m) ||
-        !sync())
+        !upload(d_orank, orank.data(), m) || !sync())
         return false;
-    sn.n = n; sn.m = m; sn.S = S; sn.L = N.L; sn.n_slots = N.n_slots; sn.nz = nz; sn.zlist = d_z; sn.arc_topo = d_topo;
+    sn.n = n; sn.m = m; sn.S = S; sn.L = N.L; sn.n_slots = N.n_slots; sn.nz = nz; sn.zlist = d_z; sn.arc_topo = d_topo; sn.orank = d_orank;
     {
         // every arc sits in one chain, so M = 1 + sum_chains 2 |R| (U + 1) (k_sub_scenario)
         // is at most 1 + 2 sum_a |r_a| (max u + 1); residual costs are below R + M <= 2 M
@@ -823,6 +834,12 @@ bool sgufp_ctx::sub_grow(int n, size_t total) {
         if (d_wstat) release(d_wstat);
         if (!alloc(d_wstat, (size_t)cap * S * 2, "sub io")) return false;
         sio.wstat = d_wstat;
+        // per path: its chains (k_sub_paths), m entries each at most
+        const size_t pm = (size_t)cap * std::max(net.m, 1);
+        if (sio.pc_info) { release(sio.pc_info); release(sio.pc_th); release(sio.pc_ol); release(sio.pc_R); release(sio.pc_arcs); }
+        if (!alloc(sio.pc_info, (size_t)cap * 2, "sub paths") || !alloc(sio.pc_th, pm, "sub paths") ||
+            !alloc(sio.pc_ol, pm, "sub paths") || !alloc(sio.pc_R, pm, "sub paths") || !alloc(sio.pc_arcs, pm, "sub paths"))
+            return false;
         int64_t *po;
         if (!alloc(po, (size_t)cap + 1, "sub io")) return false;
         if (d_spoff) release(d_spoff);

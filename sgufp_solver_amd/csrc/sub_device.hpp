@@ -40,6 +40,9 @@ struct SubNet {
     const int32_t SGUFP_GBL *slot_head;  // [n_slots]
     const int32_t SGUFP_GBL *zlist;      // [nz] free-supply / free-demand nodes: v | src << 30 | snk << 29
     const int32_t SGUFP_GBL *arc_topo;   // [m] arcs by topological rank of their tail (chain order)
+    const int16_t SGUFP_GBL *orank;      // [m] rank of head(b) among the distinct heads of tail(b)'s
+                                         // out-arcs: b's coefficient slot in a layer (i, tail(b))
+                                         // is slot_off[layer] + orank[b] (network.cpp slots)
 };
 
 struct SubIO {
@@ -77,6 +80,15 @@ struct SubIO {
     int32_t SGUFP_GBL *wst_a;            // [slots][S][n]
     int32_t SGUFP_GBL *wstat;            // [P*S][2] or null: augmentations (negative: a warm start fell
                                          // back to the cold SSP), Bellman-Ford passes
+    // The chains of each path (k_sub_paths, once per path for all its scenarios: the chains
+    // depend on the decisions only).  Stride m per path; chains in phase 2's numbering (the
+    // topological order of their first arc's tail).
+    int32_t SGUFP_GBL *pc_info;          // [P][2] chains, error (invalid path / more chains than nct_cap)
+    uint32_t SGUFP_GBL *pc_th;           // [P][m] tail (-1: V-bar or none) | head << 16 (-1: open end), int16 each
+    uint32_t SGUFP_GBL *pc_ol;           // [P][m] offset of the chain's arcs in pc_arcs | length << 16
+    int32_t SGUFP_GBL *pc_R;             // [P][m] reward sum
+    uint32_t SGUFP_GBL *pc_arcs;         // [P][m] the chains' arcs, chain after chain: arc | slot << 16
+                                         // (int16; slot of the pair with the next arc, -1 at the end)
 };
 
 // Ring of warm-start states (the B&B's refinement loops, bnb.cpp): R slots, each holding the

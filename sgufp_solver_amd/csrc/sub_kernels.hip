@@ -242,12 +242,6 @@ __device__ __forceinline__ uint64_t pack_b(int L, int U, int x, int first) {
 __device__ __forceinline__ bool is_src(const SubNet &N, int v) { return N.in_off[v + 1] == N.in_off[v]; }
 __device__ __forceinline__ bool is_snk(const SubNet &N, int v) { return N.out_off[v + 1] == N.out_off[v]; }
 
-__device__ __forceinline__ int slot_of(const SubNet &N, int layer, int j) {
-    for (int s = N.slot_off[layer]; s < N.slot_off[layer + 1]; s++)
-        if (N.slot_head[s] == j) return s;
-    return -1;
-}
-
 // ---------------------------------------------------------------------------------------
 // Bellman-Ford over the residual graph of the contracted network.
 //   SSP mode: shortest paths from Z_out (node n) to Z_in (node n+1) under the big-M costs;
@@ -903,11 +897,13 @@ struct ChainOut {
 };
 
 template <class WS>
-__device__ __forceinline__ void add_coef(const SubNet &N, const WS &W, int layer, int j, int64_t v) {
-    if (v == 0) return;
-    const int s = slot_of(N, layer, j);
+__device__ __forceinline__ void add_coef(const WS &W, int s, int64_t v) {
     // integral values far below 2^53: the sum is exact in any order
-    if (s >= 0) __hip_atomic_fetch_add(&W.coef[s], (double)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v != 0 && s >= 0) __hip_atomic_fetch_add(&W.coef[s], (double)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// slot of the root variable (layer, head(b)) for an out-arc b of the layer's V-bar node
+__device__ __forceinline__ int slot_at(const SubNet &N, int layer, int b) {
+    return layer >= 0 ? N.slot_off[layer] + N.orank[b] : -1;
 }
 
 // sigma on in-arc a of V-bar node q: every (i, q, j) of q gets u_iq * sigma (grb.cpp:257-266)
@@ -916,15 +912,15 @@ __device__ __forceinline__ void add_sigma(const SubNet &N, const WS &W, int a, i
     if (sig == 0) return;
     const int q = N.head[a], layer = N.arc_layer[a];
     const int64_t u = N.ub[(size_t)s * N.m + a];
-    for (int k = N.out_off[q]; k < N.out_off[q + 1]; k++) add_coef(N, W, layer, N.head[N.out_list[k]], u * sig);
+    for (int k = N.out_off[q]; k < N.out_off[q + 1]; k++) add_coef(W, slot_at(N, layer, N.out_list[k]), u * sig);
 }
 // phi on out-arc b of V-bar node q: every (i, q, j) of q gets u_qj * phi (grb.cpp:268-277)
 template <class WS>
 __device__ __forceinline__ void add_phi(const SubNet &N, const WS &W, int b, int64_t ph, int s) {
     if (ph == 0) return;
-    const int q = N.tail[b], j = N.head[b];
+    const int q = N.tail[b];
     const int64_t u = N.ub[(size_t)s * N.m + b];
-    for (int k = N.in_off[q]; k < N.in_off[q + 1]; k++) add_coef(N, W, N.arc_layer[N.in_list[k]], j, u * ph);
+    for (int k = N.in_off[q]; k < N.in_off[q + 1]; k++) add_coef(W, slot_at(N, N.arc_layer[N.in_list[k]], b), u * ph);
 }
 
 template <class WS>
@@ -944,40 +940,37 @@ __device__ __forceinline__ int dec_of(const SubNet &N, const SubIO &io, int64_t 
 }
 
 // ray_mode: r = 0; prescribed targets (ray_p / ray_q) for the chain that certifies an
-// infeasibility up front.  The chain is walked from its first arc over the decisions, twice
-// and without per-arc arrays (a lane's chain of up to 63 arcs would otherwise live in scratch
-// memory): the first walk gets its length, reward sum, binding arcs and the transfer total
-// of a broken start; the second emits e, the transfers of the matched pairs and sigma / phi,
-// in the order of the closed forms below (all integers: any summation order is exact).
+// infeasibility up front.  The chain's arcs come from its path's list (k_sub_paths); they are
+// walked twice without per-arc arrays (a lane's chain of up to 63 arcs would otherwise live in
+// scratch memory): the first walk gets its length, reward sum, binding arcs and the transfer
+// total of a broken start; the second emits e, the transfers of the matched pairs and sigma /
+// phi, in the order of the closed forms below (all integers: any summation order is exact).
 template <class WS>
-__device__ __forceinline__ ChainOut assemble_chain(const SubNet &N, const WS &W, const SubIO &io, int64_t poff, int64_t plen,
-                                   int k, int first, int s, bool ray_mode, int ray_p, int ray_q, bool &ok) {
+__device__ __forceinline__ ChainOut assemble_chain(const SubNet &N, const WS &W, const GBL uint32_t *arcs, int nl,
+                                   int k, int s, bool ray_mode, int ray_p, int ray_q, bool &ok) {
     ChainOut o{0, 0};
     const uint64_t ca = W.ra(k);
     const int t = ch_t(ca), h = ch_h(ca);
     const size_t so = (size_t)s * N.m;
     auto rew = [&](int a) -> int64_t { return ray_mode ? 0 : (int64_t)N.reward[a]; };
     auto cost = [&](int a, int64_t e) -> int64_t { return e >= 0 ? (int64_t)N.ub[so + a] * e : (int64_t)N.lb[so + a] * e; };
-    // the arc after a in the chain, -1 at its end (head not V-bar, or no / no valid decision)
-    auto next = [&](int a) -> int {
-        if (!N.vbar[N.head[a]]) return -1;
-        const int d = dec_of(N, io, poff, plen, a);
-        return d >= 0 ? d : -1;
-    };
+    // the chain's arcs in order: arcs[0 .. nl) (k_sub_paths)
     // prescribed targets: beta = 1 on the max-l arc (e - 1), gamma = 1 on the min-u arc (e + 1)
     const bool prescribed = ray_mode && ray_p >= 0;
     auto pres = [&](int a) -> int64_t { return prescribed ? (int64_t)(a == ray_q) - (int64_t)(a == ray_p) : 0; };
-    // matched pair (a, b) at q = head(a) with transfer tt: lambda = max(tt, 0), mu = max(-tt, 0)
-    auto pair = [&](int a, int b, int64_t tt) {
+    // matched pair (a, b) at q = head(a) with transfer tt: lambda = max(tt, 0), mu = max(-tt, 0);
+    // coefficient slot (layer(a), head(b)) from the list
+    auto pair = [&](int a, int b, int slot, int64_t tt) {
         const int64_t lam = tt > 0 ? tt : 0, mu = tt < 0 ? -tt : 0;
         const int64_t v = (int64_t)N.ub[so + a] * lam + (int64_t)N.ub[so + b] * mu;
         o.rhs += v;
-        add_coef(N, W, N.arc_layer[a], N.head[b], -v);
+        add_coef(W, slot, -v);
     };
     // walk 1: length, sum r, first min-u / first max-l arc, sum_{i >= 1} (e_i - r_i)
     int len = 0, bmin = 0, bmax = 0;
     int64_t sumr = 0, dsum = 0, umin = 0, lmax = 0;
-    for (int a = first; a >= 0; a = next(a)) {
+    for (int i = 0; i < nl; i++) {
+        const int a = (int)(arcs[i] & 0xffffu);
         const int64_t u = N.ub[so + a], l = N.lb[so + a];
         if (len == 0 || u < umin) { umin = u; bmin = len; }
         if (len == 0 || l > lmax) { lmax = l; bmax = len; }
@@ -992,27 +985,30 @@ __device__ __forceinline__ ChainOut assemble_chain(const SubNet &N, const WS &W,
         const int64_t E = sumr - alpha_of(N, W, h) + alpha_of(N, W, t);
         const int bind = E > 0 ? bmin : bmax;
         int64_t tp = 0;
-        for (int a = first, i = 0; a >= 0; i++) {
-            const int b = next(a);
+        for (int i = 0; i < nl; i++) {
+            const uint32_t w = arcs[i];
+            const int a = (int)(w & 0xffffu), slot = (int16_t)(w >> 16);
+            const int b = i + 1 < nl ? (int)(arcs[i + 1] & 0xffffu) : -1;
             int64_t e = pres(a);
             if (!prescribed && i == bind && E != 0) e = E;
             o.obj += cost(a, e);
             if (b >= 0) {
                 tp = (i == 0) ? rew(a) + alpha_of(N, W, t) - e : rew(a) - e + tp;
-                pair(a, b, tp);
+                pair(a, b, slot, tp);
             }
-            a = b;
         }
     } else if (h < 0) {
         // broken end: forward transfers, sigma at the unmatched last in-arc absorbs (e <= 0)
         int64_t tp = 0;
-        for (int a = first, i = 0; a >= 0; i++) {
-            const int b = next(a);
+        for (int i = 0; i < nl; i++) {
+            const uint32_t w = arcs[i];
+            const int a = (int)(w & 0xffffu), slot = (int16_t)(w >> 16);
+            const int b = i + 1 < nl ? (int)(arcs[i + 1] & 0xffffu) : -1;
             const int64_t P = (i == 0) ? -alpha_of(N, W, t) : 0;
             int64_t e = pres(a);
             if (b >= 0) {
                 tp = rew(a) - P - e + tp;
-                pair(a, b, tp);
+                pair(a, b, slot, tp);
             } else {
                 const int64_t free_e = rew(a) - P + tp;     // e with sigma = 0
                 int64_t sig;
@@ -1022,15 +1018,16 @@ __device__ __forceinline__ ChainOut assemble_chain(const SubNet &N, const WS &W,
                 add_sigma(N, W, a, sig, s);
             }
             o.obj += cost(a, e);
-            a = b;
         }
     } else {
         // broken start only: backward transfers t_{j} = sum_{i > j} (e_i - r_i) + alpha(h),
         // i.e. T - sum_{1 <= i <= j} (e_i - r_i); phi at the unchosen first out-arc absorbs
         const int64_t T = len >= 2 ? dsum + alpha_of(N, W, h) : 0;
         int64_t pre = 0;
-        for (int a = first, i = 0; a >= 0; i++) {
-            const int b = next(a);
+        for (int i = 0; i < nl; i++) {
+            const uint32_t w = arcs[i];
+            const int a = (int)(w & 0xffffu), slot = (int16_t)(w >> 16);
+            const int b = i + 1 < nl ? (int)(arcs[i + 1] & 0xffffu) : -1;
             int64_t e = pres(a);
             if (i == 0) {
                 const int64_t P0 = (len == 1) ? alpha_of(N, W, h) : 0;
@@ -1044,50 +1041,22 @@ __device__ __forceinline__ ChainOut assemble_chain(const SubNet &N, const WS &W,
                 pre += e - rew(a);
             }
             o.obj += cost(a, e);
-            if (b >= 0) pair(a, b, T - pre);
-            a = b;
+            if (b >= 0) pair(a, b, slot, T - pre);
         }
     }
     o.rhs += o.obj;
     return o;
 }
 
-// The chains in phase 2's numbering with their first arcs, re-derived from the path (after
-// phase 2 the matching arrays are gone): arc a starts a chain iff its tail is not V-bar or no
-// in-arc of the tail decided a; chains are numbered in arc_topo order.  visit(k, a) runs on the
-// lane of each start (the scan itself runs on every lane).
-template <int NW, class WS, class F>
-__device__ __forceinline__ void chain_starts(const SubNet &N, const WS &W, const SubIO &io, int64_t poff, int64_t plen,
-                                             F visit) {
-    using B = Blk<NW>;
-    int nct = 0;
-    for (int base = 0; base < N.m; base += B::T) {
-        const int a = base + B::tid() < N.m ? N.arc_topo[base + B::tid()] : -1;
-        bool st = false;
-        if (a >= 0) {
-            const int q = N.tail[a];
-            st = true;
-            if (N.vbar[q])
-                for (int e = N.in_off[q]; e < N.in_off[q + 1]; e++)
-                    if (dec_of(N, io, poff, plen, N.in_list[e]) == a) { st = false; break; }
-        }
-        const uint32_t incl = wave_scan_incl(st ? 1u : 0u);
-        uint32_t woff = 0, tot;
-        if constexpr (NW == 1) {
-            tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
-        } else {
-            if (lane() == kWave - 1) W.red[B::wid()] = (int64_t)incl;
-            __syncthreads();
-            tot = 0;
-            for (int w = 0; w < NW; w++) {
-                const uint32_t c = (uint32_t)W.red[w];
-                woff += w < B::wid() ? c : 0u;
-                tot += c;
-            }
-            __syncthreads();
-        }
-        if (st) visit(nct + (int)(woff + incl) - 1, a);
-        nct += (int)tot;
+// A path's slice of the decisions (io.paths)
+__device__ __forceinline__ void path_span(const SubIO &io, int p, int64_t &poff, int64_t &plen) {
+    if (io.path_slot) {
+        const int sl = io.path_slot[p];
+        poff = (int64_t)sl * io.path_stride;
+        plen = io.path_len[sl];
+    } else {
+        poff = io.path_off[p];
+        plen = io.path_off[p + 1] - poff;
     }
 }
 
@@ -1125,15 +1094,6 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
 #endif
     const int n = N.n, m = N.m;
     const size_t so = (size_t)s * m;
-    int64_t poff, plen;
-    if (io.path_slot) {
-        const int sl = io.path_slot[p];
-        poff = (int64_t)sl * io.path_stride;
-        plen = io.path_len[sl];
-    } else {
-        poff = io.path_off[p];
-        plen = io.path_off[p + 1] - poff;
-    }
     const size_t b = (size_t)p * S + s;
     // warm start (compact kernels only: no lower bound, every scenario feasible)
     constexpr bool kWarm = WARM && WS::kCompact;
@@ -1149,82 +1109,30 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
 #else
 #define SUB_PH(k)
 #endif
-    // 1. decisions and matching
-    if (tid < 8) W.misc[tid] = 0;
-    for (int a = tid; a < m; a += T) {
-        W.chosen[a] = -1;
-        W.dec[a] = (int16_t)dec_of(N, io, poff, plen, a);
-    }
-    B::sync();
-    for (int a = tid; a < m; a += T) {
-        const int d = W.dec[a];
-        if (d == -3) W.misc[0] = 1;
-        if (d >= 0) W.chosen[d] = (int16_t)a;   // one of several writers wins ...
-    }
-    B::sync();
-    for (int a = tid; a < m; a += T) {
-        const int d = W.dec[a];
-        if (d >= 0 && W.chosen[d] != a) W.misc[0] = 1;   // ... the others: two in-arcs chose one
-    }                                                    // out-arc, not a path of an exact DD
-    B::sync();
-
-    // 2. chains, numbered in the topological order of their first arc's tail
-    int nct = 0;
-    for (int base = 0; base < m; base += T) {
-        const int a = base + tid < m ? N.arc_topo[base + tid] : -1;
-        bool st = false;
-        if (a >= 0) st = !N.vbar[N.tail[a]] || W.chosen[a] < 0;
-        const uint32_t incl = wave_scan_incl(st ? 1u : 0u);
-        uint32_t woff = 0, tot;
-        if constexpr (NW == 1) {
-            tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
-        } else {
-            if (lane() == kWave - 1) W.red[B::wid()] = (int64_t)incl;
-            __syncthreads();
-            tot = 0;
-            for (int w = 0; w < NW; w++) {
-                const uint32_t c = (uint32_t)W.red[w];
-                woff += w < B::wid() ? c : 0u;
-                tot += c;
-            }
-            __syncthreads();
-        }
-        const int pos = nct + (int)(woff + incl) - 1;
-        if (st && pos < io.nct_cap) {   // the first arc, until the record is assembled below
-            if constexpr (WS::kCompact) W.cta[pos] = (uint64_t)(uint32_t)a;
-            else W.ctb[pos] = pack_b(0, 0, 0, a);
-        }
-        nct += (int)tot;
-    }
-    if (nct > io.nct_cap) {   // more chains than the host counted: not a valid path
-        if (tid == 0) W.misc[0] = 1;
-        nct = io.nct_cap;
-    }
-    B::sync();
-    // free-supply / free-demand nodes (structural, from the host; read by every pass)
+    // 1-2. the path's chains (k_sub_paths: numbered in the topological order of their first
+    //      arc's tail, with ends, reward sums and arc lists) and the free-supply / free-demand
+    //      nodes (structural, from the host; read by every pass)
+    const size_t pcb = (size_t)p * m;
+    const int perr = io.pc_info[2 * p + 1];
+    const int nct = perr ? 0 : io.pc_info[2 * p];
+    if (tid < 8) W.misc[tid] = (tid == 0 && perr) ? 1 : 0;
     const int nz = N.nz;
     for (int i = tid; i < nz; i += T) W.zlist[i] = N.zlist[i];
     int first_bad = INT_MAX;   // first chain (rank) that makes the scenario infeasible up front
     for (int k = tid; k < nct; k += T) {
-        int a = WS::kCompact ? (int)(uint32_t)W.cta[k] : ch_first(W.rb(k));
-        const int first = a;
-        const int t0 = N.tail[a];
-        int L = N.lb[so + a], U = N.ub[so + a], R = N.reward[a];
-        int xw = xprev ? (int)xprev[a] : 0;   // warm start: the smallest earlier flow of the chain's arcs
-        int h = -1, len = 1;
-        for (;;) {
-            const int q = N.head[a];
-            if (!N.vbar[q]) { h = q; break; }
-            const int d = W.dec[a];
-            if (d < 0) break;
-            a = d;
-            if (++len > kMaxChain) { W.misc[0] = 1; break; }
+        const uint32_t th = io.pc_th[pcb + k], ol = io.pc_ol[pcb + k];
+        const int t = (int16_t)(th & 0xffffu), h = (int16_t)(th >> 16), len = (int)(ol >> 16);
+        const GBL uint32_t *arcs = io.pc_arcs + pcb + (ol & 0xffffu);
+        const int R = io.pc_R[pcb + k];
+        const int first = (int)(arcs[0] & 0xffffu);
+        int L = N.lb[so + first], U = N.ub[so + first];
+        int xw = xprev ? (int)xprev[first] : 0;   // warm start: the smallest earlier flow of the chain's arcs
+        for (int i = 1; i < len; i++) {
+            const int a = (int)(arcs[i] & 0xffffu);
             L = max(L, (int)N.lb[so + a]);
             U = min(U, (int)N.ub[so + a]);
-            R += N.reward[a];
             if (xprev) xw = min(xw, (int)xprev[a]);
         }
-        const int t = N.vbar[t0] ? -1 : t0;
         const bool complete = t >= 0 && h >= 0;
         int x0 = 0;
         if (xprev && complete) {
@@ -1238,7 +1146,6 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
     }
     first_bad = B::all(first_bad, [](int x, int y) { return x < y ? x : y; }, W.red);
     B::sync();
-    // chosen is dead from here: its space holds keys / predecessors
     for (int v = tid; v < N.n_slots; v += T) W.coef[v] = 0.0;
     __threadfence();   // zeros stored before any lane's atomic adds of phase 5
     B::sync();
@@ -1248,8 +1155,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         return;
     }
 
-    // warm start: node imbalances of the initial flow (conservation rows only; dec is dead in
-    // the compact kernels from here and its space holds them)
+    // warm start: node imbalances of the initial flow (conservation rows only, in dec's space)
     LDS int32_t *imb = (LDS int32_t *)W.dec;
     if (xprev) {
         for (int v = tid; v < n + 2; v += T) imb[v] = 0;
@@ -1293,20 +1199,20 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         status = kSubInfeasible;
         ray_chain = first_bad;
         const int k = first_bad;
-        int a = ch_first(W.rb(k));
+        const uint32_t ol = io.pc_ol[pcb + k];
+        const GBL uint32_t *arcs = io.pc_arcs + pcb + (ol & 0xffffu);
         const bool complete = ch_t(W.ra(k)) >= 0 && ch_h(W.ra(k)) >= 0;
-        int bp = a, bq = a;
-        int64_t bl = N.lb[so + a], bu = N.ub[so + a];
-        for (int len = 0; len < kMaxChain; len++) {
+        int bp = (int)(arcs[0] & 0xffffu), bq = bp;
+        int64_t bl = N.lb[so + bp], bu = N.ub[so + bp];
+        for (int i = 1; i < (int)(ol >> 16); i++) {
+            const int a = (int)(arcs[i] & 0xffffu);
             const int64_t l = N.lb[so + a], u = N.ub[so + a];
             if (l > bl) { bl = l; bp = a; }
             if (u < bu) { bu = u; bq = a; }
-            if (!N.vbar[N.head[a]] || W.dec[a] < 0) break;
-            a = W.dec[a];
         }
         if (complete) { ray_p = bp; ray_q = bq; }
         else { ray_p = bp; ray_q = -1; }
-        B::sync();   // every wave has walked its chain over dec before alpha (aliasing it) is zeroed
+        B::sync();
         for (int v = tid; v <= n; v += T) W.alpha[v] = 0;
         B::sync();
     } else {
@@ -1490,10 +1396,12 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
     bool ok = true;
     if (status != kSubError) {
         const bool ray = status == kSubInfeasible;
-        // chains with their first arcs, in the numbering of phase 2 (re-derived from the path)
-        chain_starts<NW>(N, W, io, poff, plen, [&](int k, int a) {
-            if (k >= nct || (ray && ray_chain >= 0 && k != ray_chain)) return;   // (i)/(ii): only the bad chain
-            ChainOut c = assemble_chain(N, W, io, poff, plen, k, a, s, ray, (k == ray_chain) ? ray_p : -1,
+        for (int k = tid; k < nct; k += T) {
+            if (ray && ray_chain >= 0 && k != ray_chain) continue;   // (i)/(ii): only the bad chain
+            const uint32_t ol = io.pc_ol[pcb + k];
+            const GBL uint32_t *arcs = io.pc_arcs + pcb + (ol & 0xffffu);
+            const int nl = (int)(ol >> 16);
+            ChainOut c = assemble_chain(N, W, arcs, nl, k, s, ray, (k == ray_chain) ? ray_p : -1,
                                         (k == ray_chain) ? ray_q : -1, ok);
             rhs += c.rhs;
             dual += c.obj;
@@ -1501,14 +1409,9 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
                 const uint64_t ca = W.ra(k);
                 const int x = ch_x(W.rb(k));
                 if (x && ch_t(ca) >= 0 && ch_h(ca) >= 0)
-                    for (int e = a, len = 0; e >= 0 && len < kMaxChain; len++) {
-                        xs[e] = (int16_t)x;
-                        if (!N.vbar[N.head[e]]) break;
-                        const int d = dec_of(N, io, poff, plen, e);
-                        e = d >= 0 ? d : -1;
-                    }
+                    for (int i = 0; i < nl; i++) xs[arcs[i] & 0xffffu] = (int16_t)x;
             }
-        });
+        }
         rhs = B::all(rhs, [](int64_t x, int64_t y) { return x + y; }, W.red);
         dual = B::all(dual, [](int64_t x, int64_t y) { return x + y; }, W.red);
         ok = B::any(ok ? 0u : 1u, W.red) == 0;
@@ -1534,6 +1437,93 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
                (unsigned long long)(tph[1] - tph[0]), (unsigned long long)(tph[2] - tph[1]),
                (unsigned long long)(tph[3] - tph[2]), (unsigned long long)(tph[4] - tph[3]));
 #endif
+}
+
+// Per path, once for all its scenarios: the chains (maximal runs of arcs joined by the path's
+// decisions at V-bar nodes, grb.cpp's constraint (1) pairs), numbered in the topological order
+// of their first arc's tail, each with its ends (t: -1 at a V-bar tail, h: -1 at an open end),
+// reward sum and arcs in order (with the coefficient slot of each matched pair).  k_sub_scenario's phases 2 and 5 read these lists instead of
+// walking the decisions per scenario (a dependent load per arc).  pc_info[2p + 1] flags a
+// path that no exact DD could have produced: a decision that is not an out-arc of its node,
+// two in-arcs choosing one out-arc, more chains than nct_cap or a chain over kMaxChain arcs.
+// One wave per path; LDS: decisions, their inverse, the chains' first arcs (int16 each).
+__global__ void __launch_bounds__(kWave) k_sub_paths(SubNet N, SubIO io) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    const int p = blockIdx.x;
+    if (p >= io.n_paths) return;
+    const int m = N.m, ln = lane();
+    LDS int16_t *dec = (LDS int16_t *)smem_raw;
+    LDS int16_t *chosen = dec + m, *first = chosen + m;
+    int64_t poff, plen;
+    path_span(io, p, poff, plen);
+    bool err = false;
+    for (int a = ln; a < m; a += kWave) {
+        const int d = dec_of(N, io, poff, plen, a);
+        chosen[a] = -1;
+        dec[a] = (int16_t)d;
+        err |= d == -3;
+    }
+    __syncthreads();
+    for (int a = ln; a < m; a += kWave) {
+        const int d = dec[a];
+        if (d >= 0) chosen[d] = (int16_t)a;   // one of several writers wins ...
+    }
+    __syncthreads();
+    for (int a = ln; a < m; a += kWave) {
+        const int d = dec[a];
+        err |= d >= 0 && chosen[d] != a;       // ... the others: two in-arcs chose one out-arc
+    }
+    int nct = 0;
+    for (int base = 0; base < m; base += kWave) {
+        const int a = base + ln < m ? N.arc_topo[base + ln] : -1;
+        const bool st = a >= 0 && (!N.vbar[N.tail[a]] || chosen[a] < 0);
+        const uint32_t incl = wave_scan_incl(st ? 1u : 0u);
+        if (st) first[nct + (int)incl - 1] = (int16_t)a;
+        nct += __builtin_amdgcn_readlane((int)incl, kWave - 1);
+    }
+    if (nct > io.nct_cap) { err = true; nct = io.nct_cap; }
+    __syncthreads();
+    const size_t pcb = (size_t)p * m;
+    int run = 0;
+    for (int base = 0; base < nct; base += kWave) {
+        const int k = base + ln;
+        int len = 0, t = -1, h = -1, R = 0, a = -1;
+        if (k < nct) {
+            a = first[k];
+            const int t0 = N.tail[a];
+            t = N.vbar[t0] ? -1 : t0;
+            len = 1;
+            R = N.reward[a];
+            for (int e = a;;) {
+                const int q = N.head[e];
+                if (!N.vbar[q]) { h = q; break; }
+                const int d = dec[e];
+                if (d < 0) break;
+                if (++len > kMaxChain) { err = true; break; }
+                e = d;
+                R += N.reward[e];
+            }
+        }
+        const uint32_t incl = wave_scan_incl((uint32_t)len);
+        const int o = run + (int)incl - len;
+        if (k < nct && o + len <= m) {
+            io.pc_th[pcb + k] = (uint32_t)(uint16_t)t | (uint32_t)(uint16_t)h << 16;
+            io.pc_ol[pcb + k] = (uint32_t)o | (uint32_t)len << 16;
+            io.pc_R[pcb + k] = R;
+            for (int i = 0; i < len; i++) {
+                const int b = i + 1 < len ? dec[a] : -1;
+                const int slot = b >= 0 ? slot_at(N, N.arc_layer[a], b) : -1;
+                io.pc_arcs[pcb + o + i] = (uint32_t)a | (uint32_t)(uint16_t)slot << 16;
+                a = b;
+            }
+        }
+        run += __builtin_amdgcn_readlane((int)incl, kWave - 1);
+    }
+    err = __builtin_amdgcn_ballot_w64(err) != 0;   // (a chain over kMaxChain arcs: its lane wrote
+    if (ln == 0) {                                  //  no further than the first kMaxChain + 1)
+        io.pc_info[2 * p] = nct;
+        io.pc_info[2 * p + 1] = err ? 1 : 0;
+    }
 }
 
 // Per path, in scenario order: the first infeasible scenario's ray (grb.cpp:288-350,
@@ -1602,14 +1592,7 @@ __global__ void __launch_bounds__(256) k_warm_pick(SubIO io, WarmRing wr, int pt
     const int n = io.n_paths;
     if (p >= n) return;
     int64_t poff, plen;
-    if (io.path_slot) {
-        const int sl = io.path_slot[p];
-        poff = (int64_t)sl * io.path_stride;
-        plen = io.path_len[sl];
-    } else {
-        poff = io.path_off[p];
-        plen = io.path_off[p + 1] - poff;
-    }
+    path_span(io, p, poff, plen);
     if (plen > wr.Lcap) plen = wr.Lcap;
     for (int l = threadIdx.x; l < wr.Lcap; l += blockDim.x) sp[l] = l < plen ? io.paths[poff + l] : (int16_t)-1;
     __syncthreads();
@@ -1706,6 +1689,7 @@ hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st) {
     // warm starts (io.warm_src / warm_dst) only in the 32-bit-key kernels: no lower bounds
     const bool k32 = N.key32 && !(ek && atoi(ek) == 1);
     const bool warm = k32 && (io.warm_src || io.warm_dst);
+    hipLaunchKernelGGL(k_sub_paths, dim3((unsigned)io.n_paths), dim3(kWave), (size_t)N.m * 3 * sizeof(int16_t), st, N, io);
     const hipError_t e = !k32 ? launch_scenarios<int64_t, false>(N, io, st)
                               : (warm ? launch_scenarios<int32_t, true>(N, io, st) : launch_scenarios<int32_t, false>(N, io, st));
     if (e != hipSuccess) return e;
