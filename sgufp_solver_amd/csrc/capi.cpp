@@ -836,9 +836,10 @@ bool sgufp_ctx::sub_grow(int n, size_t total) {
         sio.wstat = d_wstat;
         // per path: its chains (k_sub_paths), m entries each at most
         const size_t pm = (size_t)cap * std::max(net.m, 1);
-        if (sio.pc_info) { release(sio.pc_info); release(sio.pc_th); release(sio.pc_ol); release(sio.pc_R); release(sio.pc_arcs); }
+        if (sio.pc_info) { release(sio.pc_info); release(sio.pc_th); release(sio.pc_ol); release(sio.pc_R); release(sio.pc_arcs); release(sio.pc_rw); }
         if (!alloc(sio.pc_info, (size_t)cap * 2, "sub paths") || !alloc(sio.pc_th, pm, "sub paths") ||
-            !alloc(sio.pc_ol, pm, "sub paths") || !alloc(sio.pc_R, pm, "sub paths") || !alloc(sio.pc_arcs, pm, "sub paths"))
+            !alloc(sio.pc_ol, pm, "sub paths") || !alloc(sio.pc_R, pm, "sub paths") || !alloc(sio.pc_arcs, pm, "sub paths") ||
+            !alloc(sio.pc_rw, pm, "sub paths"))
             return false;
         int64_t *po;
         if (!alloc(po, (size_t)cap + 1, "sub io")) return false;

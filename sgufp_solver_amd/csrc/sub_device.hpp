@@ -89,6 +89,7 @@ struct SubIO {
     int32_t SGUFP_GBL *pc_R;             // [P][m] reward sum
     uint32_t SGUFP_GBL *pc_arcs;         // [P][m] the chains' arcs, chain after chain: arc | slot << 16
                                          // (int16; slot of the pair with the next arc, -1 at the end)
+    int32_t SGUFP_GBL *pc_rw;            // [P][m] their rewards, in the same order
 };
 
 // Ring of warm-start states (the B&B's refinement loops, bnb.cpp): R slots, each holding the

@@ -80,8 +80,7 @@ struct SubLds {
     static constexpr bool kAllReg = ALLREG;
     static constexpr int kHop = KeyT<KT>::hop_bits;
     static constexpr KT kKInf = KeyT<KT>::inf;
-    LDS int16_t *dec;       // [m] decision at the head (out-arc id, -1 none, -2 head not V-bar);
-                            //     phases 1-2 only (union), phase 5 reads dec_of from HBM
+    LDS int32_t *imb;       // [n+2] warm starts: node imbalances of the initial flow
     LDS uint64_t *cta;      // [nct_cap] chains, in the topological order of their tails
     // 16-byte records: cta (above) and ctb = L:16 | U:16 | x:16 | first arc:16.  With 32-bit
     // keys (no lower bound anywhere, u < 2^11, n + 2 < 2^11, sum |r| < 2^18: host) the first
@@ -144,8 +143,6 @@ struct SubLds {
         if constexpr (kPack) cta[k] += (uint64_t)(int64_t)d << 52;
         else *((LDS int16_t *)&ctb[k] + (kCompact ? 1 : 2)) += (int16_t)d;
     }
-    LDS int16_t *chosen;    // [m] in-arc that chose this out-arc of a V-bar node (phases 1-2;
-                            //     aliases key / pred)
     LDS KT *key;            // [n+2] Bellman-Ford keys (cost << hop bits | hops); then alpha in place
     LDS KT *alpha;          // == key: dual node potentials after the last Bellman-Ford
     LDS int32_t *pred;      // [n+2] code of the tight in-arc << 15 | its tail (kNoPred: none)
@@ -194,8 +191,8 @@ struct Blk {
     }
 };
 
-// LDS: chains, then a union -- phases 1-2: chosen and dec (int16 [m] each);
-// phases 3-5: key (alpha), pred, plist -- then the free-node list and flags.
+// LDS: chains, key (alpha), pred, plist, the warm start's imbalances, the free-node list and
+// flags.  (The chains' arcs come from k_sub_paths' lists in HBM.)
 constexpr int kSubLdsParts = 12;
 __host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int nz, int nw, size_t *off, int kbytes = 8,
                                                  bool warm = false) {
@@ -203,16 +200,10 @@ __host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int 
     off[1] = o; o = a16(o + (size_t)nct_cap * 8);
     // b words: 8 bytes, 4 with 32-bit keys, none in the single-wave kernel's 8-byte records
     off[2] = o; o = a16(o + (size_t)nct_cap * (kbytes == 4 ? (nw == 1 ? 0 : 4) : 8));
-    const size_t u0 = o;
-    off[3] = o; o = a16(o + (size_t)(n + 2) * kbytes);   // key | chosen
+    off[3] = o; o = a16(o + (size_t)(n + 2) * kbytes);   // key
     off[4] = o; o = a16(o + (size_t)(n + 2) * 4);   // pred
     off[8] = o; o = a16(o + (size_t)(n + 2) * 2);   // plist
-    off[0] = a16(u0 + (size_t)m * 2);               // dec, after chosen
-    // warm starts: dec's space then holds the node imbalances, which live through the
-    // repair's Bellman-Fords -- so past key / pred / plist, not over them
-    if (warm && off[0] < o) off[0] = o;
-    const size_t dsz = warm && (size_t)m * 2 < (size_t)(n + 2) * 4 ? (size_t)(n + 2) * 4 : (size_t)m * 2;
-    if (o < a16(off[0] + dsz)) o = a16(off[0] + dsz);
+    off[0] = o; o = a16(o + (warm ? (size_t)(n + 2) * 4 : 0));   // imbalances
     off[5] = o;
     off[6] = o; o = a16(o + (size_t)nz * 4);
     off[7] = o; o = a16(o + 8 * 4);
@@ -407,6 +398,7 @@ __device__ __forceinline__ uint32_t bf_sweep(const SubNet &N, const WS &W, int n
             changed = 1;
         }
     };
+    auto reg_w = [&](WT w) -> KT { return sizeof(WT) == sizeof(KT) ? (KT)w : (KT)(((int64_t)w << WS::kHop) + 1); };
     const int n = N.n;
     const int G = (nct + kWave - 1) / kWave;
     // chains of group g from LDS (groups past the register-resident ones)
@@ -416,7 +408,6 @@ __device__ __forceinline__ uint32_t bf_sweep(const SubNet &N, const WS &W, int n
         cb = 0;
         if (k < nct) { ca = W.ra(k); cb = W.rb(k); }
     };
-    auto reg_w = [&](WT w) -> KT { return sizeof(WT) == sizeof(KT) ? (KT)w : (KT)(((int64_t)w << WS::kHop) + 1); };
     if constexpr (NW > 1) {
         using B = Blk<NW>;
         const int S = (G + NW - 1) / NW, wv = B::wid();
@@ -768,30 +759,44 @@ constexpr int kRepairMulti = SGUFP_REPAIR_MULTI;
 // k_sub_scenario carries it (launches with warm starts); the cold one is unchanged.
 template <int RG, typename WT, int NW, class WS>
 __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nct, int nz, int64_t M,
-                                                      LDS int32_t *imb, int64_t max_aug, int &augs, int &why) {
+                                                      LDS int32_t *imb, int64_t max_aug, int &augs, int &why,
+                                                      uint64_t *tw) {
     using B = Blk<NW>;
+#ifdef SGUFP_SUB_PHASES
+    uint64_t t0 = wall_clock64();
+#define WR_T(k) { const uint64_t t1 = wall_clock64(); tw[k] += t1 - t0; t0 = t1; }
+#else
+#define WR_T(k)
+#endif
     using KT = typename WS::Key;
     constexpr KT kKInf = WS::kKInf;
     const int n = N.n, m = N.m;
     const int tid = B::tid();
     constexpr int T = B::T;
+    // conservation nodes among this thread's nodes tid + j T (n + 2 <= 32 T: host), so the
+    // loops below test a register bit instead of loading inner / vbar
+    uint32_t cm = 0;
+    for (int v = tid, j = 0; v < n; v += T, j++) cm |= (is_cons(N, v) ? 1u : 0u) << j;
+    auto cons = [&](int j) -> bool { return (cm >> j) & 1u; };
     for (int stage = 0; stage < 2; stage++) {
         bool fresh = true;
         for (;;) {
             uint32_t left = 0;
-            for (int v = tid; v < n; v += T)
-                if (is_cons(N, v) && (stage == 0 ? imb[v] > 0 : imb[v] < 0)) left = 1;
+            for (int v = tid, j = 0; v < n; v += T, j++)
+                if (cons(j) && (stage == 0 ? imb[v] > 0 : imb[v] < 0)) left = 1;
             if (!B::any(left, W.red)) break;
             if (fresh) {
-                for (int v = tid; v < n + 2; v += T) {
+                for (int v = tid, j = 0; v < n + 2; v += T, j++) {
                     KT k = kKInf;
-                    if (stage == 0 ? (v < n && is_cons(N, v) && imb[v] > 0) : v == n) k = 0;
+                    if (stage == 0 ? (v < n && cons(j) && imb[v] > 0) : v == n) k = 0;
                     W.key[v] = k;
                 }
                 B::sync();
                 fresh = false;
             }
+            WR_T(3);
             if (!bellman_ford<RG, WT, NW>(N, W, nct, nz, kPotPlain, M, true, true)) { why = 1; return false; }
+            WR_T(0);
             // every target the predecessor tree reaches, closest first (key, then node id):
             // deficit nodes, and Z in stage 0.  The first one's tree path is a shortest path of
             // the extended network; the labels stay feasible potentials after it (its reverse
@@ -802,8 +807,8 @@ __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nc
             int64_t last = INT64_MIN;
             for (int rep = 0; rep < kRepairMulti; rep++) {
                 int64_t best = INT64_MAX;
-                for (int v = tid; v <= n; v += T) {
-                    const bool tgt = v < n ? (is_cons(N, v) && imb[v] < 0) : stage == 0;
+                for (int v = tid, j = 0; v <= n; v += T, j++) {
+                    const bool tgt = v < n ? (cons(j) && imb[v] < 0) : stage == 0;
                     const KT k = W.key[v];
                     if (tgt && k < kKInf) {
                         const int64_t c = (int64_t)k * 4096 + v;   // compact keys < 2^30, ids < 2^11 (host)
@@ -869,17 +874,20 @@ __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nc
                 B::sync();
                 if (++augs > max_aug) { why = 4; return false; }
             }
+            WR_T(1);
             invalidate_subtrees<NW>(N, W);
             // a source reached from another source (cheaper than its own key 0) hangs in that
             // one's predecessor tree: when that source runs dry the invalidation drops it too,
             // so every remaining source (and Z) restarts from 0 at most
-            for (int v = tid; v <= n; v += T) {
-                const bool src = stage == 0 ? (v < n && is_cons(N, v) && imb[v] > 0) : v == n;
+            for (int v = tid, j = 0; v <= n; v += T, j++) {
+                const bool src = stage == 0 ? (v < n && cons(j) && imb[v] > 0) : v == n;
                 if (src && W.key[v] > (KT)0) W.key[v] = (KT)0;
             }
             B::sync();
+            WR_T(2);
         }
     }
+#undef WR_T
     return true;
 }
 
@@ -923,9 +931,10 @@ __device__ __forceinline__ void add_phi(const SubNet &N, const WS &W, int b, int
     for (int k = N.in_off[q]; k < N.in_off[q + 1]; k++) add_coef(W, slot_at(N, N.arc_layer[N.in_list[k]], b), u * ph);
 }
 
+// alpha of node v (-1: none); k_sub_scenario leaves 0 at free and V-bar nodes
 template <class WS>
 __device__ __forceinline__ int64_t alpha_of(const SubNet &N, const WS &W, int v) {
-    return (v >= 0 && N.inner[v] && !N.vbar[v]) ? (int64_t)W.alpha[v] : 0;
+    return v >= 0 ? (int64_t)W.alpha[v] : 0;
 }
 
 // Decision at the head of arc a from the path in HBM (phase 1 keeps it in LDS as dec; the
@@ -946,39 +955,60 @@ __device__ __forceinline__ int dec_of(const SubNet &N, const SubIO &io, int64_t 
 // total of a broken start; the second emits e, the transfers of the matched pairs and sigma /
 // phi, in the order of the closed forms below (all integers: any summation order is exact).
 template <class WS>
-__device__ __forceinline__ ChainOut assemble_chain(const SubNet &N, const WS &W, const GBL uint32_t *arcs, int nl,
-                                   int k, int s, bool ray_mode, int ray_p, int ray_q, bool &ok) {
+__device__ __forceinline__ ChainOut assemble_chain(const SubNet &N, const WS &W, const GBL uint32_t *arcs,
+                                                   const GBL int32_t *rws, int nl, int k, int s, bool ray_mode,
+                                                   int ray_p, int ray_q, bool &ok) {
     ChainOut o{0, 0};
     const uint64_t ca = W.ra(k);
     const int t = ch_t(ca), h = ch_h(ca);
     const size_t so = (size_t)s * N.m;
-    auto rew = [&](int a) -> int64_t { return ray_mode ? 0 : (int64_t)N.reward[a]; };
-    auto cost = [&](int a, int64_t e) -> int64_t { return e >= 0 ? (int64_t)N.ub[so + a] * e : (int64_t)N.lb[so + a] * e; };
-    // the chain's arcs in order: arcs[0 .. nl) (k_sub_paths)
+    // the chain's arcs in order, arcs[0 .. nl) with their rewards rws (k_sub_paths): arc id,
+    // coefficient slot of the pair with the next arc, u, l (0 in the compact kernels: no lower
+    // bounds, host) and r; walk 1 keeps the first two in registers for walk 2 (most chains
+    // have one or two arcs)
+    struct Arc {
+        int a, slot;
+        int64_t u, l, r;
+    };
+    auto load = [&](int i) -> Arc {
+        const uint32_t w = arcs[i];
+        Arc x;
+        x.a = (int)(w & 0xffffu);
+        x.slot = (int16_t)(w >> 16);
+        x.u = N.ub[so + x.a];
+        x.l = WS::kCompact ? 0 : N.lb[so + x.a];
+        x.r = ray_mode ? 0 : rws[i];
+        return x;
+    };
+    Arc c0{}, c1{};
+    auto get = [&](int i) -> Arc { return i == 0 ? c0 : (i == 1 ? c1 : load(i)); };
+    auto cost = [&](const Arc &x, int64_t e) -> int64_t { return e >= 0 ? x.u * e : x.l * e; };
     // prescribed targets: beta = 1 on the max-l arc (e - 1), gamma = 1 on the min-u arc (e + 1)
     const bool prescribed = ray_mode && ray_p >= 0;
     auto pres = [&](int a) -> int64_t { return prescribed ? (int64_t)(a == ray_q) - (int64_t)(a == ray_p) : 0; };
-    // matched pair (a, b) at q = head(a) with transfer tt: lambda = max(tt, 0), mu = max(-tt, 0);
-    // coefficient slot (layer(a), head(b)) from the list
-    auto pair = [&](int a, int b, int slot, int64_t tt) {
+    // matched pair (x, y) at q = head(x) with transfer tt: lambda = max(tt, 0), mu = max(-tt, 0),
+    // coefficient slot (layer(x), head(y)) from the list
+    auto pair = [&](const Arc &x, const Arc &y, int64_t tt) {
         const int64_t lam = tt > 0 ? tt : 0, mu = tt < 0 ? -tt : 0;
-        const int64_t v = (int64_t)N.ub[so + a] * lam + (int64_t)N.ub[so + b] * mu;
+        const int64_t v = x.u * lam + y.u * mu;
         o.rhs += v;
-        add_coef(W, slot, -v);
+        add_coef(W, x.slot, -v);
     };
     // walk 1: length, sum r, first min-u / first max-l arc, sum_{i >= 1} (e_i - r_i)
     int len = 0, bmin = 0, bmax = 0;
     int64_t sumr = 0, dsum = 0, umin = 0, lmax = 0;
     for (int i = 0; i < nl; i++) {
-        const int a = (int)(arcs[i] & 0xffffu);
-        const int64_t u = N.ub[so + a], l = N.lb[so + a];
-        if (len == 0 || u < umin) { umin = u; bmin = len; }
-        if (len == 0 || l > lmax) { lmax = l; bmax = len; }
-        sumr += rew(a);
-        if (len > 0) dsum += pres(a) - rew(a);
+        const Arc x = load(i);
+        if (i == 0) c0 = x;
+        else if (i == 1) c1 = x;
+        if (len == 0 || x.u < umin) { umin = x.u; bmin = len; }
+        if (len == 0 || x.l > lmax) { lmax = x.l; bmax = len; }
+        sumr += x.r;
+        if (len > 0) dsum += pres(x.a) - x.r;
         if (++len >= kMaxChain) { ok = false; return o; }
     }
     const bool complete = t >= 0 && h >= 0;
+    Arc x = c0, y{};
     if (complete) {
         // all of E = sum r - alpha(h) + alpha(t) on the binding arc (min u if E > 0, max l if
         // E < 0); transfers t_i = r_i - e_i + t_{i-1} from t_0 = r_0 + alpha(t) - e_0
@@ -986,38 +1016,38 @@ __device__ __forceinline__ ChainOut assemble_chain(const SubNet &N, const WS &W,
         const int bind = E > 0 ? bmin : bmax;
         int64_t tp = 0;
         for (int i = 0; i < nl; i++) {
-            const uint32_t w = arcs[i];
-            const int a = (int)(w & 0xffffu), slot = (int16_t)(w >> 16);
-            const int b = i + 1 < nl ? (int)(arcs[i + 1] & 0xffffu) : -1;
-            int64_t e = pres(a);
+            const bool more = i + 1 < nl;
+            if (more) y = get(i + 1);
+            int64_t e = pres(x.a);
             if (!prescribed && i == bind && E != 0) e = E;
-            o.obj += cost(a, e);
-            if (b >= 0) {
-                tp = (i == 0) ? rew(a) + alpha_of(N, W, t) - e : rew(a) - e + tp;
-                pair(a, b, slot, tp);
+            o.obj += cost(x, e);
+            if (more) {
+                tp = (i == 0) ? x.r + alpha_of(N, W, t) - e : x.r - e + tp;
+                pair(x, y, tp);
             }
+            x = y;
         }
     } else if (h < 0) {
         // broken end: forward transfers, sigma at the unmatched last in-arc absorbs (e <= 0)
         int64_t tp = 0;
         for (int i = 0; i < nl; i++) {
-            const uint32_t w = arcs[i];
-            const int a = (int)(w & 0xffffu), slot = (int16_t)(w >> 16);
-            const int b = i + 1 < nl ? (int)(arcs[i + 1] & 0xffffu) : -1;
+            const bool more = i + 1 < nl;
+            if (more) y = get(i + 1);
             const int64_t P = (i == 0) ? -alpha_of(N, W, t) : 0;
-            int64_t e = pres(a);
-            if (b >= 0) {
-                tp = rew(a) - P - e + tp;
-                pair(a, b, slot, tp);
+            int64_t e = pres(x.a);
+            if (more) {
+                tp = x.r - P - e + tp;
+                pair(x, y, tp);
             } else {
-                const int64_t free_e = rew(a) - P + tp;     // e with sigma = 0
+                const int64_t free_e = x.r - P + tp;     // e with sigma = 0
                 int64_t sig;
                 if (prescribed) sig = free_e - e;
                 else { sig = free_e > 0 ? free_e : 0; e = free_e - sig; }
                 if (sig < 0) ok = false;
-                add_sigma(N, W, a, sig, s);
+                add_sigma(N, W, x.a, sig, s);
             }
-            o.obj += cost(a, e);
+            o.obj += cost(x, e);
+            x = y;
         }
     } else {
         // broken start only: backward transfers t_{j} = sum_{i > j} (e_i - r_i) + alpha(h),
@@ -1025,23 +1055,23 @@ __device__ __forceinline__ ChainOut assemble_chain(const SubNet &N, const WS &W,
         const int64_t T = len >= 2 ? dsum + alpha_of(N, W, h) : 0;
         int64_t pre = 0;
         for (int i = 0; i < nl; i++) {
-            const uint32_t w = arcs[i];
-            const int a = (int)(w & 0xffffu), slot = (int16_t)(w >> 16);
-            const int b = i + 1 < nl ? (int)(arcs[i + 1] & 0xffffu) : -1;
-            int64_t e = pres(a);
+            const bool more = i + 1 < nl;
+            if (more) y = get(i + 1);
+            int64_t e = pres(x.a);
             if (i == 0) {
                 const int64_t P0 = (len == 1) ? alpha_of(N, W, h) : 0;
-                const int64_t free_e = rew(a) - P0 - T;       // e with phi = 0
+                const int64_t free_e = x.r - P0 - T;       // e with phi = 0
                 int64_t ph;
                 if (prescribed) ph = free_e - e;
                 else { ph = free_e > 0 ? free_e : 0; e = free_e - ph; }
                 if (ph < 0) ok = false;
-                add_phi(N, W, a, ph, s);
+                add_phi(N, W, x.a, ph, s);
             } else {
-                pre += e - rew(a);
+                pre += e - x.r;
             }
-            o.obj += cost(a, e);
-            if (b >= 0) pair(a, b, slot, T - pre);
+            o.obj += cost(x, e);
+            if (more) pair(x, y, T - pre);
+            x = y;
         }
     }
     o.rhs += o.obj;
@@ -1077,10 +1107,9 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
     size_t off[kSubLdsParts];
     sub_lds_layout(N.n, N.m, io.nct_cap, N.nz, NW, off, (int)sizeof(KT), WARM && sizeof(KT) == 4);
     WS W;
-    W.dec = (LDS int16_t *)(smem + off[0]);
+    W.imb = (LDS int32_t *)(smem + off[0]);
     W.cta = (LDS uint64_t *)(smem + off[1]);
     W.ctb = (LDS typename WS::CBT *)(smem + off[2]);
-    W.chosen = (LDS int16_t *)(smem + off[3]);
     W.key = (LDS KT *)(smem + off[3]);
     W.alpha = W.key;
     W.pred = (LDS int32_t *)(smem + off[4]);
@@ -1104,10 +1133,12 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
 
 #ifdef SGUFP_SUB_PHASES
     uint64_t tph[6];
+    uint64_t twr[4] = {0, 0, 0, 0};   // warm repair: Bellman-Fords, augmentations, invalidation, checks
     tph[0] = wall_clock64();
 #define SUB_PH(k) tph[k] = wall_clock64()
 #else
 #define SUB_PH(k)
+    uint64_t *twr = nullptr;
 #endif
     // 1-2. the path's chains (k_sub_paths: numbered in the topological order of their first
     //      arc's tail, with ends, reward sums and arc lists) and the free-supply / free-demand
@@ -1125,11 +1156,11 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         const GBL uint32_t *arcs = io.pc_arcs + pcb + (ol & 0xffffu);
         const int R = io.pc_R[pcb + k];
         const int first = (int)(arcs[0] & 0xffffu);
-        int L = N.lb[so + first], U = N.ub[so + first];
+        int L = WS::kCompact ? 0 : N.lb[so + first], U = N.ub[so + first];   // (compact: no lower bounds)
         int xw = xprev ? (int)xprev[first] : 0;   // warm start: the smallest earlier flow of the chain's arcs
         for (int i = 1; i < len; i++) {
             const int a = (int)(arcs[i] & 0xffffu);
-            L = max(L, (int)N.lb[so + a]);
+            if (!WS::kCompact) L = max(L, (int)N.lb[so + a]);
             U = min(U, (int)N.ub[so + a]);
             if (xprev) xw = min(xw, (int)xprev[a]);
         }
@@ -1155,8 +1186,8 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         return;
     }
 
-    // warm start: node imbalances of the initial flow (conservation rows only, in dec's space)
-    LDS int32_t *imb = (LDS int32_t *)W.dec;
+    // warm start: node imbalances of the initial flow (conservation rows only)
+    LDS int32_t *imb = W.imb;
     if (xprev) {
         for (int v = tid; v < n + 2; v += T) imb[v] = 0;
         B::sync();
@@ -1239,7 +1270,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
             for (int v = tid; v < n; v += T)
                 if (is_cons(N, v)) imb_tot += imb[v] > 0 ? imb[v] : -imb[v];
             imb_tot = B::all(imb_tot, [](int64_t x, int64_t y) { return x + y; }, W.red);
-            repaired = warm_repair<RG, WT, NW>(N, W, nct, nz, M, imb, imb_tot + 2 * (int64_t)nct + 8, warm_augs, why);
+            repaired = warm_repair<RG, WT, NW>(N, W, nct, nz, M, imb, imb_tot + 2 * (int64_t)nct + 8, warm_augs, why, twr);
 #ifdef SGUFP_SUB_VERIFY
             if (repaired) {   // debug build: the cold SSP below must reach the same objective
                 int64_t pw = 0;
@@ -1401,8 +1432,8 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
             const uint32_t ol = io.pc_ol[pcb + k];
             const GBL uint32_t *arcs = io.pc_arcs + pcb + (ol & 0xffffu);
             const int nl = (int)(ol >> 16);
-            ChainOut c = assemble_chain(N, W, arcs, nl, k, s, ray, (k == ray_chain) ? ray_p : -1,
-                                        (k == ray_chain) ? ray_q : -1, ok);
+            ChainOut c = assemble_chain(N, W, arcs, io.pc_rw + pcb + (ol & 0xffffu), nl, k, s, ray,
+                                        (k == ray_chain) ? ray_p : -1, (k == ray_chain) ? ray_q : -1, ok);
             rhs += c.rhs;
             dual += c.obj;
             if (save) {
@@ -1433,9 +1464,10 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
 #ifdef SGUFP_SUB_PHASES
     SUB_PH(4);
     if (tid == 0 && blockIdx.x % 2047 == 0)
-        printf("SUBPH warm=%d chains %llu flow %llu potentials %llu dual %llu (ticks)\n", xprev != nullptr,
-               (unsigned long long)(tph[1] - tph[0]), (unsigned long long)(tph[2] - tph[1]),
-               (unsigned long long)(tph[3] - tph[2]), (unsigned long long)(tph[4] - tph[3]));
+        printf("SUBPH warm=%d chains %llu flow %llu potentials %llu dual %llu (ticks) repair bf %llu aug %llu inv %llu chk %llu\n",
+               xprev != nullptr, (unsigned long long)(tph[1] - tph[0]), (unsigned long long)(tph[2] - tph[1]),
+               (unsigned long long)(tph[3] - tph[2]), (unsigned long long)(tph[4] - tph[3]),
+               (unsigned long long)twr[0], (unsigned long long)twr[1], (unsigned long long)twr[2], (unsigned long long)twr[3]);
 #endif
 }
 
@@ -1514,6 +1546,7 @@ __global__ void __launch_bounds__(kWave) k_sub_paths(SubNet N, SubIO io) {
                 const int b = i + 1 < len ? dec[a] : -1;
                 const int slot = b >= 0 ? slot_at(N, N.arc_layer[a], b) : -1;
                 io.pc_arcs[pcb + o + i] = (uint32_t)a | (uint32_t)(uint16_t)slot << 16;
+                io.pc_rw[pcb + o + i] = N.reward[a];
                 a = b;
             }
         }

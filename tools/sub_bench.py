@@ -55,6 +55,11 @@ def main():
               f"(types {np.bincount(typ + 1, minlength=3).tolist()}, status {np.bincount(st.ravel(), minlength=3).tolist()}, "
               f"obj sum {float(obj.sum()):.1f})", flush=True)
     eng.close()
+    import hashlib
+    h = hashlib.sha256()
+    for x in ref:
+        h.update(np.ascontiguousarray(x).tobytes())
+    print(f"digest {h.hexdigest()[:16]}")
 
 
 if __name__ == "__main__":
