@@ -148,6 +148,9 @@ struct SubLds {
     LDS int32_t *pred;      // [n+2] code of the tight in-arc << 15 | its tail (kNoPred: none)
     LDS uint16_t *plist;    // [n+2] arc codes of the augmenting path (sink to source)
     double GBL *coef;       // [n_slots] this (path, scenario)'s row of SubIO::coef (phase 5)
+    LDS int64_t *acc;       // [n_slots] phase 5's row in LDS (over the chain records) when
+    bool use_acc;           //     use_acc, else atomic adds straight into coef (a flag: LDS
+                            //     address 0 is the null pointer of that address space)
     LDS int32_t *zlist;     // [nz] free-supply / free-demand nodes: v | src << 30 | snk << 29
     LDS int32_t *misc;      // [8] flags
     LDS int64_t *red;       // [8] cross-wave reduction slots (multi-wave workgroups)
@@ -906,8 +909,10 @@ struct ChainOut {
 
 template <class WS>
 __device__ __forceinline__ void add_coef(const WS &W, int s, int64_t v) {
-    // integral values far below 2^53: the sum is exact in any order
-    if (v != 0 && s >= 0) __hip_atomic_fetch_add(&W.coef[s], (double)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // integers (the row's doubles: values far below 2^53, so any summation order is exact)
+    if (v == 0 || s < 0) return;
+    if (W.use_acc) __hip_atomic_fetch_add(&W.acc[s], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else __hip_atomic_fetch_add(&W.coef[s], (double)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // slot of the root variable (layer, head(b)) for an out-arc b of the layer's V-bar node
 __device__ __forceinline__ int slot_at(const SubNet &N, int layer, int b) {
@@ -956,11 +961,9 @@ __device__ __forceinline__ int dec_of(const SubNet &N, const SubIO &io, int64_t 
 // phi, in the order of the closed forms below (all integers: any summation order is exact).
 template <class WS>
 __device__ __forceinline__ ChainOut assemble_chain(const SubNet &N, const WS &W, const GBL uint32_t *arcs,
-                                                   const GBL int32_t *rws, int nl, int k, int s, bool ray_mode,
+                                                   const GBL int32_t *rws, int nl, int t, int h, int s, bool ray_mode,
                                                    int ray_p, int ray_q, bool &ok) {
     ChainOut o{0, 0};
-    const uint64_t ca = W.ra(k);
-    const int t = ch_t(ca), h = ch_h(ca);
     const size_t so = (size_t)s * N.m;
     // the chain's arcs in order, arcs[0 .. nl) with their rewards rws (k_sub_paths): arc id,
     // coefficient slot of the pair with the next arc, u, l (0 in the compact kernels: no lower
@@ -1115,6 +1118,8 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
     W.pred = (LDS int32_t *)(smem + off[4]);
     W.plist = (LDS uint16_t *)(smem + off[8]);
     W.coef = io.coef + ((size_t)p * S + s) * N.n_slots;
+    W.acc = nullptr;
+    W.use_acc = false;
     W.zlist = (LDS int32_t *)(smem + off[6]);
     W.misc = (LDS int32_t *)(smem + off[7]);
     W.red = (LDS int64_t *)(smem + off[10]);
@@ -1177,8 +1182,17 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
     }
     first_bad = B::all(first_bad, [](int x, int y) { return x < y ? x : y; }, W.red);
     B::sync();
-    for (int v = tid; v < N.n_slots; v += T) W.coef[v] = 0.0;
-    __threadfence();   // zeros stored before any lane's atomic adds of phase 5
+    // phase 5 sums the cut row in LDS when it fits over the chain records (int64 per slot) and
+    // the chains' flows fit the predecessor / path / imbalance space (int16 per chain)
+#ifdef SGUFP_SUB_NO_LACC
+    const bool lacc = false;   // A/B: atomic adds into the HBM row
+#else
+    const bool lacc = (size_t)N.n_slots * 8 <= off[3] - off[1] && (size_t)nct * 2 <= off[5] - off[4];
+#endif
+    if (!lacc) {
+        for (int v = tid; v < N.n_slots; v += T) W.coef[v] = 0.0;
+        __threadfence();   // zeros stored before any lane's atomic adds of phase 5
+    }
     B::sync();
     if (W.misc[0]) {
         if (tid == 0) { io.status[b] = kSubError; io.obj[b] = 0; io.dual[b] = 0; io.rhs[b] = 0; }
@@ -1425,21 +1439,37 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
     // 5. dual solution / ray and the scenario's cut contribution
     int64_t rhs = 0, dual = 0;
     bool ok = true;
-    if (status != kSubError) {
+    const bool run5 = status != kSubError;
+    if (run5) {
         const bool ray = status == kSubInfeasible;
+        // the flows of the complete chains (the warm save) move out of the chain records, whose
+        // space then holds the LDS row; ends and arcs come from the path's lists
+        LDS int16_t *xk = (LDS int16_t *)(smem + off[4]);
+        if (lacc) {
+            if (save)
+                for (int k = tid; k < nct; k += T) {
+                    const uint64_t ca = W.ra(k);
+                    xk[k] = (ch_t(ca) >= 0 && ch_h(ca) >= 0) ? (int16_t)ch_x(W.rb(k)) : (int16_t)0;
+                }
+            B::sync();
+            W.acc = (LDS int64_t *)(smem + off[1]);
+            W.use_acc = true;
+            for (int v = tid; v < N.n_slots; v += T) W.acc[v] = 0;
+            B::sync();
+        }
         for (int k = tid; k < nct; k += T) {
             if (ray && ray_chain >= 0 && k != ray_chain) continue;   // (i)/(ii): only the bad chain
-            const uint32_t ol = io.pc_ol[pcb + k];
+            const uint32_t ol = io.pc_ol[pcb + k], th = io.pc_th[pcb + k];
             const GBL uint32_t *arcs = io.pc_arcs + pcb + (ol & 0xffffu);
             const int nl = (int)(ol >> 16);
-            ChainOut c = assemble_chain(N, W, arcs, io.pc_rw + pcb + (ol & 0xffffu), nl, k, s, ray,
+            const int t = (int16_t)(th & 0xffffu), h = (int16_t)(th >> 16);
+            ChainOut c = assemble_chain(N, W, arcs, io.pc_rw + pcb + (ol & 0xffffu), nl, t, h, s, ray,
                                         (k == ray_chain) ? ray_p : -1, (k == ray_chain) ? ray_q : -1, ok);
             rhs += c.rhs;
             dual += c.obj;
             if (save) {
-                const uint64_t ca = W.ra(k);
-                const int x = ch_x(W.rb(k));
-                if (x && ch_t(ca) >= 0 && ch_h(ca) >= 0)
+                const int x = lacc ? (int)xk[k] : ((t >= 0 && h >= 0) ? ch_x(W.rb(k)) : 0);
+                if (x)
                     for (int i = 0; i < nl; i++) xs[arcs[i] & 0xffffu] = (int16_t)x;
             }
         }
@@ -1455,6 +1485,8 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         if (!ok || (ray ? dual >= 0 : dual != primal)) { status = kSubError; err_site = ok ? 6 : 7; }
     }
     B::sync();
+    if (lacc)   // the row (zeros where phase 5 did not run)
+        for (int v = tid; v < N.n_slots; v += T) W.coef[v] = run5 ? (double)W.acc[v] : 0.0;
     if (tid == 0) {
         io.status[b] = status;
         io.obj[b] = (double)primal;
