@@ -25,6 +25,11 @@ timeout -k 10 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY 
     --output-format csv -d gpurun_out/${TAG}_bnbs_pmc_issue -o run -- python3 bench.py $BNBS --bnb-seconds 8 > gpurun_out/${TAG}_bnbs_pmc_issue.log 2>&1 || exit $?
 for d in bnbs_stats bnbs_pmc_issue; do stamp $d "bnb:C4:seed1:zero:heuristic128:batch1024"; done
 python3 tools/compact_pmc.py gpurun_out/${TAG}_bnbs_pmc_issue/*counter_collection.csv
+# the subproblem alone (C4 32 paths x 256 scenarios, cold): issue / LDS counters of k_sub_scenario
+timeout -k 10 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT \
+    --output-format csv -d gpurun_out/${TAG}_sub_pmc -o run -- python3 tools/sub_bench.py --cfg C4 --scenarios 256 --paths 32 --reps 3 > gpurun_out/${TAG}_sub_pmc.log 2>&1 || exit $?
+stamp sub_pmc "sub:C4:seed1:paths32:scenarios256:cold"
+python3 tools/compact_pmc.py gpurun_out/${TAG}_sub_pmc/*counter_collection.csv
 # the bench line reads profiles/: copy the fresh counters there on the box as well
-for d in stats pmc_fetch pmc_write pmc_issue bnbs_stats bnbs_pmc_issue; do rm -rf profiles/${TAG}_$d; cp -r gpurun_out/${TAG}_$d profiles/; done
+for d in stats pmc_fetch pmc_write pmc_issue bnbs_stats bnbs_pmc_issue sub_pmc; do rm -rf profiles/${TAG}_$d; cp -r gpurun_out/${TAG}_$d profiles/; done
 ls gpurun_out/${TAG}_bnbs_stats
