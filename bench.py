@@ -287,6 +287,35 @@ def bnb_profile_block(tag: str):
     return out
 
 
+def sub_profile_block(tag: str):
+    """Issue / LDS counters of the subproblem kernel alone (tools/sub_bench.py, C4 32 paths x 256
+    scenarios, cold: the bench's subproblem leg), from profiles/<tag>_sub_pmc when collected with
+    this very library; else None.  The pass counts per scenario of the B&B legs are in
+    profiles/<tag>_sub_pass_counts.txt."""
+    import csv
+    dp = os.path.join(ROOT, "profiles", f"{tag}_sub_pmc")
+    if profile_matches(dp) != "library":
+        return None
+    c = {}
+    for path in glob.glob(os.path.join(dp, "*counter_collection.csv")):
+        with open(path) as fh:
+            for r in csv.DictReader(fh):
+                if "k_sub_scenario" in r["Kernel_Name"]:
+                    c[r["Counter_Name"]] = c.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    wc = c.get("SQ_WAVE_CYCLES")
+    if not wc:
+        return None
+    insts = c.get("SQ_INSTS_VALU", 0.0) + c.get("SQ_INSTS_SALU", 0.0)
+    return {"source": f"profiles/{tag}_sub_pmc (rocprofv3 --pmc SQ_* of tools/sub_bench.py --cfg C4 --scenarios 256 "
+                      f"--paths 32 --reps 3, libsgufp_hip.so sha256 {lib_sha256()[:16]}; wave cycles in quad-cycles)",
+            "active_frac": round(c.get("SQ_ACTIVE_INST_ANY", 0.0) / wc, 4),
+            "wait_frac": round(c.get("SQ_WAIT_ANY", 0.0) / wc, 4),
+            "lds_active_frac": round(c.get("SQ_ACTIVE_INST_LDS", 0.0) / wc, 4),
+            "lds_bank_conflict_frac": round(c.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(1.0, c.get("SQ_ACTIVE_INST_LDS", 0.0)), 4),
+            "cycles_per_wave_instruction": round(4.0 * wc / max(1.0, insts), 2),
+            "pass_counts": f"profiles/{tag}_sub_pass_counts.txt"}
+
+
 def _native_comm(eng, world, rank):
     """The library's own RCCL communicator (shard.cpp) on this rank's context: the id made on
     rank 0 reaches the others through a gloo side group (plain bytes)."""
@@ -624,6 +653,7 @@ def main():
     if sub is not None:
         sub.pop("_paths", None)
         sub.pop("_inst0", None)
+        sub["counters"] = sub_profile_block(args.profile_tag)
     eng.close()
     if rank == 0 and world == 1 and args.bnb_leg_seconds > 0:
         # BASELINE metric with the subproblems in the loop: the device B&B on the same
