@@ -647,14 +647,13 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
                 deferred.swap(fresh);    // their current path is unseen: solved when resumed
                 break;
             }
-            // With a round deadline, one iteration solves at most kChunkLps scenario LPs
+            // With a round deadline, one iteration solves at most chunk_lps scenario LPs
             // (a 1024-leaf iteration of the 512-scenario C5 network would take minutes); the
             // other fresh records stay in the loop unchanged (path not yet seen) for the next
             // iteration, or are deferred at the deadline.
             std::vector<int> rest;
             if (ctx->bnb_seconds > 0) {
-                constexpr int64_t kChunkLps = 16384;
-                const size_t chunk = (size_t)std::max<int64_t>(1, kChunkLps / std::max(1, ctx->net.S));
+                const size_t chunk = (size_t)std::max<int64_t>(1, ctx->chunk_lps / std::max(1, ctx->net.S));
                 if (fresh.size() > chunk) {
                     rest.assign(fresh.begin() + (long)chunk, fresh.end());
                     fresh.resize(chunk);

@@ -119,6 +119,7 @@ bool sgufp_ctx::init() {
     if (const char *e = getenv("SGUFP_SUB_WARM")) warm_on = atoi(e) != 0;   // warm-started subproblems (A/B)
     if (const char *e = getenv("SGUFP_EXACT_SCREEN")) exact_screen = std::max(0, std::min(kExactScreen, atoi(e)));
     if (const char *e = getenv("SGUFP_EXACT_LAZY")) exact_lazy = std::max(0, atoi(e));
+    if (const char *e = getenv("SGUFP_CHUNK_LPS")) chunk_lps = std::max(1, atoi(e));
     if (const char *e = getenv("SGUFP_NX")) nx_on = atoi(e) != 0;
     if (const char *e = getenv("SGUFP_SUB_STATS")) sub_stats = atoi(e) != 0;
     if (const char *e = getenv("SGUFP_NX_MIN")) nx_min = std::max(1, atoi(e));

@@ -143,6 +143,8 @@ struct sgufp_ctx {
     bool seen_upload(int slot, const std::vector<std::vector<int16_t>> &paths);
     bool seen_download(int slot, int count, std::vector<std::vector<int16_t>> &paths);
     int bnb_max_iters = 0;                    // refinement iterations per round (0: no limit)
+    int64_t chunk_lps = 32768;                // scenario LPs per refinement iteration under a round
+                                              // deadline (SGUFP_CHUNK_LPS)
     double bnb_seconds = 0.0;                 // refinement-loop seconds per round (0: no limit)
     bool relax_current(double optimal_lb);
     bool relax_order(BatchIn &in);
