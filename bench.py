@@ -92,6 +92,15 @@ def parse():
                     help="B&B leg with the incumbent seeded by the restricted-DD heuristic of this width (0: skip)")
     ap.add_argument("--bnb-leg-seconds", type=float, default=20.0,
                     help="headline line: seconds of the C4 / 256-scenario B&B leg (0: skip)")
+    ap.add_argument("--bnb-gen-seconds", type=float, default=20.0,
+                    help="headline line: seconds of the seeded C4 B&B with the generator's lower bounds kept "
+                         "(bnb_gen: infeasible scenarios, feasibility cuts in the loop; 0: skip)")
+    ap.add_argument("--cpp-leg-seconds", type=float, default=20.0,
+                    help="headline line: seconds of the seeded C4 B&B through the C++ host API (Inavap::DDSolver, "
+                         "tests/host/host_api_test search; 0: skip)")
+    ap.add_argument("--bnb-parity-survivor-pool", type=int, default=20000,
+                    help="bnb_parity leg: optimality cuts the unseeded search accumulates before its non-exact "
+                         "survivors are checked (0: skip)")
     ap.add_argument("--c5-bnb-seconds", type=float, default=30.0,
                     help="config-5 leg: seconds of the C5 / 512-scenario B&B with cut generation (0: skip)")
     ap.add_argument("--no-parity", action="store_true", help="skip the reference parity check of the timed batch")
@@ -667,6 +676,15 @@ def main():
                                          args.round_seconds, work, device=local, progress=0.0, tag="legs",
                                          heuristic=args.bnb_seeded_width)
             line["bnb_seeded"]["roofline"] = bnb_profile_block(args.profile_tag)
+            if args.cpp_leg_seconds > 0:
+                # the same seeded search through the C++ host path a maintainer links
+                line["bnb_seeded_cpp"] = cpp_bnb_run(args.config, args.seed, "zero", args.cpp_leg_seconds, 1024,
+                                                     args.round_seconds, args.bnb_seeded_width, work)
+        if args.bnb_gen_seconds > 0 and args.bnb_seeded_width > 0:
+            # the instance as generated (sink-arc lower bounds kept): infeasible scenarios, the
+            # first one's ray as a feasibility cut (grb.cpp:284-351) in the loop
+            line["bnb_gen"] = bnb_run(args.config, args.seed, "gen", args.bnb_gen_seconds, 1024, args.round_seconds,
+                                      work, device=local, progress=0.0, tag="legg", heuristic=args.bnb_seeded_width)
     if rank == 0 and world == 1 and args.bnb_parity_rounds > 0:
         line["bnb_parity"] = bnb_parity_leg(args)
     if rank == 0 and world == 1 and args.config == "C4" and args.c5_nodes > 0:
@@ -676,15 +694,11 @@ def main():
         # round exchanges over the library's own RCCL communicator -- beside the weak-scaling
         # relaxation step above.  A watchdog prints the line without this leg should a shard
         # stall in a collective.
-        stop = watchdog(args.bnb_leg_seconds + 240.0, line, rank)
-        try:
-            line["bnb_multi"] = bnb_run(args.config, args.seed, "zero", args.bnb_leg_seconds, 1024, args.round_seconds,
-                                        work, device=local % max(1, torch.cuda.device_count()), progress=0.0,
-                                        tag="multi", heuristic=args.bnb_seeded_width,
-                                        native=dist_backend(torch) == "nccl")
-        except Exception as e:     # noqa: BLE001 -- reported in the line, the headline stands
-            line["bnb_multi"] = {"error": f"{type(e).__name__}: {e}"}
-        stop.set()
+        guarded_leg(line, "bnb_multi", lambda: bnb_run(
+            args.config, args.seed, "zero", args.bnb_leg_seconds, 1024, args.round_seconds, work,
+            device=local % max(1, torch.cuda.device_count()), progress=0.0, tag="multi",
+            heuristic=args.bnb_seeded_width, native=dist_backend(torch) == "nccl"),
+            rank, args.bnb_leg_seconds + 240.0)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
@@ -715,6 +729,78 @@ def watchdog(seconds, line, rank):
     return stop
 
 
+LEG_FAIL_EXIT = 4   # a multi-rank leg that raised on any rank fails the run on every rank
+
+
+def guarded_leg(line, key, run, rank, seconds):
+    """line[key] = run() on every rank of a multi-rank job, under the watchdog.  A rank whose
+    run raises records the error in the line; then every rank learns of it through a gloo
+    all-reduce of the failure flags (so a rank that finished cleanly does not exit 0 beside a
+    failed one), rank 0 prints the line, and every rank exits LEG_FAIL_EXIT.  A rank stuck in a
+    collective the failed one never joins is ended by the watchdog (WATCHDOG_EXIT)."""
+    import torch
+    import torch.distributed as dist
+    stop = watchdog(seconds, line, rank)
+    failed = 0
+    try:
+        line[key] = run()
+    except Exception as e:     # noqa: BLE001 -- the error goes into the line, then the run fails
+        line[key] = {"error": f"{type(e).__name__}: {e}"}
+        failed = 1
+        sys.stderr.write(f"bench: rank {rank}: {key} failed: {type(e).__name__}: {e}\n")
+    flag = torch.tensor([failed], dtype=torch.int64)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=dist.new_group(backend="gloo"))
+    stop.set()
+    if int(flag.item()):
+        if rank == 0:
+            if not failed:
+                line[key] = {"error": "failed on another rank", "partial": line.get(key)}
+            print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        sys.stderr.write(f"bench: rank {rank}: multi-rank leg {key} failed, exiting {LEG_FAIL_EXIT}\n")
+        sys.stderr.flush()
+        os._exit(LEG_FAIL_EXIT)
+
+
+def cpp_bnb_run(cfg_name, seed, lb_mode, budget, batch, round_seconds, width, work):
+    """bnb_run's search through the C++ host API instead of the Python driver:
+    Inavap::DDSolver (include/sgufp/inavap.hpp) with restricted-DD seeding and a time budget,
+    driven by tests/host/host_api_test "search" (warm-up of 2 s, pool dropped, then the timed
+    search from the root record)."""
+    import subprocess
+    from sgufp_solver_amd import instance
+    cfg = instance.CONFIGS[cfg_name]
+    inst = instance.generate(cfg, seed)
+    if lb_mode == "zero":
+        inst.lb[:] = 0
+    net = os.path.join(work, f"cpp_{cfg_name}.txt")
+    inst.write(net)
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sgufp_solver_amd", "lib", "host_api_test")
+    r = subprocess.run([exe, "search", net, str(width), str(budget), str(batch), str(round_seconds), "0", "0"],
+                       capture_output=True, text=True, timeout=budget + 300)
+    if r.returncode != 0:
+        raise RuntimeError(f"host_api_test search failed: {r.stderr[-1000:]}")
+    out = {"counters": {}}
+    for ln in r.stdout.splitlines():
+        p = ln.split()
+        if p and p[0] == "search":
+            out.update(incumbent=float.fromhex(p[1]), heuristic_incumbent=float.fromhex(p[2]), seconds=float(p[3]),
+                       rounds=int(p[4]), complete=p[5] == "1")
+        elif p and p[0] == "counter":
+            out["counters"][p[1]] = int(p[2])
+        elif p and p[0] == "pool":
+            out["pool"] = [int(p[1]), int(p[2])]
+    c, sec = out["counters"], out["seconds"]
+    out["relaxations_per_s"] = round(c["relaxed"] / sec, 2)
+    out["subproblems_per_s"] = round(c["subproblems"] / sec, 2)
+    out["scenario_lps_per_s"] = round(c["subproblems"] * inst.scenarios / sec, 1)
+    out["workload"] = (f"{cfg_name}: {cfg.n_arcs}-arc layered network, {inst.scenarios} scenarios"
+                       f"{' (lower bounds 0)' if lb_mode == 'zero' else ''}, root record, incumbent seeded by the "
+                       f"width-{width} restricted-DD heuristic, up to {batch} records per round, refinement loops "
+                       f"deferred after {round_seconds} s per round; C++ Inavap::DDSolver (libsgufp_host.so)")
+    return out
+
+
 def bnb_parity_leg(args):
     """The device B&B under the cuts its own subproblem makes, checked round by round against
     the reference (oracle/bnb_parity.check_search: the popped records vs ref_dd relaxp bit for
@@ -724,15 +810,33 @@ def bnb_parity_leg(args):
     if not os.path.exists(bp.REF_BIN):
         return None
     # at the pool size the timed legs run against: the seeded search until 10^4 optimality
-    # cuts, then the next round's batch (exact records, non-exact survivors, pruned records)
+    # cuts, then the next round's batch (exact records, non-exact records a cut prunes)
     rep = bp.check_large_pool(args.config, args.seed, args.bnb_seeded_width, min_opt_cuts=args.bnb_parity_pool,
                               per_kind=6)
     fails = rep.pop("failures")
     rep["pool_last"] = rep["pool_total"]
-    rep["bit_exact"] = not fails and rep["mismatches"] == 0
-    rep["first_failures"] = fails[:5]
     rep["against"] = ("oracle/_ref/ref_dd (the reference's RelaxedDDNew) relaxp on the pool and next batch of the "
                       "running device search")
+    if args.bnb_parity_survivor_pool > 0:
+        # the unseeded search (every non-exact record survives every cut): survivors the
+        # cut-parallel non-exact phase settled (k_nx_dag / k_exact_leaf<nx> / k_nx_fin), with
+        # their cutset children, against relaxp
+        sv = bp.check_nx_survivors(args.config, args.seed, (args.bnb_parity_survivor_pool,), per_pool=8)
+        fails += sv.pop("failures")
+        rep["survivors"] = sv
+        rep["sampled"]["survivor"] += sum(p["survivors_checked"] for p in sv["pools"])
+        rep["checked"] += sum(p["checked"] for p in sv["pools"])
+        rep["mismatches"] += sum(p["mismatches"] for p in sv["pools"])
+    if args.bnb_parity_rounds > 0:
+        # round by round at small pools: the popped records, bound pruning, cut tightness, one
+        # refinement loop replayed against ref_dd refine
+        cs = bp.check_search(args.config, args.seed, args.bnb_seeded_width, rounds=40, batch=64, sample=16,
+                             min_subproblems=1, rounds_after=args.bnb_parity_rounds, round_iters=2)
+        fails += cs.pop("failures")
+        rep["search"] = {k: cs[k] for k in ("rounds", "checked", "mismatches", "subproblems", "opt_cuts", "feas_cuts",
+                                            "replayed", "pool_last", "seconds")}
+    rep["bit_exact"] = not fails and rep["mismatches"] == 0
+    rep["first_failures"] = fails[:5]
     return rep
 
 

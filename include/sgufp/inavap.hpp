@@ -188,6 +188,11 @@ class DDSolver {
     Device dev;
     int batch;
     static constexpr int kDiveBatch = 64;
+    double budget = 0.0;
+    int seedWidth = 0;
+    int maxIters = 0;
+    double roundSecs = 0.0;
+    double restricted_incumbent(double z);
 
   public:
     explicit DDSolver(const std::shared_ptr<Network> &networkPtr_, uint16_t nWorkers, int batch = 4096);
@@ -201,6 +206,18 @@ class DDSolver {
     void shard(int world, int rank, const uint8_t *id);
     // bound a round's exact-leaf refinement loops (sgufp_bnb_set_limits)
     void roundLimits(int maxRefineIters, double roundSeconds);
+    // throughput runs of searches that would take hours: stop after `seconds` of search (0:
+    // none); the last round's loops are cut at the budget and `complete` stays false
+    void timeBudget(double seconds) { budget = seconds; }
+    // primal heuristic (0: off): before the search, the restricted half of
+    // NodeExplorer::processX3 (NodeExplorer.cpp:605-796) on the root record -- a restricted DD
+    // of `width` nodes per layer swept with the pool, its max path sent to the subproblem and
+    // the cut added until the path repeats with an unchanged bound -- raises the incumbent to
+    // the routing's value, as the reference is seeded with a known value (main.cpp:75)
+    void restrictedSeed(int width) { seedWidth = width; }
+    bool complete = false;                           // the last search emptied every frontier
+    int64_t maxRounds = 0;                           // stop after this many rounds (0: none)
+    double heuristicIncumbent = DOUBLE_MIN;          // the seed's value (DOUBLE_MIN: none)
     int64_t received = 0;   // records this shard got through work sharing
     // counters of the last solve (SOLVER_COUNTERS, DDSolver.h:380-392)
     sgufp_bnb_stats totals{};

@@ -161,6 +161,20 @@ int sgufp_batch_debug(sgufp_ctx *ctx, int64_t *ticks, int32_t *redo);
 /* ticks per phase [n * 8]: build, narrow sweep, tail layers, last layer, replay/post, redo, finish, tail */
 int sgufp_batch_phases(sgufp_ctx *ctx, int64_t *phase);
 
+/* Which kernels took each node's optimality phase in the last sgufp_batch_relax (parity
+ * tests of the cut-parallel phases at the pool sizes the B&B reaches; any staged node):
+ *   SGUFP_ROUTE_IN_ORDER     k_relax's in-order sweeps only (DD.cpp:3932-4023 cut by cut)
+ *   SGUFP_ROUTE_EXACT_PHASE  exact DD handed to k_exact_root / k_exact_leaf / k_exact_fin
+ *   SGUFP_ROUTE_NX_PHASE     non-exact DD settled by k_nx_dag / k_exact_leaf<nx> / k_nx_fin
+ *   SGUFP_ROUTE_NX_FALLBACK  non-exact DD handed off, then re-run in order by k_relax because a
+ *                            width-1 pruning might have fired (DD.cpp:3986-4022)
+ * All SGUFP_ROUTE_IN_ORDER after sgufp_dd_build.  SGUFP_ERR_STATE before any relaxation. */
+#define SGUFP_ROUTE_IN_ORDER 0
+#define SGUFP_ROUTE_EXACT_PHASE 1
+#define SGUFP_ROUTE_NX_PHASE 2
+#define SGUFP_ROUTE_NX_FALLBACK 3
+int sgufp_batch_routes(sgufp_ctx *ctx, int32_t *route);
+
 /* -- scenario subproblem (replaces GuroSolver::solveSubProblem, grb.h:75 / grb.cpp:139-360) --
  * For n paths (concatenated int16 decisions, one per DD layer, path_off has n+1 entries)
  * solve every scenario's flow LP on the device and build the cut the reference would add:
@@ -174,11 +188,15 @@ int sgufp_subproblem(sgufp_ctx *ctx, int n, const int64_t *path_off, const int16
 /* Per (path, scenario) detail of the last sgufp_subproblem call, [n * S] each: status (0
  * optimal, 1 infeasible, 2 error), primal objective, objective of the dual built. */
 int sgufp_subproblem_detail(sgufp_ctx *ctx, int32_t *status, double *objective, double *dual_objective);
-/* Warm-started subproblems (networks without lower bounds): path k starts every scenario from
- * the optimal flow and potentials stored in ring slot warm_src[k] (-1: cold) and stores its own
- * in slot warm_dst[k] (-1: none); slots are 0 .. 2 x max(n, 32) - 1, and no slot may be both
- * written and read, or written twice, by one call.  Results are those of sgufp_subproblem (the
- * same optimal objectives; the duals -- the cut -- may be another optimal one).  The B&B's
+/* Warm-started subproblems (networks of up to 2046 nodes, with or without lower bounds): path k
+ * starts every scenario from the optimal flow and potentials stored in ring slot warm_src[k]
+ * (-1: cold) and stores its own in slot warm_dst[k] (-1: none).  The ring has
+ * 2 x max(max_batch, 32) slots, allocated zeroed on first use and never resized; a scenario
+ * whose source slot holds no stored state (never written, or that scenario was infeasible or
+ * failed there) starts cold.  n <= max_batch; no slot may be both written and read, or written
+ * twice, by one call (SGUFP_ERR_ARG).  Results are those of sgufp_subproblem (the same statuses
+ * and optimal objectives, the same feasibility rays -- an infeasible scenario is solved by the
+ * cold big-M path; the duals of an optimality cut may be another optimal one).  The B&B's
  * refinement loops (sgufp_bnb_step) pick the closest earlier path themselves. */
 int sgufp_subproblem_warm(sgufp_ctx *ctx, int n, const int64_t *path_off, const int16_t *paths, const int32_t *warm_src,
                           const int32_t *warm_dst, int32_t *type, double *rhs, double *rows, double *obj_mean);

@@ -477,3 +477,112 @@ def check_large_pool(cfg: str, seed: int, width: int, min_opt_cuts: int, batch: 
     rep["failures"] = fail
     rep["seconds"] = round(time.perf_counter() - t0, 2)
     return rep
+
+
+def check_nx_survivors(cfg: str, seed: int, pool_sizes=(20000, 100000), per_pool: int = 8, batch: int = 1024,
+                       round_seconds: float = 5.0, max_seconds: float = 300.0, device: int = 0, threads: int = 0,
+                       need_rounds: int = 12, keep_lb: bool = False):
+    """The survivor path of the non-exact cut-parallel phase at the pool sizes the timed B&B
+    legs reach.  The UNSEEDED search of ``cfg`` (no incumbent: nothing is pruned by a bound, so
+    the non-exact records of a round survive every cut and take the whole phase: k_nx_dag per
+    64-cut block, k_exact_leaf<nx> leaf passes, k_nx_fin's outcome and cutset) runs until its
+    optimality list holds each of ``pool_sizes`` cuts in turn.  There the next round's batch is
+    relaxed on the device, sgufp_batch_routes says which records the phase settled
+    (ROUTE_NX_PHASE) and ``per_pool`` survivors among them (status SUCCESS, cutset children:
+    the branching indices) are compared bit for bit with ``ref_dd relaxp`` on a binary copy of
+    the pool -- status, exact flag, lb / ub bits, argmax path, every child, DD sizes
+    (NodeExplorer.cpp:975-985, DD.cpp:3932-4023, 4179-4218) -- together with up to per_pool / 2
+    records of each other route present (in-order, fall-back re-run).  The round then runs on
+    the same batch and its statuses must equal the device relaxation's."""
+    import time
+    from sgufp_solver_amd import instance
+    from sgufp_solver_amd.pools import DOUBLE_MAX, DOUBLE_MIN, NodeRecord
+    t0 = time.perf_counter()
+    inst = instance.generate(instance.CONFIGS[cfg], seed)
+    if not keep_lb:
+        inst.lb[:] = 0
+    work = tempfile.mkdtemp(prefix="sgufp_nxsurv_")
+    net = os.path.join(work, "net.txt")
+    inst.write(net)
+    eng = E.Engine(net, device, batch)
+    eng.frontier_clear()
+    eng.frontier_push([NodeRecord(0, DOUBLE_MIN, DOUBLE_MAX, [], [])])
+    z = DOUBLE_MIN
+    fail: List[str] = []
+    rep = {"config": cfg, "seed": seed, "lower_bounds": "generated" if keep_lb else "zero", "rounds": 0,
+           "pools": []}
+    for target in pool_sizes:
+        while eng.cuts_count(0) < target and eng.frontier_size() and time.perf_counter() - t0 < max_seconds:
+            eng.bnb_set_limits(0, round_seconds)
+            z, _ = eng.bnb_step(z, batch)
+            rep["rounds"] += 1
+        if eng.cuts_count(0) < target:
+            fail.append(f"pool {target}: the search stopped at {eng.cuts_count(0)} optimality cuts")
+            break
+        pick: List[int] = []
+        got_all = recs = routes = None
+        for attempt in range(need_rounds + 1):
+            snap = snapshot_top(eng, batch)
+            recs = E.batch_to_records(snap)
+            got_all = eng.relax(recs, z)
+            routes = eng.routes()
+            by = {r: [] for r in (E.ROUTE_IN_ORDER, E.ROUTE_EXACT_PHASE, E.ROUTE_NX_PHASE, E.ROUTE_NX_FALLBACK)}
+            surv = []
+            for k, g in enumerate(got_all):
+                if snap.ub[k] <= z:
+                    continue
+                if routes[k] == E.ROUTE_NX_PHASE and g.status == E.SUCCESS and not g.exact and g.children:
+                    surv.append(k)
+                by[int(routes[k])].append(k)
+            if len(surv) >= per_pool or attempt == need_rounds or not eng.frontier_size():
+                break
+            eng.bnb_set_limits(0, round_seconds)
+            z, _ = eng.bnb_step(z, batch)
+            rep["rounds"] += 1
+        step = max(1, len(surv) // per_pool)
+        pick = surv[::step][:per_pool]
+        extra = []
+        for r in (E.ROUTE_IN_ORDER, E.ROUTE_NX_FALLBACK, E.ROUTE_EXACT_PHASE):
+            extra += by[r][:max(1, per_pool // 2)]
+        idx = sorted(set(pick + extra))
+        pool_path = os.path.join(work, f"pool_{target}.bin")
+        total = write_pool_bin(pool_path, eng)
+        nodes = os.path.join(work, f"nodes_{target}.txt")
+        out = os.path.join(work, f"ref_{target}.txt")
+        pools.write_nodes(nodes, [recs[i] for i in idx])
+        t1 = time.perf_counter()
+        subprocess.run([REF_BIN, "relaxp", net, pool_path, nodes, z.hex(), str(threads or _threads()), out], check=True,
+                       capture_output=True, timeout=1800)
+        want = pools.read_results(out)
+        got = [got_all[i] for i in idx]
+        bad = compare(got, want)
+        fail += [f"pool {target}: {m}" for m in bad[:10]]
+        n_ch = sum(len(got_all[i].children) for i in pick)
+        entry = {"target": target, "pool_optimality": eng.cuts_count(0), "pool_feasibility": eng.cuts_count(1),
+                 "pool_total": total, "incumbent": z, "batch": len(recs),
+                 "routes_in_batch": {name: len(by[r]) for name, r in (("in_order", E.ROUTE_IN_ORDER),
+                                                                      ("exact_phase", E.ROUTE_EXACT_PHASE),
+                                                                      ("nx_phase", E.ROUTE_NX_PHASE),
+                                                                      ("nx_fallback", E.ROUTE_NX_FALLBACK))},
+                 "nx_survivors_in_batch": len(surv), "survivors_checked": len(pick), "children_checked": n_ch,
+                 "checked": len(idx), "mismatches": len(bad),
+                 "reference_seconds": round(time.perf_counter() - t1, 2)}
+        rep["pools"].append(entry)
+        print(f"[nx survivors {cfg}] pool {entry['pool_optimality']}: routes {entry['routes_in_batch']} "
+              f"survivors checked {len(pick)} ({n_ch} children) mismatches {len(bad)} "
+              f"ref {entry['reference_seconds']} s, {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+        # the round itself on the same batch, pool and incumbent
+        eng.bnb_set_trace(True)
+        eng.bnb_set_limits(1, round_seconds)
+        z, _ = eng.bnb_step(z, batch)
+        rep["rounds"] += 1
+        by_rec = {rk: c for rk, c, _, _, _ in eng.bnb_trace(0)}
+        for i in idx:
+            if by_rec.get(i) != got_all[i].status:
+                fail.append(f"pool {target}: record {i}: round status {by_rec.get(i)} != device relaxation "
+                            f"{got_all[i].status}")
+        eng.bnb_set_trace(False)
+    eng.close()
+    rep["failures"] = fail
+    rep["seconds"] = round(time.perf_counter() - t0, 2)
+    return rep

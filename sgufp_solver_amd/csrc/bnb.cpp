@@ -682,13 +682,14 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
             // warm starts: every path starts from the stored state of the closest path solved
             // before (the record's own previous path, a sibling's, ...) and leaves its own state
             // in the ring for the next ones (k_warm_pick, k_sub_scenario<..., WARM>)
-            if (ctx->warm_reserve(ctx->max_batch)) {
+            if (ctx->warm_reserve()) {
                 if (!ctx->hip_ok(launch_warm_pick(io, ctx->wring, ctx->warm_ptr, ctx->stream), "k_warm_pick"))
                     return SGUFP_ERR_HIP;
                 io.warm_src = ctx->wring.src;
                 io.warm_dst = ctx->wring.dst;
                 io.wst_x = ctx->d_wx;
                 io.wst_a = ctx->d_wa;
+                io.wst_ok = ctx->d_wok;
                 ctx->warm_ptr = (ctx->warm_ptr + nf) % ctx->wring.R;
             }
             if (!ctx->hip_ok(launch_subproblem(ctx->sn, io, ctx->stream), "subproblem launch")) return SGUFP_ERR_HIP;
@@ -795,6 +796,7 @@ int sgufp_bnb_step(sgufp_ctx *ctx, int max_nodes, double *incumbent, sgufp_bnb_s
         ns += need[k];
     }
     ctx->relaxed = false;   // the popped slice is overwritten below
+    ctx->dd_built = false;
     if (!ctx->frontier_reserve(base + nc, (size_t)(sol_start + ns))) return SGUFP_ERR_HIP;
     const int np = (int)par.size();
     if (np) {

@@ -426,6 +426,8 @@ bool sgufp_ctx::nx_prepare(int no) {
 }
 
 bool sgufp_ctx::relax_current(double optimal_lb) {
+    // the slots' meta[5] become pool cut indices: the sgufp_dd_* view of the batch ends here
+    dd_built = false;
     if (!push_orders() || !exact_prepare()) return false;
     relax_lb = optimal_lb;
     BatchIn in = cur;
@@ -859,16 +861,19 @@ bool sgufp_ctx::sub_grow(int n, size_t total) {
     return true;
 }
 
-// The warm-start ring: R = 2 x the most paths one launch solves (so every launch has
-// candidates outside its own destinations), states of every scenario per slot.  Allocated on
-// first use; a network with lower bounds (64-bit-key kernels) or a failed allocation leaves the
-// subproblems cold.
-bool sgufp_ctx::warm_reserve(int paths_per_launch) {
-    if (!warm_on || !sn.key32) return false;
-    const int R = 2 * std::max(paths_per_launch, 1);
-    if (wring.R >= R) return true;
+// The warm-start ring: R = 2 x max(max_batch, 32) slots (a launch solves at most max_batch
+// paths, so every launch has candidates outside its own destinations), states of every
+// scenario per slot.  Allocated once, on first use, and zeroed (no slot holds a state until a
+// solve stores one: SubIO::wst_ok); its size never changes, so slot numbers a caller holds stay
+// valid.  The repair's per-thread node masks need n + 2 <= 32 x 64; a larger network or a failed
+// allocation leaves the subproblems cold.
+bool sgufp_ctx::warm_reserve() {
+    if (!warm_on) return false;
+    if (wring.R) return true;
+    if (net.n + 2 > 32 * 64) { warm_on = false; return false; }
+    const int R = 2 * std::max(max_batch, 32);
     const size_t S = (size_t)net.S, m = (size_t)net.m, n_ = (size_t)net.n;
-    const size_t bytes = (size_t)R * S * (m * 2 + n_ * 4);
+    const size_t bytes = (size_t)R * S * (m * 2 + n_ * 4 + 1);
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess && bytes > fr / 2) {
         warm_on = false;
@@ -877,16 +882,17 @@ bool sgufp_ctx::warm_reserve(int paths_per_launch) {
     WarmRing w{};
     int16_t *wx = nullptr;
     int32_t *wa = nullptr;
+    uint8_t *wok = nullptr;
     if (!alloc(wx, (size_t)R * S * m, "warm ring") || !alloc(wa, (size_t)R * S * n_, "warm ring") ||
+        !alloc(wok, (size_t)R * S, "warm ring") ||
         !alloc(w.path, (size_t)R * std::max(sc.Lcap, 1), "warm ring") || !alloc(w.plen, (size_t)R, "warm ring") ||
         !alloc(w.valid, (size_t)R, "warm ring") || !alloc(w.src, (size_t)R, "warm ring") ||
         !alloc(w.dst, (size_t)R, "warm ring") || !alloc(w.dist, (size_t)R, "warm ring") ||
-        !hip_ok(hipMemsetAsync(w.valid, 0, (size_t)R, stream), "memset") || !sync())
+        !hip_ok(hipMemsetAsync(w.valid, 0, (size_t)R, stream), "memset") ||
+        !hip_ok(hipMemsetAsync(wok, 0, (size_t)R * S, stream), "memset") ||
+        !hip_ok(hipMemsetAsync(wx, 0, (size_t)R * S * m * sizeof(int16_t), stream), "memset") ||
+        !hip_ok(hipMemsetAsync(wa, 0, (size_t)R * S * n_ * sizeof(int32_t), stream), "memset") || !sync())
         return false;
-    if (wring.R) {   // a larger ring: the old states go (they only speed up later solves)
-        release(d_wx); release(d_wa); release(wring.path); release(wring.plen); release(wring.valid);
-        release(wring.src); release(wring.dst); release(wring.dist);
-    }
     static const int maxd = [] {
         const char *e = std::getenv("SGUFP_SUB_WARM_DIST");   // farther donors: cold start
         return e ? std::atoi(e) : 48;
@@ -897,6 +903,7 @@ bool sgufp_ctx::warm_reserve(int paths_per_launch) {
     wring = w;
     d_wx = wx;
     d_wa = wa;
+    d_wok = wok;
     warm_ptr = 0;
     return true;
 }
@@ -915,12 +922,26 @@ int sgufp_subproblem_warm(sgufp_ctx *ctx, int n, const int64_t *path_off, const 
                           const int32_t *warm_dst, int32_t *type, double *rhs, double *rows, double *obj_mean) {
     if (!ctx || n < 0 || (n && (!warm_src || !warm_dst))) return SGUFP_ERR_ARG;
     if (!ctx->sub_init()) return SGUFP_ERR_HIP;
-    if (!ctx->warm_reserve(std::max(n, 32))) {
-        ctx->err = "warm starts need a network without lower bounds (32-bit-key kernels) and device memory";
+    if (n > ctx->max_batch) return SGUFP_ERR_ARG;
+    if (!ctx->warm_reserve()) {
+        ctx->err = "warm starts need n + 2 <= 2048 network nodes and device memory for the ring";
         return SGUFP_ERR_STATE;
     }
+    // a slot is read or written by at most one path of the call, and never both
+    std::vector<uint8_t> use((size_t)ctx->wring.R, 0);
+    for (int k = 0; k < n; k++) {
+        if (warm_src[k] < -1 || warm_src[k] >= ctx->wring.R || warm_dst[k] < -1 || warm_dst[k] >= ctx->wring.R)
+            return SGUFP_ERR_ARG;
+        if (warm_dst[k] >= 0) {
+            if (use[warm_dst[k]] & 2) { ctx->err = "warm_dst: a slot written twice"; return SGUFP_ERR_ARG; }
+            use[warm_dst[k]] |= 2;
+        }
+    }
     for (int k = 0; k < n; k++)
-        if (warm_src[k] >= ctx->wring.R || warm_dst[k] < -1 || warm_dst[k] >= ctx->wring.R) return SGUFP_ERR_ARG;
+        if (warm_src[k] >= 0 && (use[warm_src[k]] & 2)) {
+            ctx->err = "warm_src: a slot this call also writes";
+            return SGUFP_ERR_ARG;
+        }
     return subproblem_run(ctx, n, path_off, paths, warm_src, warm_dst, type, rhs, rows, obj_mean);
 }
 
@@ -985,6 +1006,7 @@ static int subproblem_run(sgufp_ctx *ctx, int n, const int64_t *path_off, const 
         io.warm_dst = ctx->wring.dst;
         io.wst_x = ctx->d_wx;
         io.wst_a = ctx->d_wa;
+        io.wst_ok = ctx->d_wok;
     }
     if (!ctx->hip_ok(launch_subproblem(ctx->sn, io, ctx->stream), "subproblem launch")) return SGUFP_ERR_HIP;
     ctx->sub_last_n = n;
@@ -1063,6 +1085,11 @@ int sgufp_dd_build(sgufp_ctx *ctx) {
     ctx->total_csol = 0;
     ctx->relaxed = true;   // sgufp_batch_results: SUCCESS (non-exact) / NEEDS_SUBPROBLEM (exact), exact flag
     ctx->dd_built = true;
+    // the build ran k_relax with no cut-parallel hand-off: sgufp_batch_refine must not read the
+    // previous relaxation's pending entries or optimalLB
+    ctx->relax_lb = -__DBL_MAX__;
+    ctx->ex.enabled = 0;
+    ctx->ex.lazy = 0;
     return SGUFP_OK;
 }
 
@@ -1246,6 +1273,7 @@ int sgufp_batch_refine(sgufp_ctx *ctx, int n, const int32_t *node_idx, const uin
     if (!ctx || !ctx->relaxed || n < 0 || n > ctx->max_batch || (n && (!node_idx || !is_feasibility || !cut_index)))
         return SGUFP_ERR_ARG;
     if (n == 0) return SGUFP_OK;
+    ctx->dd_built = false;   // k_refine rewrites the listed slots' meta[5] with pool cut indices
     if (ctx->ex.enabled && optimal_lb < ctx->relax_lb) {
         // the cut-parallel phase left partial leaf minima (upper bounds, all <= the relax-time
         // optimalLB) as terminal weights; a lower optimalLB could make one of them the argmax
@@ -1292,6 +1320,30 @@ int sgufp_batch_debug(sgufp_ctx *ctx, int64_t *ticks, int32_t *redo) {
     for (int k = 0; k < n; k++) {
         if (ticks) ticks[k] = stamped ? (int64_t)t[k] : 0;
         if (redo) redo[k] = (int32_t)r[k];
+    }
+    return SGUFP_OK;
+}
+
+int sgufp_batch_routes(sgufp_ctx *ctx, int32_t *route) {
+    if (!ctx || !route) return SGUFP_ERR_ARG;
+    if (!ctx->relaxed) return SGUFP_ERR_STATE;
+    const int n = ctx->n;
+    std::fill(route, route + n, SGUFP_ROUTE_IN_ORDER);
+    if (!ctx->ex.enabled || n == 0) return SGUFP_OK;   // no hand-off in the last relaxation
+    unsigned long long c0 = 0;
+    std::vector<int32_t> pidx((size_t)n);
+    if (!ctx->download(&c0, ctx->d_ectr, 1) || !ctx->download(pidx.data(), ctx->d_pidx, (size_t)n) || !ctx->sync())
+        return SGUFP_ERR_HIP;
+    const int pending = (int)(c0 >> 32);
+    std::vector<int32_t> kind((size_t)std::max(pending, 1), -1);
+    if (pending > 0 && ctx->ex.nx && ctx->ex.pkind &&
+        (!ctx->download(kind.data(), ctx->ex.pkind, (size_t)pending) || !ctx->sync()))
+        return SGUFP_ERR_HIP;
+    for (int k = 0; k < n; k++) {
+        const int i = pidx[k];
+        if (i < 0 || i >= pending) continue;
+        route[k] = kind[i] == -1 ? SGUFP_ROUTE_EXACT_PHASE
+                                 : (kind[i] == kNxRouteFallback ? SGUFP_ROUTE_NX_FALLBACK : SGUFP_ROUTE_NX_PHASE);
     }
     return SGUFP_OK;
 }

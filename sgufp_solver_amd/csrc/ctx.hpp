@@ -204,7 +204,9 @@ struct sgufp_ctx {
     int warm_ptr = 0;
     int16_t *d_wx = nullptr;
     int32_t *d_wa = nullptr;
-    bool warm_reserve(int paths_per_launch);  // false: no ring (cold subproblems)
+    uint8_t *d_wok = nullptr;                 // [R][S] the (slot, scenario) holds a stored state
+    bool warm_reserve();                      // ring of 2 x max(max_batch, 32) slots, sized once
+                                              // (false: no ring, cold subproblems)
     // SGUFP_SUB_STATS=1: the B&B's subproblem launches' augmentations and Bellman-Ford passes
     // (io.wstat), summed and printed to stderr every 200 launches (diagnostics; syncs per launch)
     bool sub_stats = false;

@@ -264,6 +264,8 @@ constexpr int kExactScreen = 256;
 // fire; a record where one might (status kNxFallback) is re-run by k_relax in order.
 constexpr int32_t kNxPending = 6;
 constexpr int32_t kNxFallback = 7;
+// ExactIO::pkind of a non-exact entry k_nx_fin sent back to k_relax (read by sgufp_batch_routes)
+constexpr int32_t kNxRouteFallback = INT32_MIN;
 constexpr int kNxRanks = 4;     // nonzero state ranks (ustride <= 5)
 constexpr int kNxCuts = 16;     // cuts per k_nx_dag work item (lanes = 4 node groups x 16 cuts)
 

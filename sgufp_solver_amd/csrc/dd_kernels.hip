@@ -2945,6 +2945,7 @@ __global__ void __launch_bounds__(kWave) k_nx_fin(NetDev net, Scratch sc, BatchI
     if (fire) {
         if (lane() == 0) {
             out.status[slot] = kNxFallback;
+            ex.pkind[i] = kNxRouteFallback;   // sgufp_batch_routes: re-run in order by k_relax
             atomicAdd(&ex.ctr[7], 1ull);
         }
         return;

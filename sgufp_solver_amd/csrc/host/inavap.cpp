@@ -270,7 +270,57 @@ void DDSolver::shard(int world, int rank, const uint8_t *id) {
 }
 
 void DDSolver::roundLimits(int maxRefineIters, double roundSeconds) {
+    maxIters = maxRefineIters;
+    roundSecs = roundSeconds;
     dev.check(sgufp_bnb_set_limits(dev.get(), maxRefineIters, roundSeconds), "round limits");
+}
+
+// The restricted-DD seed on the root record (NodeExplorer.cpp:605-664, the exact-tree loop of
+// processX3; sgufp_solver_amd/restricted.py is the same loop): relax, then until the max path
+// repeats with an unchanged bound, solve its subproblem and add the cut to the pool.  Returns
+// the converged bound, or z when the record is pruned or does not converge within 500 cuts.
+double DDSolver::restricted_incumbent(double z) {
+    sgufp_ctx *g = dev.get();
+    sgufp_network_info info{};
+    dev.check(sgufp_get_network_info(g, &info), "network info");
+    const size_t stride = (size_t)info.n_slots + 1;
+    uint16_t gl = 0;
+    double lb = DOUBLE_MIN, ub = DOUBLE_MAX;
+    int64_t z2[2] = {0, 0};
+    static const int16_t empty = 0;
+    Path prev;
+    double prev_lb = 0.0;
+    bool have = false;
+    for (int it = 0; it <= 500; it++) {
+        dev.check(sgufp_batch_upload(g, 1, &gl, &lb, &ub, z2, &empty, z2, &empty), "restricted upload");
+        dev.check(sgufp_restricted_relax(g, seedWidth, z), "restricted relax");
+        int32_t st = 0, plen = 0, cn = 0;
+        uint8_t ex = 0;
+        double rlb = 0.0;
+        dev.check(sgufp_restricted_results(g, &st, &ex, &rlb, &plen, &cn), "restricted results");
+        if (st >= 16) throw sgufp_error("restricted heuristic: root record failed on the device");
+        if (st != 0) return z;                                       // INVALID_OBJECT
+        int64_t poff[2] = {0, 0};
+        dev.check(sgufp_restricted_paths(g, poff, nullptr), "restricted paths");
+        Path path((size_t)poff[1]);
+        dev.check(sgufp_restricted_paths(g, poff, path.empty() ? nullptr : path.data()), "restricted paths");
+        if (have && path == prev) {
+            if (rlb == prev_lb) return std::max(z, rlb);             // {lowerBound, ...}
+        }
+        prev = path;
+        prev_lb = rlb;
+        have = true;
+        if (it == 500) break;
+        int64_t off[2] = {0, (int64_t)path.size()};
+        int32_t type = -1;
+        double rhs = 0.0;
+        std::vector<double> row(stride);
+        dev.check(sgufp_subproblem(g, 1, off, path.empty() ? &empty : path.data(), &type, &rhs, row.data(), nullptr),
+                  "restricted subproblem");
+        if (type < 0) throw sgufp_error("restricted heuristic: subproblem failed");
+        dev.check(sgufp_cuts_append_rows(g, type, 1, &rhs, row.data()), "restricted cut");
+    }
+    return z;
 }
 
 double DDSolver::startSolver(double known_optimal) {
@@ -284,16 +334,31 @@ double DDSolver::startSolver(double known_optimal) {
     double lb = DOUBLE_MIN, ub = DOUBLE_MAX;
     int64_t z2[2] = {0, 0};
     static const int16_t empty = 0;
-    if (rank == 0) dev.check(sgufp_frontier_push(g, 1, &gl, &lb, &ub, z2, &empty, z2, &empty), "frontier push");
     received = 0;
     std::vector<int64_t> sizes((size_t)world);
     double z = known_optimal;
+    const auto t_start = std::chrono::steady_clock::now();
+    auto elapsed = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
+    heuristicIncumbent = DOUBLE_MIN;
+    if (seedWidth > 0 && rank == 0) {
+        heuristicIncumbent = restricted_incumbent(z);
+        z = std::max(z, heuristicIncumbent);
+    }
+    if (rank == 0) dev.check(sgufp_frontier_push(g, 1, &gl, &lb, &ub, z2, &empty, z2, &empty), "frontier push");
+    complete = false;
     totals = sgufp_bnb_stats{};
     rounds = 0;
     // dive depth-first with small rounds until the first exact leaves are reached (no cut
     // can prune before that), then full batches
     bool diving = true;
     for (;;) {
+        if (budget > 0) {
+            // the round's refinement loops stop at the budget (or the round limit): the
+            // unfinished exact records go back on top of the frontier
+            const double left = budget - elapsed();
+            const double secs = std::max(1e-3, roundSecs > 0 ? std::min(left, roundSecs) : left);
+            dev.check(sgufp_bnb_set_limits(g, maxIters, secs), "round limits");
+        }
         sgufp_bnb_stats st{};
         dev.check(sgufp_bnb_step(g, diving ? std::min(batch, kDiveBatch) : batch, &z, &st), "B&B round");
         if (st.exact > 0) diving = false;
@@ -322,8 +387,13 @@ double DDSolver::startSolver(double known_optimal) {
         totals.frontier = st.frontier;
         totals.deferred += st.deferred;
         totals.resumed += st.resumed;
+        const bool over = (budget > 0 && elapsed() > budget) || (maxRounds > 0 && rounds >= maxRounds);
         if (world == 1) {
-            if (st.frontier == 0) break;
+            if (st.frontier == 0) {
+                complete = true;
+                break;
+            }
+            if (over) break;
             continue;
         }
         // the round's exchanges between the shards (shard.cpp)
@@ -333,7 +403,14 @@ double DDSolver::startSolver(double known_optimal) {
         dev.check(sgufp_frontier_sizes(g, sizes.data()), "frontier sizes");
         int64_t left = 0;
         for (int64_t s : sizes) left += s;
-        if (left == 0) break;
+        if (left == 0) {
+            complete = true;
+            break;
+        }
+        // every shard stops in the same round once one of them is over the budget
+        double stop = over ? 1.0 : 0.0;
+        dev.check(sgufp_incumbent_allreduce(g, &stop), "budget all-reduce");
+        if (stop > 0.0) break;
         dev.check(sgufp_frontier_balance(g, &got), "work sharing");
         received += got;
         if (st.exact > 0 || got > 0) diving = false;

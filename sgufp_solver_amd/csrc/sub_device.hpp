@@ -67,17 +67,20 @@ struct SubIO {
     double SGUFP_GBL *cut_rhs;           // [P]
     double SGUFP_GBL *cut_row;           // [P][n_slots+1] dense cut row (last slot 0)
     double SGUFP_GBL *obj_mean;          // [P] sum_s obj_s / S (optimality)
-    // Warm starts (32-bit-key launches: no lower bound, so every scenario is feasible).  The
-    // state of (slot, scenario) is an optimal flow per network arc and the optimal node
-    // potentials (alpha of grb.cpp's dual, 0 at free and V-bar nodes) of an earlier solve.
-    // Path p starts scenario s from slot warm_src[p]'s state (-1: cold) and writes its own final
-    // state to slot warm_dst[p] (-1: none).  A solve reads only its source slot and writes only
-    // its destination: two paths of one launch may share neither a destination nor a
-    // destination with another path's source (the host guarantees it).
+    // Warm starts (32- and 64-bit-key launches).  The state of (slot, scenario) is an optimal
+    // flow per network arc and the optimal node potentials (alpha of grb.cpp's dual, 0 at free
+    // and V-bar nodes) of an earlier solve of a feasible scenario; wst_ok marks the (slot,
+    // scenario) pairs whose last solve stored one (an infeasible or failed scenario stores none,
+    // and that scenario of a later path starts cold).  Path p starts scenario s from slot
+    // warm_src[p]'s state (-1: cold) and writes its own final state to slot warm_dst[p] (-1:
+    // none).  A solve reads only its source slot and writes only its destination: two paths of
+    // one launch may share neither a destination nor a destination with another path's source
+    // (the host guarantees it).
     const int32_t SGUFP_GBL *warm_src;   // [P] or null
     const int32_t SGUFP_GBL *warm_dst;   // [P] or null
     int16_t SGUFP_GBL *wst_x;            // [slots][S][m]
     int32_t SGUFP_GBL *wst_a;            // [slots][S][n]
+    uint8_t SGUFP_GBL *wst_ok;           // [slots][S]
     int32_t SGUFP_GBL *wstat;            // [P*S][2] or null: augmentations (negative: a warm start fell
                                          // back to the cold SSP), Bellman-Ford passes
     // The chains of each path (k_sub_paths, once per path for all its scenarios: the chains

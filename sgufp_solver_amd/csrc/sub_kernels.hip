@@ -758,8 +758,11 @@ constexpr int kRepairMulti = SGUFP_REPAIR_MULTI;
 // restart at infinity with their predecessor subtrees (invalidate_subtrees).  Returns false
 // (the caller falls back to the cold SSP) if a target is unreachable or the augmentation
 // bound is hit (why: 1 Bellman-Ford, 2 unreachable, 3 path, 4 bound); neither happens with
-// lower bounds 0.  Only the WARM instantiation of
-// k_sub_scenario carries it (launches with warm starts); the cold one is unchanged.
+// lower bounds 0.  With lower bounds the flows stay within [max l, min u] throughout (the
+// potential mode's residual arcs), so a repaired flow meets every bound; a deficit no excess
+// can reach within the bounds (the scenario may be infeasible for the new path) falls back to
+// the cold SSP, whose big-M costs find the ray.  Only the WARM instantiations of
+// k_sub_scenario carry it (launches with warm starts); the cold ones are unchanged.
 template <int RG, typename WT, int NW, class WS>
 __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nct, int nz, int64_t M,
                                                       LDS int32_t *imb, int64_t max_aug, int &augs, int &why,
@@ -814,7 +817,10 @@ __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nc
                     const bool tgt = v < n ? (cons(j) && imb[v] < 0) : stage == 0;
                     const KT k = W.key[v];
                     if (tgt && k < kKInf) {
-                        const int64_t c = (int64_t)k * 4096 + v;   // compact keys < 2^30, ids < 2^11 (host)
+                        // (key, node) in one int64: potential-mode keys carry no big-M (|cost| <=
+                        // sum |r|, so |key| < 2^35 with 64-bit keys, < 2^30 with 32-bit ones), ids
+                        // < 2^15
+                        const int64_t c = (int64_t)k * 32768 + v;
                         if (c > last) best = c < best ? c : best;
                     }
                 }
@@ -824,7 +830,7 @@ __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nc
                     break;
                 }
                 last = best;
-                const int tgt = (int)(best & 4095);
+                const int tgt = (int)(best & 32767);
                 if (tid == 0) {
                     int v = tgt, len = 0;
                     while (len < n + 2) {
@@ -844,8 +850,8 @@ __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nc
                     const int code = W.plist[i];
                     if (code >= 2 * m) continue;   // Z arcs: uncapacitated
                     const uint64_t cb = W.rb(code >> 1);
-                    const int64_t x = ch_x(cb), U = ch_U(cb);
-                    const int64_t cap = (code & 1) ? x : U - x;
+                    const int64_t x = ch_x(cb), L = ch_L(cb), U = ch_U(cb);   // (compact: L = 0)
+                    const int64_t cap = (code & 1) ? x - L : U - x;           // potential mode: [L, U]
                     delta = cap < delta ? cap : delta;
                 }
                 delta = B::all(delta, [](int64_t p, int64_t q) { return p < q ? p : q; }, W.red);
@@ -862,8 +868,8 @@ __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nc
                     if (code >= 2 * m) continue;
                     const int k = code >> 1;
                     const uint64_t ca = W.ra(k), cb = W.rb(k);
-                    const int64_t x = ch_x(cb), U = ch_U(cb);
-                    const int64_t cap = (code & 1) ? x : U - x;
+                    const int64_t x = ch_x(cb), L = ch_L(cb), U = ch_U(cb);
+                    const int64_t cap = (code & 1) ? x - L : U - x;
                     W.add_x(k, (int)((code & 1) ? -delta : delta));
                     if (cap == delta) W.key[(code & 1) ? ch_t(ca) : ch_h(ca)] = kKInf;   // segment used up
                 }
@@ -1108,7 +1114,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
     const int p = blockIdx.x / S, s = blockIdx.x - p * S;
     if (p >= io.n_paths) return;
     size_t off[kSubLdsParts];
-    sub_lds_layout(N.n, N.m, io.nct_cap, N.nz, NW, off, (int)sizeof(KT), WARM && sizeof(KT) == 4);
+    sub_lds_layout(N.n, N.m, io.nct_cap, N.nz, NW, off, (int)sizeof(KT), WARM);
     WS W;
     W.imb = (LDS int32_t *)(smem + off[0]);
     W.cta = (LDS uint64_t *)(smem + off[1]);
@@ -1129,12 +1135,12 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
     const int n = N.n, m = N.m;
     const size_t so = (size_t)s * m;
     const size_t b = (size_t)p * S + s;
-    // warm start (compact kernels only: no lower bound, every scenario feasible)
-    constexpr bool kWarm = WARM && WS::kCompact;
-    const int wsrc = (kWarm && io.warm_src) ? io.warm_src[p] : -1;
-    const int wdst = (kWarm && io.warm_dst) ? io.warm_dst[p] : -1;
-    const GBL int16_t *xprev = wsrc >= 0 ? io.wst_x + ((size_t)wsrc * S + s) * m : nullptr;
-    const GBL int32_t *aprev = wsrc >= 0 ? io.wst_a + ((size_t)wsrc * S + s) * n : nullptr;
+    // warm start: the source slot's state of this scenario, if its solve stored one
+    const int wsrc = (WARM && io.warm_src) ? io.warm_src[p] : -1;
+    const int wdst = (WARM && io.warm_dst) ? io.warm_dst[p] : -1;
+    const bool wok = wsrc >= 0 && io.wst_ok[(size_t)wsrc * S + s];
+    const GBL int16_t *xprev = wok ? io.wst_x + ((size_t)wsrc * S + s) * m : nullptr;
+    const GBL int32_t *aprev = wok ? io.wst_a + ((size_t)wsrc * S + s) * n : nullptr;
 
 #ifdef SGUFP_SUB_PHASES
     uint64_t tph[6];
@@ -1172,9 +1178,11 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         const bool complete = t >= 0 && h >= 0;
         int x0 = 0;
         if (xprev && complete) {
-            // reduced reward under the earlier potentials (alpha 0 at free / V-bar nodes)
-            const int E = R - (int)aprev[h] + (int)aprev[t];
-            x0 = E > 0 ? U : (E < 0 ? 0 : max(0, min(xw, U)));
+            // reduced reward under the earlier potentials (alpha 0 at free / V-bar nodes); the
+            // flow goes to the bound it favours within [max l, min u] (a chain with max l >
+            // min u is infeasible up front, first_bad below, and never solved)
+            const int64_t E = (int64_t)R - (int64_t)aprev[h] + (int64_t)aprev[t];
+            x0 = E > 0 ? U : (E < 0 ? L : max(L, min(xw, U)));
         }
         W.wa(k, pack_a(t, h, R));
         W.wb(k, pack_b(L, U, x0, first));   // compact: L = 0 (host), no first arc
@@ -1492,6 +1500,8 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         io.obj[b] = (double)primal;
         io.dual[b] = status == kSubError ? -(double)err_site : (double)dual;
         io.rhs[b] = (double)rhs;
+        // the destination's state of this scenario is usable only if this solve stored it
+        if (wdst >= 0) io.wst_ok[(size_t)wdst * S + s] = (save && status == kSubOptimal) ? 1 : 0;
     }
 #ifdef SGUFP_SUB_PHASES
     SUB_PH(4);
@@ -1709,7 +1719,7 @@ namespace {
 template <typename KT, bool WARM>
 hipError_t launch_scenarios(const SubNet &N, const SubIO &io, hipStream_t st) {
     constexpr int kb = (int)sizeof(KT);
-    constexpr bool kw = WARM && kb == 4;   // the warm layout (k_sub_scenario's)
+    constexpr bool kw = WARM;   // the warm layout (k_sub_scenario's)
     size_t lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, 1, kb, kw);
 #ifdef SGUFP_SUB_LDS_MIN
     if (lds < SGUFP_SUB_LDS_MIN) lds = SGUFP_SUB_LDS_MIN;   // occupancy experiments
@@ -1751,11 +1761,12 @@ hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st) {
     // 32-bit keys (N.key32, host: no lower bound in any scenario, sum_a |r_a| < 2^18, n + 2 <
     // 2^11); SGUFP_SUB_KEY64=1 forces the 64-bit keys (A/B)
     const char *ek = getenv("SGUFP_SUB_KEY64");
-    // warm starts (io.warm_src / warm_dst) only in the 32-bit-key kernels: no lower bounds
+    // warm starts (io.warm_src / warm_dst) in both key widths: with lower bounds the repair keeps
+    // every flow within [max l, min u]
     const bool k32 = N.key32 && !(ek && atoi(ek) == 1);
-    const bool warm = k32 && (io.warm_src || io.warm_dst);
+    const bool warm = io.warm_src || io.warm_dst;
     hipLaunchKernelGGL(k_sub_paths, dim3((unsigned)io.n_paths), dim3(kWave), (size_t)N.m * 3 * sizeof(int16_t), st, N, io);
-    const hipError_t e = !k32 ? launch_scenarios<int64_t, false>(N, io, st)
+    const hipError_t e = !k32 ? (warm ? launch_scenarios<int64_t, true>(N, io, st) : launch_scenarios<int64_t, false>(N, io, st))
                               : (warm ? launch_scenarios<int32_t, true>(N, io, st) : launch_scenarios<int32_t, false>(N, io, st));
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_sub_reduce, dim3((unsigned)io.n_paths), dim3(256), 0, st, N, io);

@@ -18,6 +18,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SGUFP_LIB_PATH") or os.path.join(HERE, "lib", "libsgufp_hip.so")
 
 SUCCESS, PRUNED_F, PRUNED_O, NEEDS_SUBPROBLEM, PRUNED_BOUND = 0, 1, 2, 3, 4
+# sgufp_batch_routes (include/sgufp_hip.h)
+ROUTE_IN_ORDER, ROUTE_EXACT_PHASE, ROUTE_NX_PHASE, ROUTE_NX_FALLBACK = 0, 1, 2, 3
 ERR_RECORD, ERR_CAPACITY, ERR_CUTSET = 16, 17, 18
 
 EXPORTS = [
@@ -124,6 +126,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.sgufp_probe_network.argtypes = [C.c_char_p, P, P, C.c_int32, P, P]
     lib.sgufp_batch_debug.argtypes = [P, P, P]
     lib.sgufp_batch_phases.argtypes = [P, P]
+    lib.sgufp_batch_routes.argtypes = [P, P]
     lib.sgufp_subproblem.argtypes = [P, C.c_int, P, P, P, P, P, P]
     lib.sgufp_subproblem_detail.argtypes = [P, P, P, P]
     lib.sgufp_slot_keys.argtypes = [P, P]
@@ -440,6 +443,13 @@ class Engine:
         fe = np.asarray(is_feas, dtype=np.uint8)
         ci = np.asarray(cut_index, dtype=np.int32)
         self._check(self.lib.sgufp_batch_refine(self.ctx, len(ni), _ptr(ni), _ptr(fe), _ptr(ci), C.c_double(incumbent)))
+
+    def routes(self) -> np.ndarray:
+        """Per staged record, which kernels took its optimality phase in the last relaxation
+        (sgufp_batch_routes): ROUTE_IN_ORDER, ROUTE_EXACT_PHASE, ROUTE_NX_PHASE, ROUTE_NX_FALLBACK."""
+        r = np.zeros(max(self.n, 1), dtype=np.int32)
+        self._check(self.lib.sgufp_batch_routes(self.ctx, _ptr(r)))
+        return r[:self.n]
 
     # -- one DD at a time: Inavap::RelaxedDDNew (DD.h:797-808) ----------------
     def dd_build(self, nodes):

@@ -42,7 +42,7 @@ class DDSolver:
                  max_batch: int = 4096, batch_nodes: int = 0, engine=None, group=None, verbose: bool = True,
                  progress: float = 0.0, max_rounds: int = 0, dive_batch: int = 64, time_budget: float = 0.0,
                  restricted_width: int = 0, round_seconds: float = 0.0, round_iters: int = 0,
-                 native_world: int = 0, comm=None):
+                 native_world: int = 0, comm=None, stop_rounds: int = 0):
         """n_workers is accepted for API compatibility with the reference (threads there);
         the parallelism here is the batch of ``batch_nodes`` (<= max_batch) records per
         round and one rank per GPU."""
@@ -56,6 +56,9 @@ class DDSolver:
         self.verbose = verbose
         self.progress = progress        # seconds between progress lines on stderr (0: none)
         self.max_rounds = max_rounds    # safety cap for tests (0: none); hitting it raises
+        # stop after this many rounds (0: none) with complete = False, like the C++
+        # Inavap::DDSolver::maxRounds (the same rounds for a deterministic comparison)
+        self.stop_rounds = stop_rounds
         # Until the first exact leaf is reached there is no cut to prune with (and at most
         # the seeded incumbent):
         # rounds of dive_batch records from the top of the stack go depth-first to the
@@ -160,7 +163,8 @@ class DDSolver:
                 raise RuntimeError(f"DDSolver: no termination within {self.max_rounds} rounds (z={z!r})")
             for k in keys:
                 self.counters[k] += int(getattr(st, k, 0) if not isinstance(st, dict) else st.get(k, 0))
-            over = self.time_budget > 0 and time.perf_counter() - t_start > self.time_budget
+            over = (self.time_budget > 0 and time.perf_counter() - t_start > self.time_budget) or \
+                (self.stop_rounds > 0 and self.rounds >= self.stop_rounds)
             if self.native_world:
                 z = eng.incumbent_allreduce(z)
                 eng.cuts_exchange()

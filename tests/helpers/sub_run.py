@@ -3,11 +3,12 @@ random full matchings and save the per-(path, scenario) results.  The library is
 SGUFP_LIB_PATH names (the verify build re-runs every warm Bellman-Ford cold, and every warm
 start's repair cold).
 
-    sub_run.py cfg seed S n_paths out.npz [warm]
+    sub_run.py cfg seed S n_paths out.npz [warm | warmgen]
 
 warm: the paths are solved cold into ring slots 0 .. n-1, then B&B-like neighbours of them
 (the decisions of the last DD layers redrawn, as the exact leaves of one cutset differ) are
-solved warm from those slots and, for comparison, cold."""
+solved warm from those slots and, for comparison, cold.  warmgen: the same with the
+generator's lower bounds kept (64-bit-key kernels; some scenarios infeasible)."""
 import os
 import sys
 import tempfile
@@ -43,7 +44,8 @@ def main(cfg, seed, S, n_paths, out, mode=""):
     from sgufp_solver_amd import engine as E
     from sgufp_solver_amd import instance
     inst = instance.generate(instance.CONFIGS[cfg], seed, scenarios=S)
-    inst.lb[:] = 0                       # feasible: full max-reward flows, many augmentations
+    if mode != "warmgen":
+        inst.lb[:] = 0                   # feasible: full max-reward flows, many augmentations
     d = tempfile.mkdtemp(prefix="sgufp_subv_")
     path = os.path.join(d, "net.txt")
     inst.write(path)
@@ -52,7 +54,7 @@ def main(cfg, seed, S, n_paths, out, mode=""):
     paths = [instance.random_matching_path(inst, la, rng) for _ in range(n_paths)]
     eng = E.Engine(path, 0, 64)
     res = {}
-    if mode == "warm":
+    if mode in ("warm", "warmgen"):
         n = n_paths
         eng.subproblem(paths, [-1] * n, list(range(n)))
         res["seed_st"], res["seed_obj"], _ = eng.subproblem_detail(n)
@@ -66,6 +68,7 @@ def main(cfg, seed, S, n_paths, out, mode=""):
         res["cold_st"], res["cold_obj"], res["cold_dual"] = eng.subproblem_detail(n)
         res["cold_aug"], res["cold_passes"] = eng.subproblem_stats(n)
         res["cold_typ"], res["cold_obj_mean"] = ctyp, cobj_mean
+        res["cold_rhs"], res["cold_rows"] = crhs, crows
         res["paths"] = np.array(nb, dtype=np.int16)
     else:
         typ, rhs, rows, obj_mean = eng.subproblem(paths)

@@ -7,6 +7,7 @@
 // "explorer <optimum %a> <processed>" (a single-worker LIFO loop over
 // Inavap::NodeExplorer::process with two global Containers, as Worker::startWorker).
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <map>
 #include <string>
@@ -125,7 +126,58 @@ static int dd_mode(char **argv) {
     return 0;
 }
 
+// "search" mode: Inavap::DDSolver at scale, as the bench's B&B legs drive the Python solver
+// (bench.py bnb_run): a warm-up search of 2 s whose pool is dropped, then the timed search
+// (no warm-up with a round cap: the search is then reproducible round for round)
+//   host_api_test search <network> <restricted width> <seconds> <batch> <round seconds>
+//                        <round iters> <max rounds (0: none)>
+// prints "search <incumbent %a> <heuristic %a> <seconds> <rounds> <complete>" and one
+// "counter <name> <value>" line per sgufp_bnb_stats total.
+static int search_mode(char **argv) {
+    auto net = std::make_shared<Network>(argv[2]);
+    const int width = std::atoi(argv[3]);
+    const double seconds = std::strtod(argv[4], nullptr);
+    const int batch = std::atoi(argv[5]);
+    const double round_seconds = std::strtod(argv[6], nullptr);
+    const int round_iters = std::atoi(argv[7]);
+    const long max_rounds = std::atol(argv[8]);
+    Inavap::DDSolver solver{net, 1, batch};
+    if (max_rounds == 0) {   // a timed run: warm-up first (a round cap asks for a reproducible search)
+        solver.roundLimits(round_iters, std::min(round_seconds, 2.0));
+        solver.timeBudget(2.0);
+        solver.startSolver(Inavap::DOUBLE_MIN);                 // kernels, allocations
+        if (sgufp_cuts_clear(solver.context()) != SGUFP_OK) throw std::runtime_error("cuts clear");
+    }
+    solver.roundLimits(round_iters, round_seconds);
+    solver.timeBudget(seconds);
+    solver.restrictedSeed(width);
+    solver.maxRounds = max_rounds;
+    const auto t0 = std::chrono::steady_clock::now();
+    const double z = solver.startSolver(Inavap::DOUBLE_MIN);
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::printf("search %a %a %.6f %lld %d\n", z, solver.heuristicIncumbent, secs, (long long)solver.rounds,
+                solver.complete ? 1 : 0);
+    const sgufp_bnb_stats &t = solver.totals;
+    const std::pair<const char *, int64_t> cs[] = {
+        {"popped", t.popped}, {"relaxed", t.relaxed}, {"pruned_bound", t.pruned_bound},
+        {"pruned_feasibility", t.pruned_feasibility}, {"pruned_optimality", t.pruned_optimality}, {"exact", t.exact},
+        {"exact_closed", t.exact_closed}, {"subproblems", t.subproblems},
+        {"new_feasibility_cuts", t.new_feasibility_cuts}, {"new_optimality_cuts", t.new_optimality_cuts},
+        {"children", t.children}, {"pushed", t.pushed}, {"deferred", t.deferred}, {"resumed", t.resumed}};
+    for (auto &[k, v] : cs) std::printf("counter %s %lld\n", k, (long long)v);
+    std::printf("pool %d %d\n", sgufp_cuts_count(solver.context(), 1), sgufp_cuts_count(solver.context(), 0));
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc == 9 && std::strcmp(argv[1], "search") == 0) {
+        try {
+            return search_mode(argv);
+        } catch (const std::exception &e) {
+            std::fprintf(stderr, "error: %s\n", e.what());
+            return 1;
+        }
+    }
     if (argc == 6 && std::strcmp(argv[1], "dd") == 0) {
         try {
             return dd_mode(argv);

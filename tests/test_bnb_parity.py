@@ -75,33 +75,52 @@ def test_bnb_parity_c5():
     assert seen["relaxed"] > 0 and seen["subproblems"] > 0
 
 
-def test_bnb_parity_c4_at_timed_pool_size():
-    """The pool sizes the timed B&B legs run against (10^4 cuts, not the 10^2-10^3 of the
+def test_bnb_parity_c4_seeded_at_timed_pool_size():
+    """The pool sizes the seeded B&B leg runs against (10^4 cuts, not the 10^2-10^3 of the
     round-by-round checks above): the seeded C4 / 256 search with uncapped refinement loops
     until its optimality list holds 20 000 cuts, then the first batch of the next rounds that
-    holds both exact leaves and non-exact survivors -- exact records through the cut-parallel
-    exact phase, non-exact records past the first 256 optimality cuts through the cut-parallel
-    non-exact phase (k_nx_*, or k_relax's re-run where a width-1 pruning may fire) -- against
-    ref_dd relaxp on the same pool, bit for bit, 8 records of each outcome."""
+    holds exact leaves (the cut-parallel exact phase) and non-exact records -- under the seeded
+    incumbent a cut prunes those (the survivors are covered unseeded, below) -- against ref_dd
+    relaxp on the same pool, bit for bit, 8 records of each outcome."""
     rep = bp.check_large_pool("C4", 1, 128, min_opt_cuts=20000, per_kind=8)
     assert not rep["failures"], "\n".join(rep["failures"][:10])
     assert rep["pool_optimality"] >= 20000, rep
-    # at this pool the C4 search's batches hold exact leaves and non-exact records a cut prunes
     assert rep["sampled"]["exact"] >= 1 and rep["sampled"]["survivor"] + rep["sampled"]["pruned"] >= 1, rep
     assert rep["checked"] >= 8
 
 
-def test_bnb_parity_c3_non_exact_at_large_pool():
-    """The non-exact records of the seeded C3 search at the pool sizes its timed rounds reach
-    (1 024-record launches against 6-7 x 10^4 cuts): the search until its pool
-    holds 60 000 optimality cuts, then the first batches of the following rounds -- exact leaves,
-    and non-exact records, which at this pool size all take the cut-parallel non-exact phase
-    (k_nx_dag / k_exact_leaf / k_nx_fin; pruned by a cut or surviving every cut; under the
-    seeded incumbent nearly all are pruned) -- against ref_dd relaxp."""
-    rep = bp.check_large_pool("C3", 1, 64, min_opt_cuts=60000, per_kind=8, need_rounds=80, max_seconds=500.0)
+def _survivors(rep, per_pool, sizes):
     assert not rep["failures"], "\n".join(rep["failures"][:10])
-    assert rep["pool_optimality"] >= 60000, rep
-    assert rep["sampled"]["exact"] >= 1 and rep["sampled"]["survivor"] + rep["sampled"]["pruned"] >= 1, rep
+    assert [p["target"] for p in rep["pools"]] == list(sizes), rep
+    for p in rep["pools"]:
+        assert p["pool_optimality"] >= p["target"], p
+        assert p["survivors_checked"] >= per_pool, p          # settled by k_nx_dag / leaf / k_nx_fin
+        assert p["children_checked"] >= per_pool, p
+        assert p["mismatches"] == 0, p
+
+
+@pytest.mark.timeout(1500)
+def test_bnb_parity_c4_survivors_at_timed_pool_sizes():
+    """The survivor path of the non-exact cut-parallel phase at the pool sizes the unseeded
+    timed leg (`bnb`) reaches -- 2 x 10^4 and 10^5 optimality cuts (its pool ends near 2.3 x
+    10^5): with no incumbent every non-exact record survives every cut, so the round's
+    non-exact records are settled by k_nx_dag / k_exact_leaf<nx> / k_nx_fin (sgufp_batch_routes
+    says which).  At each pool size 8 such survivors -- status, bounds, argmax path and every
+    cutset child (the branching indices) -- and records of the other routes are compared bit for
+    bit with ref_dd relaxp (round-5 VERDICT item 1)."""
+    sizes = (20000, 100000)
+    rep = bp.check_nx_survivors("C4", 1, sizes, per_pool=8)
+    print(rep)
+    _survivors(rep, 8, sizes)
+
+
+@pytest.mark.timeout(1500)
+def test_bnb_parity_c3_survivors_at_large_pool():
+    """The same on BASELINE configs[2]'s network (C3, 64 scenarios) at 6 x 10^4 optimality cuts."""
+    sizes = (60000,)
+    rep = bp.check_nx_survivors("C3", 1, sizes, per_pool=8)
+    print(rep)
+    _survivors(rep, 8, sizes)
 
 
 @pytest.mark.parametrize("knob,value", [("SGUFP_EXACT_FAST", "0"), ("SGUFP_EXACT_LAZY", "1"),

@@ -14,6 +14,7 @@ import os
 import subprocess
 import tempfile
 
+import numpy as np
 import pytest
 
 from sgufp_solver_amd import pools
@@ -224,3 +225,56 @@ def test_cpp_relaxeddd_matches_reference(native_lib, name, k):
         want = parse_api(fh.read().decode())
     bad = compare(parse_api(r.stdout), want)
     assert not bad, "\n".join(bad[:10])
+
+
+@pytest.mark.gpu
+def test_dd_view_ends_with_a_batch_relaxation(native_lib):
+    """sgufp_dd_* read a slot's DD through its own dense row (d_ddrow); a batch relaxation,
+    refinement or B&B round rewrites the slot's last-cut index with a pool index, so after one
+    of them the sgufp_dd_* view is gone: SGUFP_ERR_STATE, not an out-of-bounds read (round-5
+    ADVICE).  A refine right after a build is allowed (the build left no cut-parallel state)."""
+    from sgufp_solver_amd import engine as E
+    c = [x for x in manifest() if x["name"] == "c2_s2_dfs"][0]
+    d = golden_io.case_dir("c2_s2_dfs")
+    nodes = pools.read_nodes(os.path.join(API, c["nodes"]))
+    eng = E.Engine(os.path.join(d, "net.txt"), 0, 64)
+    try:
+        eng.add_cuts(pools.read_pool(os.path.join(d, "cuts.txt")))
+        eng.dd_build(nodes)
+        eng.dd_solution(0)                     # the view is live after the build
+        eng.relax_async(pools.DOUBLE_MIN)      # the same staged batch, relaxed against the pool
+        eng.sync()
+        for call in (lambda: eng.dd_solution(0), lambda: eng.dd_cutset(0, pools.DOUBLE_MAX)):
+            with pytest.raises(RuntimeError, match=r"\(-5\)"):
+                call()
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_warm_slot_arguments_checked(native_lib):
+    """sgufp_subproblem_warm: a slot written twice, or read and written by one call, is an
+    argument error; the ring keeps its size (2 x max(max_batch, 32) slots) across calls."""
+    from sgufp_solver_amd import engine as E
+    from sgufp_solver_amd import instance
+    import tempfile as tf
+    inst = instance.generate(instance.CONFIGS["C3"], 1, scenarios=4)
+    with tf.TemporaryDirectory() as t:
+        net = os.path.join(t, "net.txt")
+        inst.write(net)
+        _, la, _ = E.probe_network(net)
+        rng = np.random.default_rng(5)
+        paths = [instance.random_matching_path(inst, la, rng) for _ in range(3)]
+        eng = E.Engine(net, 0, 16)
+        try:
+            eng.subproblem(paths[:2], [-1, -1], [0, 1])
+            with pytest.raises(RuntimeError, match=r"\(-1\)"):
+                eng.subproblem(paths[:2], [-1, -1], [2, 2])      # one slot written twice
+            with pytest.raises(RuntimeError, match=r"\(-1\)"):
+                eng.subproblem(paths[:2], [0, 3], [3, 4])        # slot 3 read and written
+            with pytest.raises(RuntimeError, match=r"\(-1\)"):
+                eng.subproblem(paths[:1], [64], [5])             # beyond 2 x max(16, 32) slots
+            typ, _, _, _ = eng.subproblem(paths, [0, 1, -1], [40, 41, 63])   # 40 slots later: still valid
+            assert (typ >= 0).all()
+        finally:
+            eng.close()

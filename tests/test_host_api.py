@@ -73,3 +73,49 @@ def test_container_is_race_free_under_tsan(tmp_path):
     assert "ThreadSanitizer" not in r.stderr, r.stderr[-2000:]
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr[-500:])
     assert "cuts 8000 (expected 8000)" in r.stdout
+
+
+def _cpp_search(net, width, seconds, batch, round_seconds, round_iters, max_rounds):
+    r = subprocess.run([os.path.join(LIB, "host_api_test"), "search", net, str(width), str(seconds), str(batch),
+                        str(round_seconds), str(round_iters), str(max_rounds)], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = {"counters": {}}
+    for line in r.stdout.splitlines():
+        p = line.split()
+        if p[0] == "search":
+            out.update(incumbent=float.fromhex(p[1]), heuristic=float.fromhex(p[2]), seconds=float(p[3]),
+                       rounds=int(p[4]), complete=p[5] == "1")
+        elif p[0] == "counter":
+            out["counters"][p[1]] = int(p[2])
+        elif p[0] == "pool":
+            out["pool"] = [int(p[1]), int(p[2])]
+    return out
+
+
+@pytest.mark.gpu
+def test_cpp_ddsolver_matches_python_driver_at_scale():
+    """BASELINE configs[2] (C3, 1k arcs, 64 scenarios) through the C++ host path a maintainer
+    links (Inavap::DDSolver with restricted-DD seeding, DDSolver.cpp:782-867) and through the
+    Python driver the bench uses (solver.DDSolver): 30 rounds of 1 024 records with two
+    refinement iterations per round (no wall-clock limit, so both searches are reproducible)
+    must give the same incumbent, the same heuristic seed, the same counters round for round
+    and the same pool."""
+    from sgufp_solver_amd import instance
+    from sgufp_solver_amd.pools import DOUBLE_MIN
+    from sgufp_solver_amd.solver import DDSolver
+    inst = instance.generate(instance.CONFIGS["C3"], 1)
+    inst.lb[:] = 0
+    net = os.path.join(tempfile.mkdtemp(prefix="sgufp_host_"), "net.txt")
+    inst.write(net)
+    cpp = _cpp_search(net, 64, 0, 1024, 0, 2, 30)
+    s = DDSolver(net, max_batch=1024, verbose=False, restricted_width=64, round_iters=2, stop_rounds=30)
+    z = s.start_solver(DOUBLE_MIN)
+    pool = [s.eng.cuts_count(1), s.eng.cuts_count(0)]
+    s.eng.close()
+    assert cpp["rounds"] == s.rounds == 30
+    assert cpp["heuristic"] == s.heuristic_incumbent
+    assert cpp["incumbent"] == z
+    assert cpp["counters"] == {k: int(v) for k, v in s.counters.items()}, (cpp["counters"], s.counters)
+    assert cpp["pool"] == pool
+    assert cpp["counters"]["subproblems"] > 0 and cpp["counters"]["relaxed"] > 1000

@@ -62,3 +62,49 @@ def test_stalled_collective_exits_nonzero(tmp_path):
     rec = json.loads(lines[-1])
     assert "timed out" in rec["bnb_multi"]["error"]
     assert "not reached" not in outs[0][0] + outs[1][0]
+
+
+FAIL_SCRIPT = textwrap.dedent("""
+    import os, sys, time
+    sys.path.insert(0, {root!r})
+    import torch
+    import torch.distributed as dist
+    import bench
+    rank = int(os.environ["RANK"])
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    line = {{"metric": "test", "value": 1.0}}
+
+    def run():
+        if rank == 1:
+            raise RuntimeError("RCCL init failed (simulated)")
+        time.sleep(1.0)
+        return {{"relaxations_per_s": 1.0}}
+
+    bench.guarded_leg(line, "bnb_multi", run, rank, 60.0)
+    print("not reached", flush=True)
+""")
+
+
+def test_failed_multi_leg_fails_every_rank(tmp_path):
+    """bnb_multi raising on one rank (an RCCL init or collective error) must end the run with a
+    non-zero status on EVERY rank, rank 0 still printing the line with the error (round-5
+    VERDICT weak 5: the exception used to be stored in the line and the run exited 0)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    script = tmp_path / "fail.py"
+    script.write_text(FAIL_SCRIPT.format(root=ROOT))
+    port = _free_port()
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=120) for p in procs]
+    codes = [p.returncode for p in procs]
+    assert codes == [bench.LEG_FAIL_EXIT, bench.LEG_FAIL_EXIT], (codes, [o[1][-500:] for o in outs])
+    lines = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
+    assert lines, outs[0]
+    rec = json.loads(lines[-1])
+    assert "error" in rec["bnb_multi"]
+    assert "not reached" not in outs[0][0] + outs[1][0]
