@@ -186,7 +186,9 @@ int sgufp_batch_routes(sgufp_ctx *ctx, int32_t *route);
 int sgufp_subproblem(sgufp_ctx *ctx, int n, const int64_t *path_off, const int16_t *paths, int32_t *type,
                      double *rhs, double *rows, double *obj_mean);
 /* Per (path, scenario) detail of the last sgufp_subproblem call, [n * S] each: status (0
- * optimal, 1 infeasible, 2 error), primal objective, objective of the dual built. */
+ * optimal, 1 infeasible, 2 error, 3 not solved: an earlier scenario of the path is infeasible
+ * -- the reference stops at the first infeasible one, grb.cpp:284-351 -- which later scenarios
+ * stop depends on timing, the cut does not), primal objective, objective of the dual built. */
 int sgufp_subproblem_detail(sgufp_ctx *ctx, int32_t *status, double *objective, double *dual_objective);
 /* Warm-started subproblems (networks of up to 2046 nodes, with or without lower bounds): path k
  * starts every scenario from the optimal flow and potentials stored in ring slot warm_src[k]

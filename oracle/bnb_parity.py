@@ -193,9 +193,13 @@ def _cut_at(rhs: float, row, ijk, y) -> float:
 
 def check_search(cfg: str, seed: int, width: int, rounds: int, batch: int, sample: int, round_seconds: float = 5.0,
                  replay: bool = True, highs: bool = True, device: int = 0, min_subproblems: int = 0,
-                 rounds_after: int = 3, min_closed: int = 0, round_iters: int = 0):
+                 rounds_after: int = 3, min_closed: int = 0, round_iters: int = 0, keep_lb: bool = False,
+                 min_feas_cuts: int = 0):
     """Run the device B&B (sgufp_bnb_step, traced) on a seeded instance of ``cfg`` (lower
-    bounds 0) -- the incumbent seeded by the restricted-DD heuristic of ``width`` (0: none) --
+    bounds 0; keep_lb: the generator's sink-arc lower bounds, so that scenarios are infeasible
+    and the loop generates feasibility cuts, grb.cpp:284-351, applied with their cascade,
+    DD.cpp:3842-3930, 4025-4177) -- the incumbent seeded by the restricted-DD heuristic of
+    ``width`` (0: none) --
     and check every round against the reference.  The search dives (LIFO batches of ``batch``
     records) until at least ``min_subproblems`` subproblems and ``min_closed`` closed loops
     were seen, then runs ``rounds_after`` more rounds; ``rounds`` caps the total.  ``round_iters``
@@ -220,7 +224,8 @@ def check_search(cfg: str, seed: int, width: int, rounds: int, batch: int, sampl
     from sgufp_solver_amd.pools import DOUBLE_MAX, DOUBLE_MIN, NodeRecord
     t0 = time.perf_counter()
     inst = instance.generate(instance.CONFIGS[cfg], seed)
-    inst.lb[:] = 0                       # feasible scenarios: optimality cuts and incumbents
+    if not keep_lb:
+        inst.lb[:] = 0                   # feasible scenarios: optimality cuts and incumbents
     work = tempfile.mkdtemp(prefix="sgufp_bnbpar_")
     net = os.path.join(work, "net.txt")
     inst.write(net)
@@ -238,6 +243,7 @@ def check_search(cfg: str, seed: int, width: int, rounds: int, batch: int, sampl
     eng.frontier_push([root])
     fail: List[str] = []
     rep = {"config": cfg, "seed": seed, "scenarios": int(inst.scenarios), "heuristic_width": width,
+           "lower_bounds": "generated" if keep_lb else "zero",
            "rounds": 0, "batch": batch, "checked": 0, "mismatches": 0, "subproblems": 0, "opt_cuts": 0,
            "feas_cuts": 0, "closed": 0, "pruned_bound": 0, "relaxed": 0, "replayed": 0, "pool_last": 0,
            "incumbent_start": z, "highs_checked": 0}
@@ -249,7 +255,8 @@ def check_search(cfg: str, seed: int, width: int, rounds: int, batch: int, sampl
     for r in range(rounds):
         if eng.frontier_size() == 0:
             break
-        if after is None and rep["subproblems"] >= min_subproblems and rep["closed"] >= min_closed:
+        if after is None and rep["subproblems"] >= min_subproblems and rep["closed"] >= min_closed and \
+                rep["feas_cuts"] >= min_feas_cuts:
             after = r
         if after is not None and r - after >= rounds_after:
             break
@@ -386,7 +393,7 @@ def write_pool_bin(path: str, eng: E.Engine) -> int:
 
 def check_large_pool(cfg: str, seed: int, width: int, min_opt_cuts: int, batch: int = 1024, per_kind: int = 8,
                      round_seconds: float = 5.0, max_seconds: float = 240.0, device: int = 0, threads: int = 0,
-                     need_rounds: int = 12):
+                     need_rounds: int = 12, keep_lb: bool = False):
     """Parity at the pool sizes the timed B&B runs against: the seeded search of ``cfg`` (lower
     bounds 0; incumbent from the width-``width`` restricted-DD heuristic) runs untraced, with
     uncapped refinement loops, until its optimality list holds ``min_opt_cuts`` cuts.  The next
@@ -402,7 +409,8 @@ def check_large_pool(cfg: str, seed: int, width: int, min_opt_cuts: int, batch: 
     from sgufp_solver_amd.pools import DOUBLE_MAX, DOUBLE_MIN, NodeRecord
     t0 = time.perf_counter()
     inst = instance.generate(instance.CONFIGS[cfg], seed)
-    inst.lb[:] = 0
+    if not keep_lb:
+        inst.lb[:] = 0
     work = tempfile.mkdtemp(prefix="sgufp_bigpool_")
     net = os.path.join(work, "net.txt")
     inst.write(net)
@@ -414,9 +422,12 @@ def check_large_pool(cfg: str, seed: int, width: int, min_opt_cuts: int, batch: 
         z = RestrictedExplorer(eng, width).incumbent([root], z)
     eng.frontier_clear()
     eng.frontier_push([root])
-    rep = {"config": cfg, "seed": seed, "heuristic_width": width, "rounds": 0, "search_seconds": 0.0}
+    rep = {"config": cfg, "seed": seed, "heuristic_width": width, "rounds": 0, "search_seconds": 0.0,
+           "lower_bounds": "generated" if keep_lb else "zero"}
     diving = True
-    while eng.cuts_count(0) < min_opt_cuts and eng.frontier_size() and time.perf_counter() - t0 < max_seconds:
+    # (with the generated lower bounds the paths are infeasible: the pool is feasibility cuts)
+    count = (lambda: eng.cuts_count(0) + eng.cuts_count(1)) if keep_lb else (lambda: eng.cuts_count(0))
+    while count() < min_opt_cuts and eng.frontier_size() and time.perf_counter() - t0 < max_seconds:
         eng.bnb_set_limits(0, round_seconds)
         z, st = eng.bnb_step(z, 64 if diving else batch)
         if st.exact:

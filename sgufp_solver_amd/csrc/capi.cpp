@@ -122,6 +122,7 @@ bool sgufp_ctx::init() {
     if (const char *e = getenv("SGUFP_CHUNK_LPS")) chunk_lps = std::max(1, atoi(e));
     if (const char *e = getenv("SGUFP_NX")) nx_on = atoi(e) != 0;
     if (const char *e = getenv("SGUFP_SUB_STATS")) sub_stats = atoi(e) != 0;
+    if (const char *e = getenv("SGUFP_LEAF_SPLIT")) leaf_split = std::max(0, atoi(e));
     if (const char *e = getenv("SGUFP_NX_MIN")) nx_min = std::max(1, atoi(e));
     if (const char *e = getenv("SGUFP_NX_SKIP")) nx_skip = std::max(0, atoi(e));
     int64_t acap = std::max<int64_t>(1, (int64_t)std::max(0, L - 4) * (kRelaxedMaxWidth - 1) * maxU);
@@ -330,8 +331,16 @@ bool sgufp_ctx::exact_prepare() {
         ocap = cap;
     }
     if (!d_pslot && (!alloc(d_pslot, (size_t)max_batch, "exact pending") || !alloc(d_pbase, (size_t)max_batch, "exact pending") ||
-                     !alloc(d_ectr, 16, "exact pending") || !alloc(d_pidx, (size_t)max_batch, "exact pending")))
+                     !alloc(d_ectr, 32, "exact pending") || !alloc(d_pidx, (size_t)max_batch, "exact pending")))
         return false;
+    // open-leaf compaction of the leaf passes: per pending record its open leaves after phase A
+    // (at most all its leaves: the leaf-pass space x kLeafPass entries)
+    if (leaf_split > 0 && !d_open_cnt) {
+        const size_t npass = (size_t)max_batch * ((size_t)sc.Ncap / kLeafPass + 1);
+        if (!alloc(d_open_cnt, (size_t)max_batch, "exact open leaves") ||
+            !alloc(d_open_list, npass * kLeafPass, "exact open leaves"))
+            return false;
+    }
     if (!nx_prepare(no)) return false;
     if (o_built < no) {
         if (!hip_ok(launch_exact_cols(d_rows, d_rhs, d_oorder, no, o_built, net.n_slots + 1, net.n_slots, ocap, d_coefO,
@@ -351,9 +360,14 @@ bool sgufp_ctx::exact_prepare() {
     }
     ex.coefS = d_coefS;
     ex.RS = d_RS;
-    if (!hip_ok(hipMemsetAsync(d_ectr, 0, 16 * sizeof(unsigned long long), stream), "memset") ||
-        !hip_ok(hipMemsetAsync(d_pidx, 0xFF, (size_t)max_batch * sizeof(int32_t), stream), "memset"))
+    if (!hip_ok(hipMemsetAsync(d_ectr, 0, 32 * sizeof(unsigned long long), stream), "memset") ||
+        !hip_ok(hipMemsetAsync(d_pidx, 0xFF, (size_t)max_batch * sizeof(int32_t), stream), "memset") ||
+        (d_open_cnt && !hip_ok(hipMemsetAsync(d_open_cnt, 0, (size_t)max_batch * sizeof(int32_t), stream), "memset")))
         return false;
+    ex.leaf_split = d_open_cnt ? leaf_split : 0;
+    ex.leaf_phase = 0;
+    ex.open_cnt = d_open_cnt;
+    ex.open_list = d_open_list;
     ex.lazy = ex.nsc == 0 ? exact_lazy : 0;
     ex.pidx = d_pidx;
     ex.nslots = max_batch;
@@ -451,17 +465,19 @@ bool sgufp_ctx::emit_current(const BatchIn &in, const Pool &p) {
     const char *es = std::getenv("SGUFP_EXACT_STATS");   // diagnostics (tests read them from stderr)
     const bool estats = es && es[0] == '1';
     if (estats && ex.enabled) {
-        unsigned long long c[16];
-        if (download(c, d_ectr, 16) && sync())
+        unsigned long long c[32];
+        if (download(c, d_ectr, 32) && sync())
             std::fprintf(stderr,
                          "[exact] pending %llu passes %llu blocks swept %llu of %llu (no %d, screen %d, lazy %d: "
                          "%llu resolves, %llu blocks); non-exact: dag items %llu, fallbacks %llu, kept back "
                          "(ranks %llu, tail %llu, segment %llu, program %llu, other %llu), handed off %llu; exact "
-                         "leaves %llu, open after 16 blocks %llu, after 64 %llu\n",
+                         "leaves %llu, open after 16 blocks %llu, after 64 %llu; split %d: open after it %llu, "
+                         "phase-B blocks %llu\n",
                          c[0] >> 32, c[0] & 0xFFFFFFFFull, c[3],
                          (c[0] & 0xFFFFFFFFull) * (unsigned long long)((ex.no + 63) / 64 + (ex.nsc + 63) / 64), ex.no,
                          ex.nsc, ex.lazy, c[4], c[5], c[6], c[7], c[9] & 1023, (c[9] >> 10) & 1023, (c[9] >> 20) & 1023,
-                         (c[9] >> 30) & 1023, (c[9] >> 40) & 1023, c[12], c[15], c[14], c[13]);
+                         (c[9] >> 30) & 1023, (c[9] >> 40) & 1023, c[12], c[15], c[14], c[13], ex.leaf_split, c[18],
+                         c[19]);
     }
     total_children = (int64_t)tot[0];
     total_csol = (int64_t)tot[1];
@@ -837,6 +853,8 @@ bool sgufp_ctx::sub_grow(int n, size_t total) {
         if (d_wstat) release(d_wstat);
         if (!alloc(d_wstat, (size_t)cap * S * 2, "sub io")) return false;
         sio.wstat = d_wstat;
+        if (sio.first_inf) release(sio.first_inf);
+        if (!alloc(sio.first_inf, (size_t)cap, "sub io")) return false;
         // per path: its chains (k_sub_paths), m entries each at most
         const size_t pm = (size_t)cap * std::max(net.m, 1);
         if (sio.pc_info) { release(sio.pc_info); release(sio.pc_th); release(sio.pc_ol); release(sio.pc_R); release(sio.pc_arcs); release(sio.pc_rw); }

@@ -259,6 +259,9 @@ struct sgufp_ctx {
     int nx_min = 2048;
     int nx_skip = 256;
     int32_t *d_pkind = nullptr, *d_P = nullptr, *d_nxh = nullptr, *d_pstop = nullptr, *d_nxlist = nullptr;
+    // open-leaf compaction of the exact leaf passes (SGUFP_LEAF_SPLIT cut blocks in phase A; 0: off)
+    int leaf_split = 16;
+    int32_t *d_open_cnt = nullptr, *d_open_list = nullptr;
     double *d_G = nullptr;
     unsigned long long *d_MS = nullptr;
     int nx_cap = 0;                           // columns of G / MS allocated

@@ -214,11 +214,13 @@ struct ExactIO {
     double SGUFP_GBL *R;                  // [max_batch][ostride]: root folds, pending index x newest-first position
     int32_t SGUFP_GBL *pend_slot;         // [max_batch] batch slot of pending record i
     uint32_t SGUFP_GBL *pend_base;        // [max_batch] first leaf pass of pending record i
-    unsigned long long SGUFP_GBL *ctr;    // [16]: (pending << 32 | leaf passes), root work, leaf work,
+    unsigned long long SGUFP_GBL *ctr;    // [32]: (pending << 32 | leaf passes), root work, leaf work,
                                           // blocks swept, lazy resolves, blocks they swept, non-exact:
                                           // DAG work, fallbacks, leaf work, kept back; wide leaf work,
                                           // maxState completion work, non-exact entries;
-                                          // diagnostics: exact leaves open after 64 / 16 blocks, alive
+                                          // diagnostics: exact leaves open after 64 / 16 blocks, alive;
+                                          // 16 / 17: phase-B leaf work (narrow / wide), 18: leaves
+                                          // open after phase A, 19: phase-B blocks swept
     // Lazy terminal weights: a leaf pass sweeps at most `lazy` cut blocks (the newest 64 x lazy
     // O cuts); when that leaves some leaf above optimalLB the pass's leaves keep the partial
     // minimum (an upper bound of the terminal weight) flagged kLazy, and the argmax scans
@@ -249,6 +251,16 @@ struct ExactIO {
     unsigned long long SGUFP_GBL *MS;     // [max_batch][ostride] maxState per cut (order-preserving key, atomic max)
     int32_t SGUFP_GBL *nxh;               // [nslots][4] per handed-off slot: k0, packed node words, k0's node,
                                           // first pool position of the phase
+    // Open-leaf compaction of the exact DDs' leaf passes (k_exact_leaf, phase A / B): phase A
+    // sweeps the first leaf_split cut blocks of every pass; a leaf still above optimalLB after
+    // them joins its record's open list (leaf indices from pend_base[i] x kLeafPass) with its
+    // partial minimum in tw, and phase B sweeps the remaining blocks over passes of kLeafPass OPEN
+    // leaves, so a pass whose leaves are all settled stops holding the other leaves' sweep.
+    // leaf_split 0: one phase (every pass sweeps until its leaves are settled).
+    int leaf_split;
+    int leaf_phase;                       // 0: single phase / phase A, 1: phase B
+    int32_t SGUFP_GBL *open_cnt;          // [nslots] open leaves per pending record after phase A
+    int32_t SGUFP_GBL *open_list;         // [leaf passes x kLeafPass] their leaf indices
 };
 constexpr int kExactScreen = 256;
 

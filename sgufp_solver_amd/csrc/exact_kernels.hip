@@ -188,6 +188,7 @@ struct LeafSharedT {
     LeafWave lw[kLeafWaves];
     double vb[kLeafWaves][kExactMaxT - 1][kWave];   // ancestor values of the current leaf (layers 0 .. T - 2), per wave
     int32_t item, flags[kLeafWaves];
+    uint32_t rmask[2];                   // rows (layer, rank) some leaf of the pass adds a coefficient of
 };
 
 // order-preserving key of a double (unsigned compare = numeric order, -0 below +0): the
@@ -199,6 +200,13 @@ __device__ __forceinline__ unsigned long long nx_key(double x) {
 
 // running min of a lane's cuts meeting a path value (std::min(w, v): keeps w on ties)
 __device__ __forceinline__ double rmin(double w, double v) { return (v < w) ? v : w; }
+// the same as one v_min_f64 (no NaN operands here; it may keep either of +0 / -0 on a tie, the
+// callers re-scan zero minima in pool order): fmin would add two canonicalizing v_max_f64
+__device__ __forceinline__ double vmin64(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 
 // ancestors of leaf j (wave-local) from layer dj down to the leaf's parent, values in vb;
 // returns the parent value
@@ -246,6 +254,9 @@ __device__ double first_zero(const NetDev &net, const ExactIO &ex, LeafShared &S
 #ifndef SGUFP_LEAF_PIPE
 #define SGUFP_LEAF_PIPE 1   // the next cut block's coefficients load while this one is swept
 #endif
+#ifndef SGUFP_LEAF_ROWMASK
+#define SGUFP_LEAF_ROWMASK 1   // stage only the rows the pass's leaves add (0: all rows, A/B)
+#endif
 #ifndef SGUFP_LEAF_MIN_WAVES
 #define SGUFP_LEAF_MIN_WAVES 6   // three 8-wave workgroups per CU (VGPRs <= 85)
 #endif
@@ -261,7 +272,7 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LeafShared &S = *(LeafShared *)smem_raw;
     if (NX && ex.ctr[12] == 0) return;   // no non-exact entry in this batch
-    const int w = wid();
+    const int w = uni(wid());   // (wave-uniform: the per-leaf tests below stay scalar branches)
     const int tid = (int)threadIdx.x;
     const unsigned long long packed = ex.ctr[0];
     const int npend = (int)(packed >> 32);
@@ -269,8 +280,15 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
     const int nbs = (ex.nsc + kWave - 1) / kWave;              // screening blocks first
     const int nblk = nbs + (ex.no + kWave - 1) / kWave;
     const int us = sc.us;
+    // open-leaf compaction (ExactIO::leaf_split): phase A sweeps blocks [0, split) of every pass,
+    // phase B (pb) the rest over passes of open leaves
+    const bool split = !NX && ex.leaf_split > 0 && ex.lazy == 0;
+    const bool pb = split && ex.leaf_phase == 1;
     for (;;) {
-        if (tid == 0) S.item = (int32_t)atomicAdd(&ex.ctr[NX ? (ex.nx_ms ? 11 : 8) : (kWide ? 10 : 2)], 1ull);
+        if (tid == 0) {
+            S.item = (int32_t)atomicAdd(&ex.ctr[NX ? (ex.nx_ms ? 11 : 8) : (pb ? (kWide ? 17 : 16) : (kWide ? 10 : 2))], 1ull);
+            S.rmask[0] = S.rmask[1] = 0u;
+        }
         __syncthreads();
         const uint32_t item = (uint32_t)uni(S.item);
         __syncthreads();
@@ -311,6 +329,10 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
         const int T = Tdd - kb;
         const int E = (T - 1) * us;
         if (!NX && (E > kExactMaxEntries) != kWide) continue;   // the other row count's entry
+        // phase B: this item is chunk `pass` of the record's open list
+        const int nopen = pb ? uni(ex.open_cnt[i]) : 0;
+        if (pb && pass * kLeafPass >= nopen) continue;
+        const GBL int32_t *olist = pb ? ex.open_list + (size_t)ex.pend_base[i] * kLeafPass : nullptr;
         const GBL uint32_t *lay = sc.lay + (size_t)slot * sc.Tcap * 5;
         const uint32_t lnoff = uni(lay[Tdd - 1]), lnn = uni(lay[sc.Tcap + Tdd - 1]);
         const size_t N = (size_t)slot * sc.Ncap;
@@ -320,25 +342,36 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
         }
         // this wave's leaves: ancestry tables and alive mask
         const int j0 = pass * kLeafPass + w * kLeavesPerWave;
-        const int cnt = max(0, min(kLeavesPerWave, (int)lnn - j0));
+        const int cnt = uni(max(0, min(kLeavesPerWave, (pb ? nopen : (int)lnn) - j0)));
+        // lane j's leaf (index among the record's leaves): consecutive in phase A, from the open
+        // list in phase B (in the order phase A's passes appended them)
+        const int lid = lane() < cnt ? (pb ? olist[j0 + lane()] : j0 + lane()) : 0;
         uint32_t alive = 0;
         {
             const int j = lane();
             bool al = false;
             uint32_t anc[kExactMaxT];
+            uint64_t used = 0;   // rows this leaf's path adds: (layer, rank) with an alive in-arc, rank > 0
             if (j < cnt) {
-                uint32_t node = lnoff + (uint32_t)(j0 + j);
+                uint32_t node = lnoff + (uint32_t)lid;
                 al = (sc.nflag[N + node] & kAlive) != 0;
 #pragma unroll
                 for (int k = kExactMaxT - 1; k >= 1; k--) {
                     if (k < T) {
                         const uint32_t t = sc.ntopo[N + node];
                         const uint8_t f = sc.nflag[N + node];
-                        S.lw[w].info[j][k] = (uint8_t)(((t >> kRankShift) & 63u) | ((f & kInAlive) ? 128u : 0u));
+                        const uint32_t r = (t >> kRankShift) & 63u;
+                        S.lw[w].info[j][k] = (uint8_t)(r | ((f & kInAlive) ? 128u : 0u));
+                        if ((f & kInAlive) && r) used |= 1ull << ((k - 1) * us + (int)r);
                         anc[k] = node;
                         node = lay[kb + k - 1] + (t & kParentMask);
                     }
                 }
+            }
+            used = (uint64_t)lane_reduce<1>((int64_t)used, [](int64_t a, int64_t b) { return a | b; });
+            if (lane() == 0) {
+                if ((uint32_t)used) atomicOr(&S.rmask[0], (uint32_t)used);
+                if ((uint32_t)(used >> 32)) atomicOr(&S.rmask[1], (uint32_t)(used >> 32));
             }
             // first layer where this leaf's ancestors leave the previous leaf's
             int dv = 1;
@@ -381,7 +414,8 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
         // non-exact: per leaf the first cut (pool position) with value <= optimalLB; a leaf whose
         // in-order minimum already is counts as done before the phase
         double twold = EDMAX;
-        if (!nx && !ex.nx_ms && lane() == 0) atomicAdd(&ex.ctr[15], (unsigned long long)__popc(alive));
+        if (!nx && !pb && lane() == 0) atomicAdd(&ex.ctr[15], (unsigned long long)__popc(alive));
+        if (pb && lane() < cnt) twold = sc.tw[N + lnoff + (uint32_t)lid];   // phase A's partial minimum
         if (nx) {
             const bool al = lane() < cnt && ((alive >> lane()) & 1u);
             if (al) twold = sc.tw[N + lnoff + (uint32_t)(j0 + lane())];
@@ -390,27 +424,48 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
             if (lane() < kLeavesPerWave) S.lw[w].fle[lane()] = pre ? 0 : INT_MAX;
         }
         int bb_last = -1;
-        const int bend = ph2 ? bto + 1 : nlim;
+        // phase A stops after the split blocks, phase B starts there
+        const int bsplit = split ? min(nlim, ex.leaf_split) : nlim;
+        if (pb) bfrom = bsplit;
+        const int bend = ph2 ? bto + 1 : (split && !pb ? bsplit : nlim);
 #if SGUFP_LEAF_PIPE
         // a block's coefficients are loaded into registers while the previous block is swept
         // (every load of a block issued at once), stored to LDS at the top of its iteration --
-        // the end of the previous iteration's barriers found every wave done with the old ones
+        // the end of the previous iteration's barriers found every wave done with the old ones.
+        // Only the rows some leaf of the pass adds are staged (S.rmask: the pass's 128 leaves
+        // share their upper ancestors, so about 14 of the C4 trees' 24 coefficient rows): the
+        // others are never read.  Wave w stages the pass's used rows w, w + 8, ... (in row
+        // order), one row per 64 lanes, the same in every block.
         constexpr int kSU = (ROWS * kWave + kLeafWaves * kWave - 1) / (kLeafWaves * kWave);
         double stg[kSU];
+        int srow[kSU], sslot[kSU];
+        {
+            // (a used row with no coefficient slot is staged as zeros, as before)
+#if SGUFP_LEAF_ROWMASK
+            uint64_t mm = (uint64_t)S.rmask[0] | (uint64_t)S.rmask[1] << 32;
+#else
+            uint64_t mm = E >= 64 ? ~0ull : (1ull << E) - 1ull;   // A/B: every row of the tree
+#endif
+            // the (w + 8 u)-th set bit of mm for u = 0 .. kSU - 1 (uniform scalar walk, once a pass)
+            for (int c = 0; c < w && mm; c++) mm &= mm - 1;
+#pragma unroll
+            for (int u = 0; u < kSU; u++) {
+                srow[u] = mm ? (int)__builtin_ctzll(mm) : -1;
+                sslot[u] = srow[u] >= 0 ? uni(S.stab[srow[u]]) : -1;
+#pragma unroll
+                for (int c = 0; c < kLeafWaves; c++) mm &= mm - 1;
+            }
+        }
         auto stage_load = [&](int bbx) {
             const bool scrx = bbx < nbs_r;
             const int bx = scrx ? bbx : bbx - nbs_r;
             const int ncx = scrx ? ex.nsc : ex.no;
             const GBL double *cmx = scrx ? ex.coefS : ex.coefO;
             const size_t csx = scrx ? (size_t)kExactScreen : (size_t)ex.ostride;
+            const int sx = bx * kWave + lane();
 #pragma unroll
-            for (int u = 0; u < kSU; u++) {
-                const int x = tid + u * kLeafWaves * kWave;
-                const int e = x >> 6, l = x & (kWave - 1);
-                const int sx = bx * kWave + l;
-                const int sl = x < E * kWave ? S.stab[e] : -1;
-                stg[u] = (sl >= 0 && sx < ncx) ? cmx[(size_t)sl * csx + (scrx ? sx : ncx - 1 - sx)] : 0.0;
-            }
+            for (int u = 0; u < kSU; u++)
+                stg[u] = (sslot[u] >= 0 && sx < ncx) ? cmx[(size_t)sslot[u] * csx + (scrx ? sx : ncx - 1 - sx)] : 0.0;
         };
         if (bfrom < bend) stage_load(bfrom);
 #endif
@@ -422,10 +477,8 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
             const int ncut = scr ? ex.nsc : ex.no;
 #if SGUFP_LEAF_PIPE
 #pragma unroll
-            for (int u = 0; u < kSU; u++) {
-                const int x = tid + u * kLeafWaves * kWave;
-                if (x < E * kWave) S.C[x >> 6][x & (kWave - 1)] = stg[u];
-            }
+            for (int u = 0; u < kSU; u++)
+                if (srow[u] >= 0) S.C[srow[u]][lane()] = stg[u];
             __syncthreads();
             if (bb + 1 < bend) stage_load(bb + 1);
 #else
@@ -444,9 +497,14 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
             const bool vc = s < ncut && s >= first;
             double ms = -INFINITY;   // non-exact: max over this wave's alive leaves, this lane's cut
             if (cnt > 0 && (nx || (done & alive) != alive)) {
-                const double root = vc ? (scr ? ex.RS[(size_t)i * kExactScreen + s] : ex.R[(size_t)i * ex.ostride + s]) : 0.0;
-                const uint32_t open = alive & ~done;
-                const uint32_t need = nx ? alive : open;
+                // exact entries: a lane past the pool's end starts at +inf, so its values leave every
+                // running minimum alone (a dead path gives DOUBLE_MIN on every lane, valid or not)
+                // and the leaf loop below needs no per-lane condition -- no exec-mask switching
+                const double root = vc ? (scr ? ex.RS[(size_t)i * kExactScreen + s] : ex.R[(size_t)i * ex.ostride + s])
+                                       : (nx ? 0.0 : INFINITY);
+                // (wave-uniform: in scalar registers, so the leaf tests below are scalar branches)
+                const uint32_t open = uni(alive & ~done);
+                const uint32_t need = uni(nx ? alive : open);
                 double par = root;
 #if SGUFP_LEAF_REGS
                 // ancestor values in registers (anc[k] = local layer k): a leaf recomputes the
@@ -485,7 +543,14 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
                             if (row == kRowDead) v = EDMIN;
                             else if (row == kRowNoAdd) v = par;
                             else v = par + S.C[row][lane()];
-                            if (!ph2 && vc && ((open >> j) & 1u)) m[j] = rmin(m[j], v);
+                            if (nx) {
+                                if (!ph2 && vc && ((open >> j) & 1u)) m[j] = rmin(m[j], v);
+                            } else if ((open >> j) & 1u) {
+                                // v_min_f64: it may keep either of +0 / -0 where std::min keeps the
+                                // first; a zero minimum above optimalLB is re-scanned in pool order
+                                // (first_zero) as it is across lanes, so the result is the same
+                                m[j] = vmin64(m[j], v);
+                            }
                             if (nx) {
                                 ms = (vc && v > ms) ? v : ms;
                                 if (!ph2 && ((open >> j) & 1u)) {
@@ -504,7 +569,7 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
 #pragma unroll
                     for (int j = 0; j < kLeavesPerWave; j++)
                         if ((open >> j) & 1u)
-                            if (__ballot(vc && m[j] <= incumbent)) done |= 1u << j;
+                            if (__ballot(m[j] <= incumbent)) done |= 1u << j;   // (+inf on lanes past the pool)
                     // diagnostics: leaves still open after 16 / 64 blocks
                     if (lane() == 0 && (bb == 15 || bb == 63))
                         atomicAdd(&ex.ctr[bb == 15 ? 14 : 13], (unsigned long long)__popc(alive & ~done));
@@ -540,8 +605,12 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
             if (lane() == 0 && cnt > 0) atomicMax(&ex.P[i], pm);
         }
         const bool lazy = !nx && !finished && nlim < nblk;
-        if (tid == 0) atomicAdd(&ex.ctr[3], (unsigned long long)nb_done);   // diagnostics: cut blocks swept
+        // phase A with blocks left: the open leaves' partial minima go to tw and the leaves to
+        // the record's open list (no zero re-scan yet: phase B decides the final value)
+        const bool to_b = split && !pb && !finished && bsplit < nlim;
+        if (tid == 0) atomicAdd(&ex.ctr[pb ? 19 : 3], (unsigned long long)max(0, nb_done - (pb ? bsplit : 0)));   // diagnostics: cut blocks swept
         // terminal weights: min over the lanes
+        uint32_t openb = 0;
 #pragma unroll
         for (int j = 0; j < kLeavesPerWave; j++) {
             if ((alive >> j) & 1u) {
@@ -552,13 +621,34 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
                     const double old = lane_get(twold, j);
                     if (!(v < old)) v = old;
                     else if (v == 0.0 && v > incumbent && !((done >> j) & 1u)) v = first_zero(net, ex, S, w, j, T, us, i, first);
+                } else if (pb) {
+                    // phase A's minimum covers the earlier blocks (pool order: it stays on ties); a
+                    // zero from either phase (lane minima of equal values differ only in the sign of
+                    // zero) is re-scanned in pool order from the first cut
+                    const double old = lane_get(twold, j);
+                    if (!(v < old)) v = old;
+                    if (v == 0.0 && v > incumbent) v = first_zero(net, ex, S, w, j, T, us, i);
+                } else if (to_b && v > incumbent) {
+                    openb |= 1u << j;
                 } else if (!lazy && v == 0.0 && v > incumbent && !((done >> j) & 1u))
                     v = first_zero(net, ex, S, w, j, T, us, i);
+                const int lj = __builtin_amdgcn_readlane(lid, j);
                 if (lane() == 0) {
-                    sc.tw[N + lnoff + (uint32_t)(j0 + j)] = v;
-                    if (lazy) sc.nflag[N + lnoff + (uint32_t)(j0 + j)] |= kLazy;
+                    sc.tw[N + lnoff + (uint32_t)lj] = v;
+                    if (lazy) sc.nflag[N + lnoff + (uint32_t)lj] |= kLazy;
                 }
             }
+        }
+        if (to_b && openb) {
+            int base = 0;
+            if (lane() == 0) {
+                base = atomicAdd(&ex.open_cnt[i], __popc(openb));
+                atomicAdd(&ex.ctr[18], (unsigned long long)__popc(openb));
+            }
+            base = __builtin_amdgcn_readfirstlane(base);
+            const int j = lane();
+            if (j < kLeavesPerWave && ((openb >> j) & 1u))
+                ex.open_list[(size_t)ex.pend_base[i] * kLeafPass + base + __popc(openb & ((1u << j) - 1u))] = lid;
         }
         __syncthreads();
     }
@@ -749,13 +839,27 @@ hipError_t launch_exact(const NetDev &net, const Scratch &sc, const ExactIO &ex,
     }
     using Narrow = LeafSharedT<kExactMaxEntries>;
     using Wide = LeafSharedT<kExactMaxEntriesWide>;
+    // exact DDs: phase A (or the single phase), then phase B over the open leaves
+    ExactIO pb = ex;
+    pb.leaf_phase = 1;
+    const bool two = ex.leaf_split > 0 && ex.lazy == 0;
     hipLaunchKernelGGL((k_exact_leaf<false, kExactMaxEntries>), dim3(4 * cus), dim3(kLeafWaves * kWave), sizeof(Narrow), st,
                        net, sc, ex, incumbent);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (two) {
+        hipLaunchKernelGGL((k_exact_leaf<false, kExactMaxEntries>), dim3(4 * cus), dim3(kLeafWaves * kWave), sizeof(Narrow),
+                           st, net, sc, pb, incumbent);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     if ((kExactMaxT - 1) * sc.us > kExactMaxEntries) {   // deeper / wider exact trees are possible
         hipLaunchKernelGGL((k_exact_leaf<false, kExactMaxEntriesWide>), dim3(4 * cus), dim3(kLeafWaves * kWave), sizeof(Wide),
                            st, net, sc, ex, incumbent);
         if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (two) {
+            hipLaunchKernelGGL((k_exact_leaf<false, kExactMaxEntriesWide>), dim3(4 * cus), dim3(kLeafWaves * kWave),
+                               sizeof(Wide), st, net, sc, pb, incumbent);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
     }
     if (!ex.nx || !ex.pkind) return hipSuccess;
     hipLaunchKernelGGL((k_exact_leaf<true, kExactMaxEntries>), dim3(4 * cus), dim3(kLeafWaves * kWave), sizeof(Narrow), st,

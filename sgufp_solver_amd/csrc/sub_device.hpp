@@ -13,6 +13,8 @@ enum SubStatus : int32_t {
     kSubOptimal = 0,      // optimality-cut contribution written
     kSubInfeasible = 1,   // feasibility ray written (grb.cpp:288-350)
     kSubError = 2,        // invalid path (two in-arcs choosing one out-arc) or certificate failure
+    kSubSkipped = 3,      // not solved: an earlier scenario of the path is infeasible, and the
+                          // reference stops at the first infeasible one (grb.cpp:284-351)
 };
 
 struct SubNet {
@@ -81,6 +83,8 @@ struct SubIO {
     int16_t SGUFP_GBL *wst_x;            // [slots][S][m]
     int32_t SGUFP_GBL *wst_a;            // [slots][S][n]
     uint8_t SGUFP_GBL *wst_ok;           // [slots][S]
+    int32_t SGUFP_GBL *first_inf;        // [P] or null: smallest scenario of the path found infeasible so
+                                         // far (launch_subproblem sets INT_MAX-like); later scenarios stop
     int32_t SGUFP_GBL *wstat;            // [P*S][2] or null: augmentations (negative: a warm start fell
                                          // back to the cold SSP), Bellman-Ford passes
     // The chains of each path (k_sub_paths, once per path for all its scenarios: the chains

@@ -1190,6 +1190,31 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
     }
     first_bad = B::all(first_bad, [](int x, int y) { return x < y ? x : y; }, W.red);
     B::sync();
+    // The reference returns at the first infeasible scenario (grb.cpp:284-351): only its ray
+    // reaches the cut.  A scenario infeasible up front records itself in first_inf[p]; one that
+    // finds an earlier infeasible scenario of its path recorded stops (kSubSkipped), here or
+    // between its augmentations below.  (The cut is the same whichever later scenarios stop.)
+    auto skip_now = [&]() -> bool {
+        if (!io.first_inf) return false;
+        int fi = __hip_atomic_load(&io.first_inf[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fi = B::all(fi, [](int x, int y) { return x < y ? x : y; }, W.red);
+        return fi < s;
+    };
+    auto skip_out = [&]() {
+        if (tid == 0) {
+            io.status[b] = kSubSkipped;
+            io.obj[b] = 0;
+            io.dual[b] = 0;
+            io.rhs[b] = 0;
+            if (io.wstat) { io.wstat[2 * b] = 0; io.wstat[2 * b + 1] = 0; }
+            if (wdst >= 0) io.wst_ok[(size_t)wdst * S + s] = 0;
+        }
+    };
+    if (io.first_inf && first_bad != INT_MAX && tid == 0) atomicMin(&io.first_inf[p], s);
+    if (skip_now()) {
+        skip_out();
+        return;
+    }
     // phase 5 sums the cut row in LDS when it fits over the chain records (int64 per slot) and
     // the chains' flows fit the predecessor / path / imbalance space (int16 per chain)
 #ifdef SGUFP_SUB_NO_LACC
@@ -1320,7 +1345,12 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         // used-up arcs restarted (invalidate_subtrees).  (Reusing the labels without any
         // Bellman-Ford while a tight residual path survives never found one on C3 / C4.)
         bool warm = false;
+        bool skipped = false;
         for (; status == kSubOptimal && !repaired; iters++) {
+            if ((iters & 7) == 7 && skip_now()) {
+                skipped = true;
+                break;
+            }
             SUB_T0();
             if (!bellman_ford<RG, WT, NW>(N, W, nct, nz, kSsp, M, warm)) { status = kSubError; err_site = 1; break; }
             SUB_T1(t_bf);
@@ -1383,6 +1413,10 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
                    (int)blockIdx.x, nct, nz, iters, nbf, W.misc[5], (unsigned long long)(wall_clock64() - tr0),
                    (unsigned long long)t_bf, (unsigned long long)t_pred, (unsigned long long)t_walk);
 #endif
+        if (skipped) {
+            skip_out();
+            return;
+        }
         // lower bounds met?
         int unmet = 0;
         for (int k = tid; k < nct; k += T) {
@@ -1411,7 +1445,10 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
             // 4. potentials of the final residual: plain costs (optimal duals) or big-M
             //    costs (their M-multiple is a dual ray, case (iii))
             const int mode = unmet ? kPotBigM : kPotPlain;
-            if (unmet) status = kSubInfeasible;
+            if (unmet) {
+                status = kSubInfeasible;
+                if (io.first_inf && tid == 0) atomicMin(&io.first_inf[p], s);
+            }
             if (!bellman_ford<RG, WT, NW>(N, W, nct, nz, mode, M)) { status = kSubError; err_site = 5; }
             const int64_t dz = key_cost<WS>(W.key[n]);
             B::sync();   // every thread read Z's key before the alphas overwrite it in place
@@ -1756,8 +1793,15 @@ hipError_t launch_scenarios(const SubNet &N, const SubIO &io, hipStream_t st) {
 }
 }  // namespace
 
-hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st) {
-    if (io.n_paths <= 0) return hipSuccess;
+hipError_t launch_subproblem(const SubNet &N, const SubIO &io_in, hipStream_t st) {
+    if (io_in.n_paths <= 0) return hipSuccess;
+    // SGUFP_SUB_SKIP=0: every scenario solved to the end (A/B of the first-infeasible stop)
+    static const bool no_skip = [] {
+        const char *e = getenv("SGUFP_SUB_SKIP");
+        return e && atoi(e) == 0;
+    }();
+    SubIO io = io_in;
+    if (no_skip) io.first_inf = nullptr;
     // 32-bit keys (N.key32, host: no lower bound in any scenario, sum_a |r_a| < 2^18, n + 2 <
     // 2^11); SGUFP_SUB_KEY64=1 forces the 64-bit keys (A/B)
     const char *ek = getenv("SGUFP_SUB_KEY64");
@@ -1765,6 +1809,8 @@ hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st) {
     // every flow within [max l, min u]
     const bool k32 = N.key32 && !(ek && atoi(ek) == 1);
     const bool warm = io.warm_src || io.warm_dst;
+    if (io.first_inf && hipMemsetAsync(io.first_inf, 0x7F, (size_t)io.n_paths * sizeof(int32_t), st) != hipSuccess)
+        return hipGetLastError();
     hipLaunchKernelGGL(k_sub_paths, dim3((unsigned)io.n_paths), dim3(kWave), (size_t)N.m * 3 * sizeof(int16_t), st, N, io);
     const hipError_t e = !k32 ? (warm ? launch_scenarios<int64_t, true>(N, io, st) : launch_scenarios<int64_t, false>(N, io, st))
                               : (warm ? launch_scenarios<int32_t, true>(N, io, st) : launch_scenarios<int32_t, false>(N, io, st));

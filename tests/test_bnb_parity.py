@@ -133,3 +133,32 @@ def test_bnb_parity_exact_phase_variants(monkeypatch, knob, value):
     monkeypatch.setenv(knob, value)
     seen = _search_rounds("M1", 1, 0, rounds=120, batch=64, sample=12, min_closed=2, highs=False)
     assert seen["closed"] >= 2 and seen["replayed"] > 0
+
+
+def test_bnb_parity_c3_generated_lower_bounds():
+    """BASELINE configs[2] as generated (sink-arc lower bounds kept): the scenarios of the paths
+    the search sends are infeasible, every subproblem returns the first infeasible scenario's
+    ray as a feasibility cut (grb.cpp:284-351), the loop applies it with applyFeasibilityCut's
+    cascade (DD.cpp:3842-3930, 4025-4177) -- round by round against ref_dd relaxp under the
+    device-made F pool, each new cut checked to cut its path off (round-5 VERDICT item 2)."""
+    seen = _search_rounds("C3", 1, 64, rounds=80, batch=64, sample=32, min_subproblems=1, round_iters=2,
+                          keep_lb=True, min_feas_cuts=50)
+    assert seen["feas_cuts"] >= 50 and seen["checked"] > 0 and seen["mismatches"] == 0
+
+
+def test_bnb_parity_c5_generated_lower_bounds():
+    """BASELINE configs[4] (5k arcs, 512 scenarios, cut generation in the loop) with its
+    generated lower bounds: feasibility cuts in the loop at the 5k-arc scale."""
+    seen = _search_rounds("C5", 1, 0, rounds=80, batch=32, sample=8, round_seconds=3.0, replay=False,
+                          min_subproblems=1, rounds_after=2, round_iters=1, keep_lb=True, min_feas_cuts=4)
+    assert seen["feas_cuts"] >= 4 and seen["relaxed"] > 0
+
+
+def test_bnb_parity_c4_generated_lower_bounds_at_large_pool():
+    """The seeded C4 / 256 search with the generated lower bounds until its pool holds 5 000
+    feasibility cuts (the bench's bnb_gen leg reaches ~7k), then the next round's batch against
+    ref_dd relaxp on the same pool (records pruned by a feasibility cut, survivors, exact leaves)."""
+    rep = bp.check_large_pool("C4", 1, 128, min_opt_cuts=5000, per_kind=8, keep_lb=True)
+    assert not rep["failures"], "\n".join(rep["failures"][:10])
+    assert rep["pool_feasibility"] >= 5000, rep
+    assert rep["checked"] >= 8

@@ -144,13 +144,14 @@ def test_subproblem_matches_highs(cfg, seed, S, zl, trials):
             assert abs(obj_mean[k] - mean) <= TOL * max(1.0, abs(mean))
             # tight at y-bar
             v = _cut_at(rhs[k], rows[k], keys, y)
-            assert abs(v - mean) <= 1e-7 * max(1.0, abs(mean)), (v, mean)
+            assert abs(v - mean) <= 1e-9 * max(1.0, abs(mean)), (v, mean)
             # valid at other matchings: RHS + coef.y >= mean_s Q_s(y)
             for _ in range(2):
                 y2 = _full_matching(net, rng, 0.9)
                 q2 = [so.dual_lp(net, y2, s)[:2] for s in range(net.S)]
                 if all(w == "optimal" for w, _ in q2):
                     m2 = sum(o for _, o in q2) / net.S
+                    # (validity against HiGHS's objective at another matching: its LP tolerances, 1e-7)
                     assert _cut_at(rhs[k], rows[k], keys, y2) >= m2 - 1e-7 * max(1.0, abs(m2))
         else:
             seen.add("feas")
@@ -161,7 +162,7 @@ def test_subproblem_matches_highs(cfg, seed, S, zl, trials):
             for _ in range(3):
                 y2 = _full_matching(net, rng, 1.0)
                 if so.dual_lp(net, y2, first_inf)[0] == "optimal":
-                    assert _cut_at(rhs[k], rows[k], keys, y2) >= -1e-7
+                    assert _cut_at(rhs[k], rows[k], keys, y2) >= -1e-9
     eng.close()
     if zl:
         assert "opt" in seen            # optimality cuts exercised
@@ -213,7 +214,7 @@ def test_subproblem_at_benchmark_scenario_counts(cfg, seed, zl, n_paths, sample)
             mean = float(np.sum(obj[k])) / S
             assert abs(obj_mean[k] - mean) <= TOL * max(1.0, abs(mean))
             v = _cut_at(rhs[k], rows[k], keys, y)
-            assert abs(v - mean) <= 1e-7 * max(1.0, abs(mean)), (v, mean)
+            assert abs(v - mean) <= 1e-9 * max(1.0, abs(mean)), (v, mean)
             if cfg == "C4" and "valid" not in kinds:     # one path: 256 HiGHS LPs (~25 s)
                 kinds.add("valid")
                 y2 = _full_matching(net, rng, 0.9)
@@ -337,11 +338,11 @@ def test_warm_start_matches_cold(cfg, seed, S, n_paths, lib, tmp_path):
     for k in range(n_paths):
         y = so.ybar_of_path(net, [int(x) for x in r["paths"][k]])
         v = _cut_at(r["rhs"][k], r["rows"][k], keys, y)
-        assert abs(v - r["obj_mean"][k]) <= 1e-7 * max(1.0, abs(r["obj_mean"][k])), (k, v, r["obj_mean"][k])
+        assert abs(v - r["obj_mean"][k]) <= 1e-9 * max(1.0, abs(r["obj_mean"][k])), (k, v, r["obj_mean"][k])
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,seed,S,n_paths", [("C3", 4, 16, 12), ("C4", 1, 256, 4), ("C5", 4, 4, 4)])
+@pytest.mark.parametrize("cfg,seed,S,n_paths", [("C3", 4, 16, 12), ("C4", 1, 256, 4), ("C5", 4, 16, 4)])
 @pytest.mark.parametrize("lib", ["prod", "verify"])
 def test_warm_start_with_lower_bounds(cfg, seed, S, n_paths, lib, tmp_path):
     """Warm starts on the generator's instances with their sink-arc lower bounds kept (64-bit
@@ -364,11 +365,20 @@ def test_warm_start_with_lower_bounds(cfg, seed, S, n_paths, lib, tmp_path):
     subprocess.run([sys.executable, helper, cfg, str(seed), str(S), str(n_paths), out, "warmgen"], env=env,
                    check=True, timeout=240)
     r = np.load(out)
-    st, cst = r["st"], r["cold_st"]
+    st, cst = r["st"].reshape(n_paths, S), r["cold_st"].reshape(n_paths, S)
     assert (st != 2).all() and (cst != 2).all(), "error / verify mismatch"
-    np.testing.assert_array_equal(st, cst)
-    feas = cst == 0
-    assert feas.any() and (~feas).any(), "the case should hold feasible and infeasible scenarios"
+    # per path up to its first infeasible scenario (the later ones may stop unsolved: status 3,
+    # the reference returns at the first infeasible one, grb.cpp:284-351)
+    for k in range(n_paths):
+        inf = np.nonzero(cst[k] == 1)[0]
+        upto = int(inf[0]) + 1 if inf.size else S
+        np.testing.assert_array_equal(st[k, :upto], cst[k, :upto])
+        assert (cst[k, :upto] != 3).all() and (st[k, :upto] != 3).all()
+    st, cst = st.reshape(-1), cst.reshape(-1)
+    feas = (cst == 0) & (st == 0)
+    assert feas.any()
+    if cfg != "C5":   # (C5's random matchings are mostly feasible: its 8-wave kernel is the point there)
+        assert (~feas).any(), "the case should hold feasible and infeasible scenarios"
     np.testing.assert_array_equal(r["obj"][feas], r["cold_obj"][feas])
     np.testing.assert_array_equal(r["dual"][feas], r["obj"][feas])
     np.testing.assert_array_equal(r["typ"], r["cold_typ"])

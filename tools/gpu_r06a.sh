@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 ( while sleep 50; do date >> gpurun_out/r06a_heartbeat.log; done ) &
 HB=$!
 T="python3 -u -m pytest -x -v --timeout 300 --timeout-method thread"
-timeout -k 10 600 $T tests/test_dd_api.py -k "view_ends or warm_slot" tests/test_subproblem.py -k "warm or view_ends or warm_slot" \
+timeout -k 10 600 $T tests/test_subproblem.py -k "lower_bounds" \
   > gpurun_out/r06a_tests.log 2>&1 || { kill $HB; exit 11; }
 SGUFP_SUB_STATS=1 timeout -k 10 300 python3 bench.py --mode bnb --bnb-config C4 --bnb-lb gen --nodes 1024 --round-seconds 5 \
   --bnb-heuristic 128 --bnb-seconds 20 > gpurun_out/r06a_bnb_gen_seeded.json 2> gpurun_out/r06a_bnb_gen_seeded.log || { kill $HB; exit 12; }
