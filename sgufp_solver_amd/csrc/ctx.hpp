@@ -24,7 +24,7 @@ namespace sgufp {
 struct Transport;   // shard.cpp
 // dd_kernels.hip
 size_t relax_lds_bytes(int Tcap, int Lcap, int cb, int us);
-size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw, int kbytes = 8, bool warm = false);
+size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw, int kbytes = 8, bool warm = false, bool wl = false);
 hipError_t launch_subproblem(const SubNet &N, const SubIO &io, hipStream_t st);
 hipError_t launch_warm_pick(const SubIO &io, const WarmRing &wr, int ptr, hipStream_t st);
 hipError_t launch_relax(const NetDev &, const Scratch &, const BatchIn &, const Pool &, const BatchOut &, double, int,

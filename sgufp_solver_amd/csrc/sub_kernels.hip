@@ -78,6 +78,14 @@ template <typename KT, bool ALLREG = false, bool PACK = false>
 struct SubLds {
     using Key = KT;
     static constexpr bool kAllReg = ALLREG;
+    // work-list Bellman-Ford (bf_converge_wl): single wave (PACK is "one wave per scenario"),
+    // every chain group in registers (<= 16 groups)
+#ifdef SGUFP_SUB_WL
+    static constexpr bool kWL = ALLREG && PACK;
+#else
+    static constexpr bool kWL = false;   // full sweeps (the work list measured slower)
+#endif
+    LDS uint32_t *inc;      // [n+2] kWL: groups with a chain out of v (bits 0-15) / into v (16-31)
     static constexpr int kHop = KeyT<KT>::hop_bits;
     static constexpr KT kKInf = KeyT<KT>::inf;
     LDS int32_t *imb;       // [n+2] warm starts: node imbalances of the initial flow
@@ -198,7 +206,7 @@ struct Blk {
 // flags.  (The chains' arcs come from k_sub_paths' lists in HBM.)
 constexpr int kSubLdsParts = 12;
 __host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int nz, int nw, size_t *off, int kbytes = 8,
-                                                 bool warm = false) {
+                                                 bool warm = false, bool wl = false) {
     size_t o = 0;
     off[1] = o; o = a16(o + (size_t)nct_cap * 8);
     // b words: 8 bytes, 4 with 32-bit keys, none in the single-wave kernel's 8-byte records
@@ -211,6 +219,7 @@ __host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int 
     off[6] = o; o = a16(o + (size_t)nz * 4);
     off[7] = o; o = a16(o + 8 * 4);
     off[10] = o; o = a16(o + (nw > 1 ? 8 * 8 : 0));   // red
+    off[11] = o; o = a16(o + (wl ? (size_t)(n + 2) * 4 : 0));   // inc (work-list Bellman-Ford)
 #ifdef SGUFP_SUB_VERIFY
     off[9] = o; o = a16(o + (size_t)(n + 2) * kbytes);
 #endif
@@ -561,6 +570,137 @@ __device__ __forceinline__ bool bf_converge(const SubNet &N, const WS &W, int nc
     return false;
 }
 
+// Work-list Bellman-Ford (one wave, every chain group in registers: WS::kWL).  The full sweeps
+// above relax every group of 64 chains per sweep -- one dependent LDS round trip each -- and
+// need two quiet sweeps to stop; after an augmentation most groups hold no arc whose end keys
+// moved.  Here a group is relaxed only while its bit is set in df (forward residual arcs) / db
+// (backward ones).  An arc u -> v can be unsettled only if key[u] fell or key[v] rose since it
+// was last relaxed, or it changed itself, so:
+//   * a lowered key[v] sets the groups of the arcs out of v: chains with tail v in df (W.inc
+//     bits 0-15), chains with head v in db (bits 16-31) -- read with the arc's end keys, one
+//     round trip, and OR-ed over the wave right away, so a group later in the sweep's order
+//     sees it in the same sweep (the Gauss-Seidel propagation of the full sweeps);
+//   * keys raised to infinity (invalidate_subtrees) set the groups of the arcs into them, and
+//     the chains whose flow an augmentation changed set their own group in both: those callers
+//     OR their bits into W.misc[1] / misc[2], which the next warm Bellman-Ford starts from
+//     (wl_mark); a cold one starts with every group set.
+// The Z arcs (a list of at most a few groups) are relaxed every forward sweep.  A forward +
+// backward iteration that lowers no key ends it: every group is then clean, so every arc is
+// settled -- the same fixed point (the unique shortest (cost, hops) keys) as the full sweeps.
+template <class WS>
+__device__ __forceinline__ void wl_mark(const WS &W, uint32_t mf, uint32_t mb) {
+    // uniform control flow (wave_or); single wave: lane 0's read-modify-write is not raced
+    mf = uni(wave_or(mf));
+    mb = uni(wave_or(mb));
+    if ((mf | mb) && lane() == 0) {
+        W.misc[1] |= (int32_t)mf;
+        W.misc[2] |= (int32_t)mb;
+    }
+}
+
+template <int RG, typename WT, class WS>
+__device__ __forceinline__ bool bf_converge_wl(const SubNet &N, const WS &W, int nct, int nz, int mode,
+                                               const ChainRegs<RG, WT> &C, uint32_t df, uint32_t db) {
+    static_assert(RG <= 16, "group masks are 16 bits");
+    using KT = typename WS::Key;
+    constexpr KT kKInf = WS::kKInf;
+    const int n = N.n;
+    const int G = (nct + kWave - 1) / kWave;
+    const uint32_t all = G >= 16 ? 0xFFFFu : ((1u << G) - 1u);
+    df &= all;
+    db &= all;
+    auto reg_w = [&](WT w) -> KT { return sizeof(WT) == sizeof(KT) ? (KT)w : (KT)(((int64_t)w << WS::kHop) + 1); };
+    for (int it = 0; it < 2 * (n + 4); it++) {
+        if (lane() == 0) W.misc[5]++;   // passes (io.wstat)
+        bool lowered = false;            // uniform: some key fell in this iteration
+        // the wave's lowered keys -> groups to (re)relax
+        auto note = [&](bool c, uint32_t iv) {
+            if (__ballot(c)) {
+                const uint32_t mo = uni(wave_or(c ? iv : 0u));
+                df |= mo & 0xFFFFu;
+                db |= mo >> 16;
+                lowered = true;
+            }
+        };
+        auto arc = [&](uint32_t th, KT w, bool exists, bool forward) {
+            const int t = (int)(th & 0xFFFFu), h = (int)(th >> 16);
+            const int u = forward ? t : h, v = forward ? h : t;
+            const KT ku = W.key[u], kv = W.key[v];
+            const uint32_t iv = W.inc[v];
+            sched_fence();
+            const KT nk = ku + w;
+            const bool c = exists & (ku < kKInf) & (nk < kv);
+            if (c) __hip_atomic_fetch_min(&W.key[v], nk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            note(c, iv);
+        };
+        // Z_out -> sources (SSP) / Z -> every free node (potentials), cost 0
+        {
+            const KT kz = W.key[n];
+            bool c = false;
+            uint32_t iv = 0;
+            if (kz < kKInf)
+                for (int i = lane(); i < nz; i += kWave) {
+                    const uint32_t e = (uint32_t)W.zlist[i];
+                    const int v = (int)(e & 0x1FFFFFFFu);
+                    if (mode != kSsp || ((e >> 30) & 1u)) {
+                        const KT kv = W.key[v];
+                        const uint32_t i2 = W.inc[v];
+                        sched_fence();
+                        if (kz + 1 < kv) {
+                            __hip_atomic_fetch_min(&W.key[v], (KT)(kz + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            c = true;
+                            iv |= i2;
+                        }
+                    }
+                }
+            note(c, iv);
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int g = 0; g < RG; g++) {
+            if (g < G && ((df >> g) & 1u)) {
+                df &= ~(1u << g);
+#ifdef SGUFP_SUB_TRACE
+                if (lane() == 0) W.misc[7]++;   // groups relaxed
+#endif
+                arc(C.th[g], reg_w(C.wf[g]), (C.fmask >> g) & 1ull, true);
+            }
+        }
+        // sinks -> Z_in (SSP) / free nodes -> Z (potentials), cost 0 (Z_in has no out-arc; Z's
+        // arcs out are the list above)
+        {
+            bool c = false;
+            for (int i = lane(); i < nz; i += kWave) {
+                const uint32_t e = (uint32_t)W.zlist[i];
+                const int v = (int)(e & 0x1FFFFFFFu);
+                const KT kv = W.key[v];
+                if (kv >= kKInf) continue;
+                const int z = mode == kSsp ? n + 1 : n;
+                if (mode == kSsp && !((e >> 29) & 1u)) continue;
+                if (kv + 1 < W.key[z]) {
+                    __hip_atomic_fetch_min(&W.key[z], (KT)(kv + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    c = true;
+                }
+            }
+            if (__ballot(c)) lowered = true;
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int g = RG - 1; g >= 0; g--) {
+            if (g < G && ((db >> g) & 1u)) {
+                db &= ~(1u << g);
+#ifdef SGUFP_SUB_TRACE
+                if (lane() == 0) W.misc[7]++;
+#endif
+                arc(C.th[g], reg_w(C.wb[g]), (C.bmask >> g) & 1ull, false);
+            }
+        }
+        if (!lowered) return true;
+        wave_lds_sync();
+    }
+    return false;
+}
+
 // Predecessors of the SSP labels: the smallest arc code among the residual arcs into each
 // node that are tight in (cost, hops).  Hops grow by one along such arcs, so the
 // predecessor graph has no cycle and the walk from Z_in ends at Z_out.
@@ -637,7 +777,22 @@ __device__ __forceinline__ bool bellman_ford(const SubNet &N, const WS &W, int n
     ChainRegs<RG, WT> C;
     load_chain_regs<RG, WT, NW>(W, N.n, nct, mode, M, C);
     B::sync();
-    const bool converged = bf_converge<RG, WT, NW>(N, W, nct, nz, mode, M, C);
+    bool converged;
+    if constexpr (NW == 1 && WS::kWL) {
+        // a warm start resumes from the groups its callers marked (wl_mark), a cold one
+        // relaxes every group; the marks restart for the next call
+        uint32_t df = 0xFFFFu, db = 0xFFFFu;
+        if (warm) {
+            df = uni((uint32_t)W.misc[1]);
+            db = uni((uint32_t)W.misc[2]);
+        }
+        wave_lds_sync();
+        if (lane() == 0) { W.misc[1] = 0; W.misc[2] = 0; }
+        wave_lds_sync();
+        converged = bf_converge_wl<RG, WT>(N, W, nct, nz, mode, C, df, db);
+    } else {
+        converged = bf_converge<RG, WT, NW>(N, W, nct, nz, mode, M, C);
+    }
     if (!converged) return false;
     if (mode != kSsp) {
         // potentials; with preds (the warm start's repair): the tight in-arcs under the
@@ -727,8 +882,18 @@ __device__ __forceinline__ void invalidate_subtrees(const SubNet &N, const WS &W
         B::sync();
         if (!B::any(moved, W.red)) break;
     }
+    uint32_t mf = 0, mb = 0;   // work list: the arcs into a restarted node (forward: chains with
+                               // head v, backward: chains with tail v)
     for (int v = B::tid(); v < nn; v += B::T)
-        if (anc[v] & 0x8000u) W.key[v] = kKInf;
+        if (anc[v] & 0x8000u) {
+            W.key[v] = kKInf;
+            if constexpr (WS::kWL) {
+                const uint32_t iv = W.inc[v];
+                mf |= iv >> 16;
+                mb |= iv & 0xFFFFu;
+            }
+        }
+    if constexpr (WS::kWL) wl_mark(W, mf, mb);
     B::sync();
 }
 
@@ -797,6 +962,8 @@ __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nc
                     if (stage == 0 ? (v < n && cons(j) && imb[v] > 0) : v == n) k = 0;
                     W.key[v] = k;
                 }
+                if constexpr (WS::kWL)   // new keys everywhere: every group
+                    if (tid == 0) { W.misc[1] = 0xFFFF; W.misc[2] = 0xFFFF; }
                 B::sync();
                 fresh = false;
             }
@@ -863,6 +1030,7 @@ __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nc
                     continue;
                 }
                 B::sync();   // every lane read the imbalances before they change
+                uint32_t pm = 0;   // work list: the path's chains changed their residual arcs
                 for (int i = tid; i < plen; i += T) {
                     const int code = W.plist[i];
                     if (code >= 2 * m) continue;
@@ -872,7 +1040,9 @@ __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nc
                     const int64_t cap = (code & 1) ? x - L : U - x;
                     W.add_x(k, (int)((code & 1) ? -delta : delta));
                     if (cap == delta) W.key[(code & 1) ? ch_t(ca) : ch_h(ca)] = kKInf;   // segment used up
+                    pm |= 1u << ((k >> 6) & 31);
                 }
+                if constexpr (WS::kWL) wl_mark(W, pm, pm);
                 if (tid == 0) {
                     if (stage == 0) {
                         imb[src] -= (int32_t)delta;
@@ -888,10 +1058,19 @@ __device__ __forceinline__ bool warm_repair(const SubNet &N, const WS &W, int nc
             // a source reached from another source (cheaper than its own key 0) hangs in that
             // one's predecessor tree: when that source runs dry the invalidation drops it too,
             // so every remaining source (and Z) restarts from 0 at most
+            uint32_t mf = 0, mb = 0;   // work list: the arcs out of a re-seeded source
             for (int v = tid, j = 0; v <= n; v += T, j++) {
                 const bool src = stage == 0 ? (v < n && cons(j) && imb[v] > 0) : v == n;
-                if (src && W.key[v] > (KT)0) W.key[v] = (KT)0;
+                if (src && W.key[v] > (KT)0) {
+                    W.key[v] = (KT)0;
+                    if constexpr (WS::kWL) {
+                        const uint32_t iv = W.inc[v];
+                        mf |= iv & 0xFFFFu;
+                        mb |= iv >> 16;
+                    }
+                }
             }
+            if constexpr (WS::kWL) wl_mark(W, mf, mb);
             B::sync();
             WR_T(2);
         }
@@ -1114,8 +1293,9 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
     const int p = blockIdx.x / S, s = blockIdx.x - p * S;
     if (p >= io.n_paths) return;
     size_t off[kSubLdsParts];
-    sub_lds_layout(N.n, N.m, io.nct_cap, N.nz, NW, off, (int)sizeof(KT), WARM);
+    sub_lds_layout(N.n, N.m, io.nct_cap, N.nz, NW, off, (int)sizeof(KT), WARM, WS::kWL);
     WS W;
+    W.inc = (LDS uint32_t *)(smem + off[11]);
     W.imb = (LDS int32_t *)(smem + off[0]);
     W.cta = (LDS uint64_t *)(smem + off[1]);
     W.ctb = (LDS typename WS::CBT *)(smem + off[2]);
@@ -1190,6 +1370,20 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
     }
     first_bad = B::all(first_bad, [](int x, int y) { return x < y ? x : y; }, W.red);
     B::sync();
+    if constexpr (WS::kWL) {
+        // work list: per node the groups of the complete chains out of it / into it
+        for (int v = tid; v < n + 2; v += T) W.inc[v] = 0;
+        B::sync();
+        for (int k = tid; k < nct; k += T) {
+            const uint64_t ca = W.ra(k);
+            const int t = ch_t(ca), h = ch_h(ca);
+            if (t >= 0 && h >= 0) {
+                __hip_atomic_fetch_or(&W.inc[t], 1u << (k >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_or(&W.inc[h], 1u << (16 + (k >> 6)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        B::sync();
+    }
     // The reference returns at the first infeasible scenario (grb.cpp:284-351): only its ray
     // reaches the cut.  A scenario infeasible up front records itself in first_inf[p]; one that
     // finds an earlier infeasible scenario of its path recorded stops (kSubSkipped), here or
@@ -1387,6 +1581,7 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
             }
             delta = B::all(delta, [](int64_t p, int64_t q) { return p < q ? p : q; }, W.red);
             if (plen < 0 || delta <= 0 || delta >= kInf) { status = kSubError; err_site = plen < 0 ? 3 : 4; break; }
+            uint32_t pm = 0;   // work list: the path's chains changed their residual arcs
             for (int i = tid; i < plen; i += T) {
                 const int code = W.plist[i];
                 if (code >= 2 * m) continue;
@@ -1396,7 +1591,9 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
                 const int64_t cap = (code & 1) ? (x > L ? x - L : x) : (x < L ? L - x : U - x);
                 W.add_x(k, (int)((code & 1) ? -delta : delta));
                 if (cap == delta) W.key[(code & 1) ? ch_t(ca) : ch_h(ca)] = WS::kKInf;   // segment used up
+                pm |= 1u << ((k >> 6) & 31);
             }
+            if constexpr (WS::kWL) wl_mark(W, pm, pm);
             B::sync();
             SUB_T1(t_walk);
             SUB_T0();
@@ -1409,8 +1606,8 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
         }
 #ifdef SGUFP_SUB_TRACE
         if (blockIdx.x % 997 == 0 && tid == 0)
-            printf("SUB blk=%d nct=%d nz=%d aug=%d bf=%d passes=%d ticks=%llu t_bf=%llu t_pred=%llu t_walk=%llu\n",
-                   (int)blockIdx.x, nct, nz, iters, nbf, W.misc[5], (unsigned long long)(wall_clock64() - tr0),
+            printf("SUB blk=%d nct=%d nz=%d aug=%d bf=%d passes=%d groups=%d ticks=%llu t_bf=%llu t_pred=%llu t_walk=%llu\n",
+                   (int)blockIdx.x, nct, nz, iters, nbf, W.misc[5], W.misc[7], (unsigned long long)(wall_clock64() - tr0),
                    (unsigned long long)t_bf, (unsigned long long)t_pred, (unsigned long long)t_walk);
 #endif
         if (skipped) {
@@ -1747,9 +1944,9 @@ hipError_t launch_warm_pick(const SubIO &io, const WarmRing &wr, int ptr, hipStr
 }
 
 // ---------------------------------------------------------------------------------------
-size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw, int kbytes, bool warm) {
+size_t sub_lds_bytes(int n, int m, int nct_cap, int nz, int nw, int kbytes, bool warm, bool wl) {
     size_t off[kSubLdsParts];
-    return sub_lds_layout(n, m, nct_cap, nz, nw, off, kbytes, warm);
+    return sub_lds_layout(n, m, nct_cap, nz, nw, off, kbytes, warm, wl);
 }
 
 namespace {
@@ -1757,7 +1954,13 @@ template <typename KT, bool WARM>
 hipError_t launch_scenarios(const SubNet &N, const SubIO &io, hipStream_t st) {
     constexpr int kb = (int)sizeof(KT);
     constexpr bool kw = WARM;   // the warm layout (k_sub_scenario's)
-    size_t lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, 1, kb, kw);
+    size_t lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, 1, kb, kw, false);
+    // the single-wave kernels with every chain group in registers carry the work-list table
+#ifdef SGUFP_SUB_WL
+    const size_t lds_wl = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, 1, kb, kw, true);
+#else
+    const size_t lds_wl = lds;
+#endif
 #ifdef SGUFP_SUB_LDS_MIN
     if (lds < SGUFP_SUB_LDS_MIN) lds = SGUFP_SUB_LDS_MIN;   // occupancy experiments
 #endif
@@ -1765,11 +1968,11 @@ hipError_t launch_scenarios(const SubNet &N, const SubIO &io, hipStream_t st) {
     // LDS allows at most two scenarios per CU (in its own layout: the single-wave 8-byte
     // records would bring C5 under the bar and back to one wave per scenario, 4x slower) and
     // the big-M costs fit 32 bits (host bound)
-    const bool large = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, kLargeWaves, kb, false) > 64 * 1024 &&
+    const bool large = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, kLargeWaves, kb, false, false) > 64 * 1024 &&
                        io.nct_cap > kRegGroupsSmall * kWave && N.cost_bound < ((int64_t)1 << 30);
     const char *ev = getenv("SGUFP_SUB_WAVES");
     if (large && !(ev && atoi(ev) == 1)) {
-        lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, kLargeWaves, kb, kw);
+        lds = sub_lds_bytes(N.n, N.m, io.nct_cap, N.nz, kLargeWaves, kb, kw, false);
         if (io.nct_cap <= kRegGroupsLarge * kLargeWaves * kWave && !N.preds_lds)
             hipLaunchKernelGGL((k_sub_scenario<kRegGroupsLarge, int32_t, kLargeWaves, KT, true, WARM>),
                                dim3((unsigned)io.n_paths * N.S), dim3(kWave * kLargeWaves), lds, st, N, io);
@@ -1780,11 +1983,11 @@ hipError_t launch_scenarios(const SubNet &N, const SubIO &io, hipStream_t st) {
         // warm starts: the repair's code needs registers too; 13 groups (the 1k-arc networks'
         // ~800 chains) keep the all-in-registers kernel without the 16-group one's spills
         hipLaunchKernelGGL((k_sub_scenario<kRegGroupsWarm, KT, 1, KT, true, WARM>), dim3((unsigned)io.n_paths * N.S),
-                           dim3(kWave), lds, st, N, io);
+                           dim3(kWave), lds_wl, st, N, io);
     } else if (io.nct_cap <= kRegGroupsSmall * kWave && !N.preds_lds) {
         // register groups hold key increments: 64-bit with 64-bit keys, 32-bit with 32-bit keys
         hipLaunchKernelGGL((k_sub_scenario<kRegGroupsSmall, KT, 1, KT, true, WARM>), dim3((unsigned)io.n_paths * N.S),
-                           dim3(kWave), lds, st, N, io);
+                           dim3(kWave), lds_wl, st, N, io);
     } else {
         hipLaunchKernelGGL((k_sub_scenario<kRegGroupsSmall, KT, 1, KT, false, WARM>), dim3((unsigned)io.n_paths * N.S),
                            dim3(kWave), lds, st, N, io);

@@ -379,8 +379,9 @@ def test_warm_start_with_lower_bounds(cfg, seed, S, n_paths, lib, tmp_path):
     assert feas.any()
     if cfg != "C5":   # (C5's random matchings are mostly feasible: its 8-wave kernel is the point there)
         assert (~feas).any(), "the case should hold feasible and infeasible scenarios"
-    np.testing.assert_array_equal(r["obj"][feas], r["cold_obj"][feas])
-    np.testing.assert_array_equal(r["dual"][feas], r["obj"][feas])
+    obj, cobj, dual = r["obj"].reshape(-1), r["cold_obj"].reshape(-1), r["dual"].reshape(-1)
+    np.testing.assert_array_equal(obj[feas], cobj[feas])
+    np.testing.assert_array_equal(dual[feas], obj[feas])
     np.testing.assert_array_equal(r["typ"], r["cold_typ"])
     for k in range(n_paths):
         if r["typ"][k] == 0:
