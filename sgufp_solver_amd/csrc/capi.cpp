@@ -478,6 +478,15 @@ bool sgufp_ctx::emit_current(const BatchIn &in, const Pool &p) {
                          ex.nsc, ex.lazy, c[4], c[5], c[6], c[7], c[9] & 1023, (c[9] >> 10) & 1023, (c[9] >> 20) & 1023,
                          (c[9] >> 30) & 1023, (c[9] >> 40) & 1023, c[12], c[15], c[14], c[13], ex.leaf_split, c[18],
                          c[19]);
+        if (estats && ex.enabled && download(c, d_ectr, 32) && sync()) {
+            // the leaf passes' algorithmic bytes, summed over the context's launches: per swept cut
+            // block of a pass, its staged coefficient rows and the root-fold column (64 cuts x 8 B each)
+            leaf_cum[0] += c[21];
+            leaf_cum[1] += c[20];
+            std::fprintf(stderr, "[exact-cum] leaf pass-blocks %llu row-blocks %llu bytes %.6e\n",
+                         (unsigned long long)leaf_cum[0], (unsigned long long)leaf_cum[1],
+                         (double)(leaf_cum[0] + leaf_cum[1]) * 64.0 * 8.0);
+        }
     }
     total_children = (int64_t)tot[0];
     total_csol = (int64_t)tot[1];

@@ -187,7 +187,7 @@ struct LeafSharedT {
     int32_t stab[ROWS];                  // their slots (-1: no coefficient)
     LeafWave lw[kLeafWaves];
     double vb[kLeafWaves][kExactMaxT - 1][kWave];   // ancestor values of the current leaf (layers 0 .. T - 2), per wave
-    int32_t item, flags[kLeafWaves];
+    int32_t item, flags[2][kLeafWaves];   // per block, double-buffered (exact entries: one barrier fewer)
     uint32_t rmask[2];                   // rows (layer, rank) some leaf of the pass adds a coefficient of
 };
 
@@ -210,11 +210,23 @@ __device__ __forceinline__ double vmin64(double a, double b) {
 
 // ancestors of leaf j (wave-local) from layer dj down to the leaf's parent, values in vb;
 // returns the parent value
+#ifndef SGUFP_LEAF_INFOREG
+#define SGUFP_LEAF_INFOREG 1   // the walk's per-layer info bytes from registers (v_readlane), not LDS
+#endif
 template <class LeafShared>
-__device__ __forceinline__ double walk_down(LeafShared &S, int w, int j, int dj, int T, int us, double root) {
+__device__ __forceinline__ double walk_down(LeafShared &S, int w, int j, int dj, int T, int us, double root, uint32_t ilo,
+                                            uint32_t ihi) {
     double prev = (dj <= 1) ? root : S.vb[w][dj - 1][lane()];
     for (int k = dj; k < T - 1; k++) {
+#if SGUFP_LEAF_INFOREG
+        static_assert(kExactMaxT <= 9, "layers 1-8 in two packed words");
+        // lane j packs leaf j's info bytes of layers 1-4 (ilo) and 5-7 (ihi): a scalar read with
+        // no LDS round trip before the coefficient's
+        const uint32_t src = k <= 4 ? ilo : ihi;
+        const uint32_t b = ((uint32_t)__builtin_amdgcn_readlane((int)src, j) >> (8 * ((k - 1) & 3))) & 0xFFu;
+#else
         const uint32_t b = uni((uint32_t)S.lw[w].info[j][k]);
+#endif
         const uint32_t r = b & 63u;
         const double x = !(b & 128u) ? EDMIN : (r ? prev + S.C[(k - 1) * us + r][lane()] : prev);
         S.vb[w][k][lane()] = x;
@@ -257,6 +269,10 @@ __device__ double first_zero(const NetDev &net, const ExactIO &ex, LeafShared &S
 #ifndef SGUFP_LEAF_ROWMASK
 #define SGUFP_LEAF_ROWMASK 1   // stage only the rows the pass's leaves add (0: all rows, A/B)
 #endif
+#ifndef SGUFP_LEAF_LASTREG
+#define SGUFP_LEAF_LASTREG 0   // 1: the last layer's rows of a block in registers (measured slower)
+#endif
+constexpr int kLastRegs = 4;   // ranks 1 .. 4 (C3 / C4 trees: 3; higher ranks read LDS)
 #ifndef SGUFP_LEAF_MIN_WAVES
 #define SGUFP_LEAF_MIN_WAVES 6   // three 8-wave workgroups per CU (VGPRs <= 85)
 #endif
@@ -385,6 +401,20 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
             if (j < cnt) S.lw[w].dv[j] = (uint8_t)((j == 0) ? 1 : dv);
             alive = (uint32_t)__ballot(j < cnt && al);
         }
+        // leaf j's info bytes in lane j's registers (walk_down reads them with v_readlane)
+        uint32_t ilo = 0, ihi = 0;
+#if SGUFP_LEAF_INFOREG
+        if (lane() < kLeavesPerWave) {
+#pragma unroll
+            for (int k = 1; k < kExactMaxT; k++) {
+                if (k < T) {
+                    const uint32_t b = (uint32_t)S.lw[w].info[lane()][k];
+                    if (k <= 4) ilo |= b << (8 * (k - 1));
+                    else ihi |= b << (8 * (k - 5));
+                }
+            }
+        }
+#endif
         __syncthreads();
         // per leaf, in scalar registers for the whole pass: 16 bits = the LDS row of its
         // last-layer coefficient (bits 0-6; kRowNoAdd: a -1 decision, kRowDead: in-arc dead) |
@@ -497,6 +527,14 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
             const bool vc = s < ncut && s >= first;
             double ms = -INFINITY;   // non-exact: max over this wave's alive leaves, this lane's cut
             if (cnt > 0 && (nx || (done & alive) != alive)) {
+#if SGUFP_LEAF_LASTREG
+                // the last layer's rows (ranks 1 .. kLastRegs) of this block in registers, read once:
+                // a leaf's own coefficient is then a select, not an LDS round trip per leaf
+                const int lrow1 = (T - 2) * us + 1;
+                double cl[kLastRegs];
+#pragma unroll
+                for (int q = 0; q < kLastRegs; q++) cl[q] = (q + 1 < us) ? S.C[lrow1 + q][lane()] : 0.0;
+#endif
                 // exact entries: a lane past the pool's end starts at +inf, so its values leave every
                 // running minimum alone (a dead path gives DOUBLE_MIN on every lane, valid or not)
                 // and the leaf loop below needs no per-lane condition -- no exec-mask switching
@@ -535,14 +573,29 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
                             for (int k = 1; k < kExactMaxT - 1; k++) par = (k == T - 2) ? anc[k] : par;
                         }
 #else
-                        if (dj < T - 1 || j == 0) par = walk_down(S, w, j, dj, T, us, root);
+                        if (dj < T - 1 || j == 0) par = walk_down(S, w, j, dj, T, us, root, ilo, ihi);
 #endif
                         if ((need >> j) & 1u) {
                             const uint32_t row = x & 0x7Fu;
                             double v;
                             if (row == kRowDead) v = EDMIN;
                             else if (row == kRowNoAdd) v = par;
-                            else v = par + S.C[row][lane()];
+                            else {
+#if SGUFP_LEAF_LASTREG
+                                const uint32_t q = row - (uint32_t)lrow1;   // rank - 1 (wave-uniform)
+                                double c;
+                                if (q < (uint32_t)kLastRegs) {
+                                    c = cl[0];
+#pragma unroll
+                                    for (int qq = 1; qq < kLastRegs; qq++) c = (q == (uint32_t)qq) ? cl[qq] : c;
+                                } else {
+                                    c = S.C[row][lane()];
+                                }
+                                v = par + c;
+#else
+                                v = par + S.C[row][lane()];
+#endif
+                            }
                             if (nx) {
                                 if (!ph2 && vc && ((open >> j) & 1u)) m[j] = rmin(m[j], v);
                             } else if ((open >> j) & 1u) {
@@ -576,18 +629,21 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
                 }
             }
             if (nx) S.vb[w][0][lane()] = ms;   // free until the next block's walks
-            if (lane() == 0) S.flags[w] = ((done & alive) == alive) ? 1 : 0;
+            if (lane() == 0) S.flags[bb & 1][w] = ((done & alive) == alive) ? 1 : 0;
             __syncthreads();
             int all = 1;
 #pragma unroll
-            for (int q = 0; q < kLeafWaves; q++) all &= S.flags[q];
+            for (int q = 0; q < kLeafWaves; q++) all &= S.flags[bb & 1][q];
             if (nx && w == 0 && vc) {
                 double mx = -INFINITY;
 #pragma unroll
                 for (int q = 0; q < kLeafWaves; q++) mx = S.vb[q][0][lane()] > mx ? S.vb[q][0][lane()] : mx;
                 if (mx != -INFINITY) atomicMax(&ex.MS[(size_t)i * ex.ostride + s], nx_key(mx));
             }
-            __syncthreads();
+            // exact entries: the barrier above already found every wave done with this block's
+            // coefficients (the next block's are stored after it) and the flags alternate
+            // buffers, so only the non-exact maxState (vb, rewritten by the next walks) waits here
+            if (nx) __syncthreads();
             if (all && !ph2) {
                 finished = true;
                 break;
@@ -608,7 +664,13 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
         // phase A with blocks left: the open leaves' partial minima go to tw and the leaves to
         // the record's open list (no zero re-scan yet: phase B decides the final value)
         const bool to_b = split && !pb && !finished && bsplit < nlim;
-        if (tid == 0) atomicAdd(&ex.ctr[pb ? 19 : 3], (unsigned long long)max(0, nb_done - (pb ? bsplit : 0)));   // diagnostics: cut blocks swept
+        if (tid == 0) {   // diagnostics: cut blocks swept; staged row-blocks (the byte model)
+            const int nbs_item = max(0, nb_done - bfrom);   // (phase B: bfrom = bsplit)
+            atomicAdd(&ex.ctr[pb ? 19 : 3], (unsigned long long)max(0, nb_done - (pb ? bsplit : 0)));
+            const uint64_t rm = (uint64_t)S.rmask[0] | (uint64_t)S.rmask[1] << 32;
+            atomicAdd(&ex.ctr[20], (unsigned long long)(SGUFP_LEAF_ROWMASK ? __popcll(rm) : E) * (unsigned long long)nbs_item);
+            atomicAdd(&ex.ctr[21], (unsigned long long)nbs_item);
+        }
         // terminal weights: min over the lanes
         uint32_t openb = 0;
 #pragma unroll

@@ -82,8 +82,13 @@ struct SubLds {
     // every chain group in registers (<= 16 groups)
 #ifdef SGUFP_SUB_WL
     static constexpr bool kWL = ALLREG && PACK;
+    // 2: a group with a lowered key marks its precomputed successor groups (all the groups of
+    // the arcs out of the group's heads / tails: a superset, no per-lane mask or wave OR);
+    // 1: the exact groups of the lowered keys (an LDS table read per arc, a wave OR per group)
+    static constexpr bool kCoarse = SGUFP_SUB_WL == 2;
 #else
     static constexpr bool kWL = false;   // full sweeps (the work list measured slower)
+    static constexpr bool kCoarse = false;
 #endif
     LDS uint32_t *inc;      // [n+2] kWL: groups with a chain out of v (bits 0-15) / into v (16-31)
     static constexpr int kHop = KeyT<KT>::hop_bits;
@@ -219,7 +224,7 @@ __host__ __device__ inline size_t sub_lds_layout(int n, int m, int nct_cap, int 
     off[6] = o; o = a16(o + (size_t)nz * 4);
     off[7] = o; o = a16(o + 8 * 4);
     off[10] = o; o = a16(o + (nw > 1 ? 8 * 8 : 0));   // red
-    off[11] = o; o = a16(o + (wl ? (size_t)(n + 2) * 4 : 0));   // inc (work-list Bellman-Ford)
+    off[11] = o; o = a16(o + (wl ? (size_t)(n + 2 + 32) * 4 : 0));   // inc + group successors (work list)
 #ifdef SGUFP_SUB_VERIFY
     off[9] = o; o = a16(o + (size_t)(n + 2) * kbytes);
 #endif
@@ -610,6 +615,13 @@ __device__ __forceinline__ bool bf_converge_wl(const SubNet &N, const WS &W, int
     df &= all;
     db &= all;
     auto reg_w = [&](WT w) -> KT { return sizeof(WT) == sizeof(KT) ? (KT)w : (KT)(((int64_t)w << WS::kHop) + 1); };
+    // coarse marks: lane g holds group g's successor masks (forward arcs: the groups of the arcs
+    // out of its heads; backward arcs: out of its tails), wave-uniform through readlane
+    uint32_t sucF = 0, sucB = 0;
+    if constexpr (WS::kCoarse) {
+        sucF = lane() < 16 ? W.inc[n + 2 + lane()] : 0u;
+        sucB = lane() < 16 ? W.inc[n + 2 + 16 + lane()] : 0u;
+    }
     for (int it = 0; it < 2 * (n + 4); it++) {
         if (lane() == 0) W.misc[5]++;   // passes (io.wstat)
         bool lowered = false;            // uniform: some key fell in this iteration
@@ -622,16 +634,27 @@ __device__ __forceinline__ bool bf_converge_wl(const SubNet &N, const WS &W, int
                 lowered = true;
             }
         };
-        auto arc = [&](uint32_t th, KT w, bool exists, bool forward) {
+        auto arc = [&](uint32_t th, KT w, bool exists, bool forward, int g) {
             const int t = (int)(th & 0xFFFFu), h = (int)(th >> 16);
             const int u = forward ? t : h, v = forward ? h : t;
             const KT ku = W.key[u], kv = W.key[v];
-            const uint32_t iv = W.inc[v];
+            uint32_t iv = 0;
+            if constexpr (!WS::kCoarse) iv = W.inc[v];
             sched_fence();
             const KT nk = ku + w;
             const bool c = exists & (ku < kKInf) & (nk < kv);
             if (c) __hip_atomic_fetch_min(&W.key[v], nk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            note(c, iv);
+            if constexpr (WS::kCoarse) {
+                // (readfirstlane keeps df / db in scalar registers: the group tests stay scalar
+                // branches, not exec-mask regions)
+                const uint32_t any = uni((uint32_t)(__ballot(c) != 0));
+                const uint32_t mo = any ? (uint32_t)__builtin_amdgcn_readlane((int)(forward ? sucF : sucB), g) : 0u;
+                df = uni(df | (mo & 0xFFFFu));
+                db = uni(db | (mo >> 16));
+                lowered = lowered || any;
+            } else {
+                note(c, iv);
+            }
         };
         // Z_out -> sources (SSP) / Z -> every free node (potentials), cost 0
         {
@@ -658,12 +681,12 @@ __device__ __forceinline__ bool bf_converge_wl(const SubNet &N, const WS &W, int
         wave_lds_sync();
 #pragma unroll
         for (int g = 0; g < RG; g++) {
-            if (g < G && ((df >> g) & 1u)) {
-                df &= ~(1u << g);
+            if (g < G && ((uni(df) >> g) & 1u)) {
+                df = uni(df & ~(1u << g));
 #ifdef SGUFP_SUB_TRACE
                 if (lane() == 0) W.misc[7]++;   // groups relaxed
 #endif
-                arc(C.th[g], reg_w(C.wf[g]), (C.fmask >> g) & 1ull, true);
+                arc(C.th[g], reg_w(C.wf[g]), (C.fmask >> g) & 1ull, true, g);
             }
         }
         // sinks -> Z_in (SSP) / free nodes -> Z (potentials), cost 0 (Z_in has no out-arc; Z's
@@ -687,12 +710,12 @@ __device__ __forceinline__ bool bf_converge_wl(const SubNet &N, const WS &W, int
         wave_lds_sync();
 #pragma unroll
         for (int g = RG - 1; g >= 0; g--) {
-            if (g < G && ((db >> g) & 1u)) {
-                db &= ~(1u << g);
+            if (g < G && ((uni(db) >> g) & 1u)) {
+                db = uni(db & ~(1u << g));
 #ifdef SGUFP_SUB_TRACE
                 if (lane() == 0) W.misc[7]++;
 #endif
-                arc(C.th[g], reg_w(C.wb[g]), (C.bmask >> g) & 1ull, false);
+                arc(C.th[g], reg_w(C.wb[g]), (C.bmask >> g) & 1ull, false, g);
             }
         }
         if (!lowered) return true;
@@ -1383,6 +1406,23 @@ __global__ void __launch_bounds__(kWave * NW, NW == 1 ? (sizeof(KT) == 4 ? 4 : 3
             }
         }
         B::sync();
+        if constexpr (WS::kCoarse) {
+            // per group: the groups of the arcs out of its chains' heads (a forward relaxation
+            // lowers a head) and out of their tails (a backward one lowers a tail)
+            for (int g = 0; g * kWave < nct; g++) {
+                const int k = g * kWave + lane();
+                uint32_t mh = 0, mt = 0;
+                if (k < nct) {
+                    const uint64_t ca = W.ra(k);
+                    const int t = ch_t(ca), h = ch_h(ca);
+                    if (t >= 0 && h >= 0) { mh = W.inc[h]; mt = W.inc[t]; }
+                }
+                mh = uni(wave_or(mh));
+                mt = uni(wave_or(mt));
+                if (lane() == 0) { W.inc[n + 2 + g] = mh; W.inc[n + 2 + 16 + g] = mt; }
+            }
+            B::sync();
+        }
     }
     // The reference returns at the first infeasible scenario (grb.cpp:284-351): only its ray
     // reaches the cut.  A scenario infeasible up front records itself in first_inf[p]; one that

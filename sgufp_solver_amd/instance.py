@@ -54,6 +54,10 @@ CONFIGS = {
     # (64 scenarios) at a size that finishes; C3 itself closes neither
     "M1": InstanceConfig("M1", 60, 4, 6, 2, 0.5, 64),
     "M2": InstanceConfig("M2", 100, 5, 8, 2, 0.4, 64),
+    # P1 / P3: between T4 and M1, generated lower bounds kept -- 64-scenario instances whose
+    # extensive form (HiGHS) and device B&B both close (tools/closure_study.py)
+    "P1": InstanceConfig("P1", 48, 4, 6, 2, 0.45, 64),
+    "P3": InstanceConfig("P3", 52, 4, 6, 2, 0.5, 64),
     "C1": InstanceConfig("C1", 40, 3, 6, 2, 1.0, 1),
     "C2": InstanceConfig("C2", 200, 6, 12, 3, 0.5, 1),
     "C3": InstanceConfig("C3", 1000, 12, 30, 3, 0.3, 64),

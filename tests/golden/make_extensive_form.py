@@ -15,7 +15,9 @@ from oracle import extensive_form as ef  # noqa: E402
 from sgufp_solver_amd import instance  # noqa: E402
 
 # (config, seed, scenarios)
-CASES = [("C1", 1, 1), ("C1", 2, 1), ("C1", 3, 1), ("C1", 4, 2), ("C1", 5, 3), ("C2", 1, 1), ("C2", 3, 2)]
+CASES = [("C1", 1, 1), ("C1", 2, 1), ("C1", 3, 1), ("C1", 4, 2), ("C1", 5, 3), ("C2", 1, 1), ("C2", 3, 2),
+         # 64 scenarios, generated lower bounds (the closure study's instances between T4 and M1)
+         ("P1", 1, 64), ("P1", 3, 64), ("P3", 2, 64), ("P3", 3, 64)]
 # lower bounds 0 (suffix "z"): the 64-scenario end-to-end case of tests/test_bnb.py
 CASES_LB0 = [("T4", 1, 64)]
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "extensive_form.json")
