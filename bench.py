@@ -292,7 +292,66 @@ def bnb_profile_block(tag: str):
         out["issue_source"] = (f"profiles/{tag}_bnbs_pmc_issue (rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY "
                                f"SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS "
                                f"SQ_LDS_BANK_CONFLICT, same command and library; wave cycles in quad-cycles)")
+    leaf = leaf_roofline(tag, top[0][0], shares.get(top[0][0], 0.0), d)
+    if leaf:
+        out["dominant_roofline"] = leaf
     out["bound"] = "issue/latency (waves parked on dependent LDS / memory round trips; see issue)"
+    return out
+
+
+def _exact_cum(path):
+    """The last [exact-cum] line of a log (SGUFP_EXACT_STATS=1): (pass-blocks, row-blocks, bytes)."""
+    last = None
+    if os.path.exists(path):
+        with open(path, errors="replace") as fh:
+            for ln in fh:
+                if ln.startswith("[exact-cum]"):
+                    last = ln.split()
+    if not last:
+        return None
+    return int(last[3]), int(last[5]), float(last[7])
+
+
+def leaf_roofline(tag: str, kernel: str, kernel_ns: float, stats_dir: str):
+    """Roofline of the seeded leg's dominant kernel when it is the exact leaf passes
+    (k_exact_leaf): algorithmic bytes = per swept 64-cut block of a pass its staged coefficient
+    rows plus the root-fold column, 64 x 8 B each (the kernel's own counters, summed over the leg:
+    SGUFP_EXACT_STATS [exact-cum] in the stats run's log), over the kernel's total time in the same
+    run; HBM traffic per pass-block from the FETCH_SIZE / WRITE_SIZE passes of the same command
+    (profiles/<tag>_bnbs_pmc_fetch / _write, each with its own [exact-cum] counts)."""
+    import csv
+    if "k_exact_leaf" not in kernel or kernel_ns <= 0:
+        return None
+    cum = _exact_cum(os.path.join(stats_dir, "exact_cum.log"))
+    if not cum:
+        return None
+    blocks, rows, model = cum
+    out = {"kernel": kernel, "model": "per pass-block: (staged rows + 1 root-fold column) x 64 cuts x 8 B",
+           "pass_blocks": blocks, "row_blocks": rows, "model_bytes": model,
+           "kernel_seconds": round(kernel_ns * 1e-9, 4),
+           "achieved": round(model / (kernel_ns * 1e-9) / 1e9, 2), "peak": 8000.0, "unit": "GB/s"}
+    out["frac"] = round(out["achieved"] / out["peak"], 4)
+    traffic = {}
+    for sub, name in (("bnbs_pmc_fetch", "FETCH_SIZE"), ("bnbs_pmc_write", "WRITE_SIZE")):
+        dp = os.path.join(ROOT, "profiles", f"{tag}_{sub}")
+        if profile_matches(dp) != "library":
+            return out
+        c2 = _exact_cum(os.path.join(dp, "exact_cum.log"))
+        kb = 0.0
+        for path in glob.glob(os.path.join(dp, "*counter_collection.csv")):
+            with open(path) as fh:
+                for r in csv.DictReader(fh):
+                    if kernel in r["Kernel_Name"] and r["Counter_Name"] == name:
+                        kb += float(r["Counter_Value"])
+        if not c2 or not c2[0] or not kb:
+            return out
+        traffic[name] = kb * 1024.0 * (FETCH_CORRECTION if name == "FETCH_SIZE" else 1.0) / c2[0]
+    per_block = traffic["FETCH_SIZE"] + traffic["WRITE_SIZE"]
+    out["traffic_bytes_per_pass_block"] = round(per_block, 1)
+    out["model_bytes_per_pass_block"] = round(model / blocks, 1)
+    out["traffic"] = round(per_block * blocks, 1)
+    out["traffic_source"] = (f"profiles/{tag}_bnbs_pmc_fetch / _write (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
+                             f"FETCH_SIZE x {FETCH_CORRECTION}), per pass-block of each run's own counters")
     return out
 
 

@@ -492,7 +492,7 @@ def check_large_pool(cfg: str, seed: int, width: int, min_opt_cuts: int, batch: 
 
 def check_nx_survivors(cfg: str, seed: int, pool_sizes=(20000, 100000), per_pool: int = 8, batch: int = 1024,
                        round_seconds: float = 5.0, max_seconds: float = 300.0, device: int = 0, threads: int = 0,
-                       need_rounds: int = 12, keep_lb: bool = False):
+                       need_rounds: int = 12, keep_lb: bool = False, round_iters: int = 2):
     """The survivor path of the non-exact cut-parallel phase at the pool sizes the timed B&B
     legs reach.  The UNSEEDED search of ``cfg`` (no incumbent: nothing is pruned by a bound, so
     the non-exact records of a round survive every cut and take the whole phase: k_nx_dag per
@@ -504,7 +504,15 @@ def check_nx_survivors(cfg: str, seed: int, pool_sizes=(20000, 100000), per_pool
     the pool -- status, exact flag, lb / ub bits, argmax path, every child, DD sizes
     (NodeExplorer.cpp:975-985, DD.cpp:3932-4023, 4179-4218) -- together with up to per_pool / 2
     records of each other route present (in-order, fall-back re-run).  The round then runs on
-    the same batch and its statuses must equal the device relaxation's."""
+    the same batch and its statuses must equal the device relaxation's.
+
+    The search's own closed loops soon set an incumbent, and a round's batch may then hold exact
+    records only.  So the survivors come from the first non-exact batch the search pushed (the
+    root's cutset children, kept from round 1): at each pool size they are relaxed with no
+    incumbent (DOUBLE_MIN, device and reference alike: every record survives every cut) and the
+    phase's survivors among them are compared.  ``round_iters`` caps the refinement iterations
+    per round (sgufp_bnb_set_limits) so that the pool passes each size gradually instead of in
+    one round of uncapped loops."""
     import time
     from sgufp_solver_amd import instance
     from sgufp_solver_amd.pools import DOUBLE_MAX, DOUBLE_MIN, NodeRecord
@@ -522,61 +530,61 @@ def check_nx_survivors(cfg: str, seed: int, pool_sizes=(20000, 100000), per_pool
     fail: List[str] = []
     rep = {"config": cfg, "seed": seed, "lower_bounds": "generated" if keep_lb else "zero", "rounds": 0,
            "pools": []}
+    early = None                         # the root's cutset children (non-exact), kept from round 1
     for target in pool_sizes:
         while eng.cuts_count(0) < target and eng.frontier_size() and time.perf_counter() - t0 < max_seconds:
-            eng.bnb_set_limits(0, round_seconds)
+            eng.bnb_set_limits(round_iters, round_seconds)
             z, _ = eng.bnb_step(z, batch)
             rep["rounds"] += 1
+            if early is None:
+                early = E.batch_to_records(snapshot_top(eng, batch))
         if eng.cuts_count(0) < target:
             fail.append(f"pool {target}: the search stopped at {eng.cuts_count(0)} optimality cuts")
             break
-        pick: List[int] = []
-        got_all = recs = routes = None
-        for attempt in range(need_rounds + 1):
-            snap = snapshot_top(eng, batch)
-            recs = E.batch_to_records(snap)
-            got_all = eng.relax(recs, z)
-            routes = eng.routes()
-            by = {r: [] for r in (E.ROUTE_IN_ORDER, E.ROUTE_EXACT_PHASE, E.ROUTE_NX_PHASE, E.ROUTE_NX_FALLBACK)}
-            surv = []
-            for k, g in enumerate(got_all):
-                if snap.ub[k] <= z:
-                    continue
-                if routes[k] == E.ROUTE_NX_PHASE and g.status == E.SUCCESS and not g.exact and g.children:
-                    surv.append(k)
+        # the next round's batch under the search's incumbent: the other routes
+        snap = snapshot_top(eng, batch)
+        recs = E.batch_to_records(snap)
+        got_all = eng.relax(recs, z)
+        routes = eng.routes()
+        by = {r: [] for r in (E.ROUTE_IN_ORDER, E.ROUTE_EXACT_PHASE, E.ROUTE_NX_PHASE, E.ROUTE_NX_FALLBACK)}
+        for k, g in enumerate(got_all):
+            if snap.ub[k] > z:
                 by[int(routes[k])].append(k)
-            if len(surv) >= per_pool or attempt == need_rounds or not eng.frontier_size():
-                break
-            eng.bnb_set_limits(0, round_seconds)
-            z, _ = eng.bnb_step(z, batch)
-            rep["rounds"] += 1
+        extra = []
+        for r in (E.ROUTE_IN_ORDER, E.ROUTE_NX_FALLBACK, E.ROUTE_EXACT_PHASE, E.ROUTE_NX_PHASE):
+            extra += by[r][:max(1, per_pool // 2)]
+        idx = sorted(set(extra))
+        # the survivors: the kept non-exact records with no incumbent
+        got_e = eng.relax(early, DOUBLE_MIN)
+        routes_e = eng.routes()
+        surv = [k for k, g in enumerate(got_e)
+                if routes_e[k] == E.ROUTE_NX_PHASE and g.status == E.SUCCESS and not g.exact and g.children]
         step = max(1, len(surv) // per_pool)
         pick = surv[::step][:per_pool]
-        extra = []
-        for r in (E.ROUTE_IN_ORDER, E.ROUTE_NX_FALLBACK, E.ROUTE_EXACT_PHASE):
-            extra += by[r][:max(1, per_pool // 2)]
-        idx = sorted(set(pick + extra))
         pool_path = os.path.join(work, f"pool_{target}.bin")
         total = write_pool_bin(pool_path, eng)
-        nodes = os.path.join(work, f"nodes_{target}.txt")
-        out = os.path.join(work, f"ref_{target}.txt")
-        pools.write_nodes(nodes, [recs[i] for i in idx])
         t1 = time.perf_counter()
-        subprocess.run([REF_BIN, "relaxp", net, pool_path, nodes, z.hex(), str(threads or _threads()), out], check=True,
-                       capture_output=True, timeout=1800)
-        want = pools.read_results(out)
-        got = [got_all[i] for i in idx]
-        bad = compare(got, want)
+        bad = []
+        for tag, zz, rs, gs in (("batch", z, [recs[i] for i in idx], [got_all[i] for i in idx]),
+                                ("survivors", DOUBLE_MIN, [early[i] for i in pick], [got_e[i] for i in pick])):
+            if not rs:
+                continue
+            nodes = os.path.join(work, f"nodes_{target}_{tag}.txt")
+            out = os.path.join(work, f"ref_{target}_{tag}.txt")
+            pools.write_nodes(nodes, rs)
+            subprocess.run([REF_BIN, "relaxp", net, pool_path, nodes, zz.hex(), str(threads or _threads()), out],
+                           check=True, capture_output=True, timeout=1800)
+            bad += [f"{tag}: {m}" for m in compare(gs, pools.read_results(out))]
         fail += [f"pool {target}: {m}" for m in bad[:10]]
-        n_ch = sum(len(got_all[i].children) for i in pick)
+        n_ch = sum(len(got_e[i].children) for i in pick)
         entry = {"target": target, "pool_optimality": eng.cuts_count(0), "pool_feasibility": eng.cuts_count(1),
                  "pool_total": total, "incumbent": z, "batch": len(recs),
                  "routes_in_batch": {name: len(by[r]) for name, r in (("in_order", E.ROUTE_IN_ORDER),
                                                                       ("exact_phase", E.ROUTE_EXACT_PHASE),
                                                                       ("nx_phase", E.ROUTE_NX_PHASE),
                                                                       ("nx_fallback", E.ROUTE_NX_FALLBACK))},
-                 "nx_survivors_in_batch": len(surv), "survivors_checked": len(pick), "children_checked": n_ch,
-                 "checked": len(idx), "mismatches": len(bad),
+                 "nx_survivors": len(surv), "survivor_candidates": len(early), "survivors_checked": len(pick),
+                 "children_checked": n_ch, "checked": len(idx) + len(pick), "mismatches": len(bad),
                  "reference_seconds": round(time.perf_counter() - t1, 2)}
         rep["pools"].append(entry)
         print(f"[nx survivors {cfg}] pool {entry['pool_optimality']}: routes {entry['routes_in_batch']} "

@@ -483,9 +483,11 @@ bool sgufp_ctx::emit_current(const BatchIn &in, const Pool &p) {
             // block of a pass, its staged coefficient rows and the root-fold column (64 cuts x 8 B each)
             leaf_cum[0] += c[21];
             leaf_cum[1] += c[20];
-            std::fprintf(stderr, "[exact-cum] leaf pass-blocks %llu row-blocks %llu bytes %.6e\n",
+            for (int x = 0; x < 3; x++) leaf_cum[2 + x] += c[22 + x];   // SGUFP_LEAF_CLOCKS builds
+            std::fprintf(stderr, "[exact-cum] leaf pass-blocks %llu row-blocks %llu bytes %.6e wave-cycles stage %llu "
+                                 "leaves %llu sync %llu\n",
                          (unsigned long long)leaf_cum[0], (unsigned long long)leaf_cum[1],
-                         (double)(leaf_cum[0] + leaf_cum[1]) * 64.0 * 8.0);
+                         (double)(leaf_cum[0] + leaf_cum[1]) * 64.0 * 8.0, leaf_cum[2], leaf_cum[3], leaf_cum[4]);
         }
     }
     total_children = (int64_t)tot[0];

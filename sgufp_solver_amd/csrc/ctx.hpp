@@ -261,7 +261,7 @@ struct sgufp_ctx {
     int32_t *d_pkind = nullptr, *d_P = nullptr, *d_nxh = nullptr, *d_pstop = nullptr, *d_nxlist = nullptr;
     // open-leaf compaction of the exact leaf passes (SGUFP_LEAF_SPLIT cut blocks in phase A; 0: off)
     int leaf_split = 16;
-    unsigned long long leaf_cum[2] = {0, 0};   // SGUFP_EXACT_STATS: leaf pass-blocks, staged row-blocks (summed)
+    unsigned long long leaf_cum[5] = {0, 0, 0, 0, 0};   // SGUFP_EXACT_STATS: leaf pass-blocks, staged row-blocks (summed)
     int32_t *d_open_cnt = nullptr, *d_open_list = nullptr;
     double *d_G = nullptr;
     unsigned long long *d_MS = nullptr;

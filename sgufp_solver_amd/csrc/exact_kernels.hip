@@ -269,6 +269,9 @@ __device__ double first_zero(const NetDev &net, const ExactIO &ex, LeafShared &S
 #ifndef SGUFP_LEAF_ROWMASK
 #define SGUFP_LEAF_ROWMASK 1   // stage only the rows the pass's leaves add (0: all rows, A/B)
 #endif
+#ifndef SGUFP_LEAF_BALANCE
+#define SGUFP_LEAF_BALANCE 1   // a pass's leaves split evenly over its eight waves
+#endif
 #ifndef SGUFP_LEAF_LASTREG
 #define SGUFP_LEAF_LASTREG 0   // 1: the last layer's rows of a block in registers (measured slower)
 #endif
@@ -356,9 +359,19 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
             const int k = e / us + 1, r = e % us;
             S.stab[e] = r == 0 ? -1 : slot_of(net, g, len, aligned, kb + k, r);
         }
-        // this wave's leaves: ancestry tables and alive mask
+        // this wave's leaves: ancestry tables and alive mask.  A pass's n leaves are split into
+        // eight runs of ceil(n / 8) consecutive leaves (not 16 for the first waves and none for the
+        // rest): a partial pass -- every record's last one, and phase B's open lists are mostly
+        // short -- keeps all waves busy, and each barrier waits for ceil(n / 8) leaves, not 16
+#if SGUFP_LEAF_BALANCE
+        const int npass = min(kLeafPass, (pb ? nopen : (int)lnn) - pass * kLeafPass);
+        const int per = (npass + kLeafWaves - 1) / kLeafWaves;
+        const int j0 = pass * kLeafPass + w * per;
+        const int cnt = uni(max(0, min(per, npass - w * per)));
+#else
         const int j0 = pass * kLeafPass + w * kLeavesPerWave;
         const int cnt = uni(max(0, min(kLeavesPerWave, (pb ? nopen : (int)lnn) - j0)));
+#endif
         // lane j's leaf (index among the record's leaves): consecutive in phase A, from the open
         // list in phase B (in the order phase A's passes appended them)
         const int lid = lane() < cnt ? (pb ? olist[j0 + lane()] : j0 + lane()) : 0;
@@ -499,6 +512,13 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
         };
         if (bfrom < bend) stage_load(bfrom);
 #endif
+#ifdef SGUFP_LEAF_CLOCKS
+        // diagnostics build: per wave the cycles of (staging + first barrier, leaf loop, the rest)
+        uint64_t ck[3] = {0, 0, 0}, ct = clock64();
+#define LEAF_CK(x) { const uint64_t c2 = clock64(); ck[x] += c2 - ct; ct = c2; }
+#else
+#define LEAF_CK(x)
+#endif
         for (int bb = bfrom; bb < bend; bb++) {
             bb_last = bb;
             nb_done = bb + 1;
@@ -510,6 +530,7 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
             for (int u = 0; u < kSU; u++)
                 if (srow[u] >= 0) S.C[srow[u]][lane()] = stg[u];
             __syncthreads();
+            LEAF_CK(0);
             if (bb + 1 < bend) stage_load(bb + 1);
 #else
             const GBL double *cm = scr ? ex.coefS : ex.coefO;
@@ -628,6 +649,7 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
                         atomicAdd(&ex.ctr[bb == 15 ? 14 : 13], (unsigned long long)__popc(alive & ~done));
                 }
             }
+            LEAF_CK(1);
             if (nx) S.vb[w][0][lane()] = ms;   // free until the next block's walks
             if (lane() == 0) S.flags[bb & 1][w] = ((done & alive) == alive) ? 1 : 0;
             __syncthreads();
@@ -644,6 +666,7 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
             // coefficients (the next block's are stored after it) and the flags alternate
             // buffers, so only the non-exact maxState (vb, rewritten by the next walks) waits here
             if (nx) __syncthreads();
+            LEAF_CK(2);
             if (all && !ph2) {
                 finished = true;
                 break;
@@ -671,6 +694,11 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
             atomicAdd(&ex.ctr[20], (unsigned long long)(SGUFP_LEAF_ROWMASK ? __popcll(rm) : E) * (unsigned long long)nbs_item);
             atomicAdd(&ex.ctr[21], (unsigned long long)nbs_item);
         }
+#ifdef SGUFP_LEAF_CLOCKS
+        if (lane() == 0)
+            for (int x = 0; x < 3; x++) atomicAdd(&ex.ctr[22 + x], (unsigned long long)ck[x]);
+#endif
+#undef LEAF_CK
         // terminal weights: min over the lanes
         uint32_t openb = 0;
 #pragma unroll

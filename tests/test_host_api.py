@@ -70,6 +70,15 @@ def test_container_is_race_free_under_tsan(tmp_path):
         pytest.skip("ThreadSanitizer toolchain unavailable: " + r.stderr[-200:])
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:exitcode=66")
     r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=120)
+    if "unexpected memory mapping" in r.stderr:
+        # the TSan runtime cannot map its shadow under this kernel's address-space randomisation
+        # (an environment limit, seen on the GPU boxes): run it without randomisation
+        setarch = shutil.which("setarch")
+        if setarch:
+            r = subprocess.run([setarch, os.uname().machine, "-R", exe], capture_output=True, text=True, env=env,
+                               timeout=120)
+        if "unexpected memory mapping" in r.stderr:
+            pytest.skip("ThreadSanitizer cannot map its shadow memory here: " + r.stderr[-200:])
     assert "ThreadSanitizer" not in r.stderr, r.stderr[-2000:]
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr[-500:])
     assert "cuts 8000 (expected 8000)" in r.stdout
