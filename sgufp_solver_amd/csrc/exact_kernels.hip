@@ -272,6 +272,9 @@ __device__ double first_zero(const NetDev &net, const ExactIO &ex, LeafShared &S
 #ifndef SGUFP_LEAF_BALANCE
 #define SGUFP_LEAF_BALANCE 1   // a pass's leaves split evenly over its eight waves
 #endif
+#ifndef SGUFP_LEAF_FAST
+#define SGUFP_LEAF_FAST 0   // 1: exact entries with lazy walks, mask tests, row offsets (measured: no gain)
+#endif
 #ifndef SGUFP_LEAF_LASTREG
 #define SGUFP_LEAF_LASTREG 0   // 1: the last layer's rows of a block in registers (measured slower)
 #endif
@@ -441,6 +444,14 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
             const uint32_t row = !(b & 128u) ? kRowDead : (r ? (uint32_t)((T - 2) * us) + r : kRowNoAdd);
             lp = row | (uint32_t)S.lw[w].dv[lane()] << 8;
         }
+#if SGUFP_LEAF_FAST
+        // exact entries' leaf loop (below): per pass, wave-uniform masks of the leaves that start a
+        // walk (a new parent) and of the leaves whose last arc adds nothing (dead in-arc, -1
+        // decision), and per leaf the byte offset of its coefficient row in S.C
+        const uint32_t walkm = uni((uint32_t)__ballot(lane() < cnt && (lane() == 0 || (int)(lp >> 8) < T - 1)));
+        const uint32_t specm = uni((uint32_t)__ballot(lane() < cnt && (lp & 0x7Fu) >= kRowDead));
+        const uint32_t lpo = (lp & 0x7Fu) < kRowDead ? (lp & 0x7Fu) * (uint32_t)(kWave * sizeof(double)) : 0u;
+#endif
         double m[kLeavesPerWave];
 #pragma unroll
         for (int j = 0; j < kLeavesPerWave; j++) m[j] = EDMAX;
@@ -565,6 +576,74 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
                 const uint32_t open = uni(alive & ~done);
                 const uint32_t need = uni(nx ? alive : open);
                 double par = root;
+#if SGUFP_LEAF_FAST
+                if constexpr (!NX) {
+                    // exact entries: walks only for open leaves (a skipped leaf's walk is owed to the
+                    // next open one: it starts at the shallowest first-differing layer since the last
+                    // walk, `pend`), scalar-branch tests on the masks, the row read at a precomputed
+                    // offset.  The same adds in the same order as the general loop below.
+                    const LDS char *cbase = (const LDS char *)&S.C[0][lane()];
+                    int pend = T - 1;
+#if SGUFP_LEAF_FAST == 2
+                    // pairs of leaves: both coefficient reads are issued before either leaf's walk or
+                    // add (they do not depend on the parent's value), one LDS round trip per pair
+                    static_assert(kLeavesPerWave % 2 == 0, "leaf pairs");
+#pragma unroll
+                    for (int jp = 0; jp < kLeavesPerWave; jp += 2) {
+                        const uint32_t o2 = (open >> jp) & 3u;
+                        if (!o2 && !((walkm >> jp) & 3u)) continue;
+                        double c2[2] = {0.0, 0.0};
+#pragma unroll
+                        for (int q = 0; q < 2; q++)
+                            if (((o2 >> q) & 1u) && !((specm >> (jp + q)) & 1u))
+                                c2[q] = *(const LDS double *)(cbase + (uint32_t)__builtin_amdgcn_readlane((int)lpo, jp + q));
+#pragma unroll
+                        for (int q = 0; q < 2; q++) {
+                            const int j = jp + q;
+                            if ((o2 >> q) & 1u) {
+                                if (((walkm >> j) & 1u) || pend < T - 1) {
+                                    const int dj = j == 0 ? 1 : (int)((uint32_t)__builtin_amdgcn_readlane((int)lp, j) >> 8);
+                                    par = walk_down(S, w, j, min(pend, dj), T, us, root, ilo, ihi);
+                                    pend = T - 1;
+                                }
+                                double v;
+                                if ((specm >> j) & 1u)
+                                    v = ((uint32_t)__builtin_amdgcn_readlane((int)lp, j) & 0x7Fu) == kRowDead ? EDMIN : par;
+                                else
+                                    v = par + c2[q];
+                                m[j] = vmin64(m[j], v);
+                            } else if ((walkm >> j) & 1u) {
+                                const int dj = j == 0 ? 1 : (int)((uint32_t)__builtin_amdgcn_readlane((int)lp, j) >> 8);
+                                pend = min(pend, dj);
+                            }
+                        }
+                    }
+                    if (false)
+#endif
+#pragma unroll
+                    for (int j = 0; j < kLeavesPerWave; j++) {
+                        if ((open >> j) & 1u) {
+                            if (((walkm >> j) & 1u) || pend < T - 1) {
+                                const int dj = j == 0 ? 1 : (int)((uint32_t)__builtin_amdgcn_readlane((int)lp, j) >> 8);
+                                par = walk_down(S, w, j, min(pend, dj), T, us, root, ilo, ihi);
+                                pend = T - 1;
+                            }
+                            double v;
+                            if ((specm >> j) & 1u) {
+                                v = ((uint32_t)__builtin_amdgcn_readlane((int)lp, j) & 0x7Fu) == kRowDead ? EDMIN : par;
+                            } else {
+                                const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)lpo, j);
+                                v = par + *(const LDS double *)(cbase + off);
+                            }
+                            m[j] = vmin64(m[j], v);
+                        } else if ((walkm >> j) & 1u) {
+                            const int dj = j == 0 ? 1 : (int)((uint32_t)__builtin_amdgcn_readlane((int)lp, j) >> 8);
+                            pend = min(pend, dj);
+                        }
+                    }
+                } else
+#endif
+                {
 #if SGUFP_LEAF_REGS
                 // ancestor values in registers (anc[k] = local layer k): a leaf recomputes the
                 // levels from its first ancestor that differs from the previous leaf's (dv), the
@@ -637,6 +716,7 @@ __global__ void __launch_bounds__(kLeafWaves * kWave, SGUFP_LEAF_MIN_WAVES) k_ex
                             }
                         }
                     }
+                }
                 }
                 // every fourth block (and the last): leaves some lane already took to <= optimalLB
                 if (!nx && ((bb & 3) == 3 || bb == nlim - 1)) {

@@ -117,13 +117,15 @@ def test_cpp_ddsolver_matches_python_driver_at_scale():
     inst.lb[:] = 0
     net = os.path.join(tempfile.mkdtemp(prefix="sgufp_host_"), "net.txt")
     inst.write(net)
-    cpp = _cpp_search(net, 64, 0, 1024, 0, 2, 30)
-    s = DDSolver(net, max_batch=1024, verbose=False, restricted_width=64, round_iters=2, stop_rounds=30)
+    # unseeded: the dive reaches exact leaves (subproblems, cuts, refinement) within the rounds
+    # (seeded by the width-64 heuristic, 30 rounds of this search stayed above the exact layers)
+    cpp = _cpp_search(net, 0, 0, 1024, 0, 2, 60)
+    s = DDSolver(net, max_batch=1024, verbose=False, restricted_width=0, round_iters=2, stop_rounds=60)
     z = s.start_solver(DOUBLE_MIN)
     pool = [s.eng.cuts_count(1), s.eng.cuts_count(0)]
     s.eng.close()
-    assert cpp["rounds"] == s.rounds == 30
-    assert cpp["heuristic"] == s.heuristic_incumbent
+    assert cpp["rounds"] == s.rounds == 60
+    assert cpp["heuristic"] == (DOUBLE_MIN if s.heuristic_incumbent is None else s.heuristic_incumbent)
     assert cpp["incumbent"] == z
     assert cpp["counters"] == {k: int(v) for k, v in s.counters.items()}, (cpp["counters"], s.counters)
     assert cpp["pool"] == pool
