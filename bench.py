@@ -67,7 +67,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-sample", type=int, default=2048)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--profile-tag", default="r05")
+    ap.add_argument("--profile-tag", default="r06")
     ap.add_argument("--sub-paths", type=int, default=32, help="subproblem leg: random full-matching paths (0: skip)")
     ap.add_argument("--cpu-sub-seconds", type=float, default=8.0)
     ap.add_argument("--c5-nodes", type=int, default=4096,
