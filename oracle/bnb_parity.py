@@ -492,7 +492,7 @@ def check_large_pool(cfg: str, seed: int, width: int, min_opt_cuts: int, batch: 
 
 def check_nx_survivors(cfg: str, seed: int, pool_sizes=(20000, 100000), per_pool: int = 8, batch: int = 1024,
                        round_seconds: float = 5.0, max_seconds: float = 300.0, device: int = 0, threads: int = 0,
-                       need_rounds: int = 12, keep_lb: bool = False, round_iters: int = 2):
+                       need_rounds: int = 12, keep_lb: bool = False, round_iters: int = 4):
     """The survivor path of the non-exact cut-parallel phase at the pool sizes the timed B&B
     legs reach.  The UNSEEDED search of ``cfg`` (no incumbent: nothing is pruned by a bound, so
     the non-exact records of a round survive every cut and take the whole phase: k_nx_dag per
@@ -512,7 +512,7 @@ def check_nx_survivors(cfg: str, seed: int, pool_sizes=(20000, 100000), per_pool
     incumbent (DOUBLE_MIN, device and reference alike: every record survives every cut) and the
     phase's survivors among them are compared.  ``round_iters`` caps the refinement iterations
     per round (sgufp_bnb_set_limits) so that the pool passes each size gradually instead of in
-    one round of uncapped loops."""
+    one round of uncapped loops; the survivors compared are those with the smallest DDs."""
     import time
     from sgufp_solver_amd import instance
     from sgufp_solver_amd.pools import DOUBLE_MAX, DOUBLE_MIN, NodeRecord
@@ -562,8 +562,9 @@ def check_nx_survivors(cfg: str, seed: int, pool_sizes=(20000, 100000), per_pool
         routes_e = eng.routes()
         surv = [k for k, g in enumerate(got_e)
                 if routes_e[k] == E.ROUTE_NX_PHASE and g.status == E.SUCCESS and not g.exact and g.children]
-        step = max(1, len(surv) // per_pool)
-        pick = surv[::step][:per_pool]
+        # the per_pool survivors with the smallest DDs (the reference sweeps each one's DD once per
+        # cut on one host thread: minutes per record at 10^5 cuts for the largest)
+        pick = sorted(sorted(surv, key=lambda k: (got_e[k].dd_nodes, k))[:per_pool])
         pool_path = os.path.join(work, f"pool_{target}.bin")
         total = write_pool_bin(pool_path, eng)
         t1 = time.perf_counter()
